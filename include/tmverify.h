@@ -1,0 +1,105 @@
+/*
+ * tmverify.h — C-ABI of the MI355X signature-verification engine
+ * (libtmgpu.so).  Plain pointers and sizes only; no torch or HIP types.
+ *
+ * This is the L0 replacement behind Tendermint's crypto.BatchVerifier
+ * (crypto/crypto.go:66-76).  Each entry point names the reference interface
+ * it replaces; INTEGRATION.md shows the cgo binding a maintainer adds to
+ * crypto/ed25519, crypto/sr25519 and crypto/batch.
+ *
+ * Packed batch layout (shared by every batch entry point):
+ *   pk      n x 32 bytes, entry i at pk + 32*i
+ *   sig     n x 64 bytes, entry i at sig + 64*i  (R || S)
+ *   msg     concatenated messages
+ *   msg_off n+1 offsets into msg; message i = msg[msg_off[i] .. msg_off[i+1])
+ *
+ * Return codes of the batch entry points:
+ *   TMV_ALL_VALID (1)   n > 0 and every entry verified
+ *   TMV_NOT_ALL   (0)   some entry failed, or n == 0 (voi: an empty batch
+ *                       verifies false)
+ *   < 0                 infrastructure error (no device, allocation, launch);
+ *                       the validity vector is then unspecified and the
+ *                       caller must not treat any entry as verified.
+ */
+#ifndef TMVERIFY_H
+#define TMVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMV_ALL_VALID 1
+#define TMV_NOT_ALL 0
+#define TMV_ERR_ARG (-1)
+#define TMV_ERR_NO_DEVICE (-2)
+#define TMV_ERR_NOMEM (-3)
+#define TMV_ERR_LAUNCH (-4)
+
+/* Per-entry sr25519 status (tmv_sr25519_verify_batch, tmv_verify_mixed_batch):
+ *   1 valid, 0 invalid, TMV_SR_ADDERR_* = BatchVerifier.Add would have
+ *   returned an error (crypto/sr25519/batch.go:30-37). */
+#define TMV_SR_ADDERR_PUBKEY (-1)
+#define TMV_SR_ADDERR_SIG (-2)
+
+/* Key kinds for tmv_verify_mixed_batch (crypto/batch/batch.go:11-21). */
+#define TMV_KIND_ED25519 0
+#define TMV_KIND_SR25519 1
+
+typedef struct tmv_ctx tmv_ctx;
+
+/* Open a context on the GPUs selected by device_mask (bit i = HIP device i;
+ * 0 = all visible devices).  Builds the per-device base-point tables.
+ * Returns NULL on failure (tmv_last_error() says why). */
+tmv_ctx *tmv_open(uint32_t device_mask);
+void tmv_close(tmv_ctx *ctx);
+int tmv_num_devices(const tmv_ctx *ctx);
+const char *tmv_last_error(void);
+const char *tmv_version(void);
+
+/* ed25519 batch verification with ZIP-215 semantics.
+ * Replaces: crypto/ed25519/ed25519.go:231-233 BatchVerifier.Verify (after the
+ * Adds of :209-229 have been collected into the packed arrays; the Go-side
+ * Add keeps its type/length checks and error strings).
+ * Multi-device contexts shard the batch by contiguous index ranges.
+ * valid_out[i] = 1/0 in Add order. */
+int tmv_ed25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                             const uint32_t *msg_off, uint32_t n, uint8_t *valid_out);
+
+/* Single ed25519 verification.
+ * Replaces: crypto/ed25519/ed25519.go:173-180 PubKey.VerifySignature
+ * (returns 0 when sig_len != 64, as the reference does).  Returns 1/0 or <0. */
+int tmv_ed25519_verify(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *msg, size_t msg_len,
+                       const uint8_t *sig, size_t sig_len);
+
+/* sr25519 batch verification (Schnorrkel, empty signing context).
+ * Replaces: crypto/sr25519/batch.go:23-47 Add + Verify.  status_out[i] is
+ * 1 / 0 / TMV_SR_ADDERR_*; the return value is TMV_ALL_VALID only if every
+ * status is 1. */
+int tmv_sr25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                             const uint32_t *msg_off, uint32_t n, int8_t *status_out);
+
+/* Mixed ed25519 + sr25519 batch in one launch; kind[i] = TMV_KIND_*.
+ * status_out as for sr25519 (ed25519 entries are 1/0). */
+int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
+                           const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out);
+
+/* Device-resident variants: every pointer is device memory on HIP device
+ * `device` (inputs already in HBM), `stream` is a hipStream_t (NULL = the
+ * context's own stream for that device).  Asynchronous: the call enqueues the
+ * kernel and returns TMV_NOT_ALL immediately (the verdict is in d_valid once
+ * the stream is synchronised), or <0 on a launch error.  Used by the
+ * multi-GPU sharded path (one process per GPU) and by bench.py. */
+int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_pk, const uint8_t *d_sig,
+                                    const uint8_t *d_msg, const uint32_t *d_msg_off, uint32_t n,
+                                    uint8_t *d_valid, void *stream);
+int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kind, const uint8_t *d_pk,
+                                  const uint8_t *d_sig, const uint8_t *d_msg, const uint32_t *d_msg_off,
+                                  uint32_t n, int8_t *d_status, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMVERIFY_H */

@@ -1,0 +1,112 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes loader for the C oracle (oracle/_build/liboracle.so).
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as
+the *checker*.  The product path (tendermint_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.oracle_ed25519_verify.argtypes = [u8p, u8p, ctypes.c_size_t, u8p]
+        L.oracle_ed25519_verify_batch.argtypes = [u8p, u8p, u8p, ctypes.POINTER(ctypes.c_uint32),
+                                                  ctypes.c_size_t, u8p, ctypes.c_int]
+        L.oracle_sr25519_status_batch.argtypes = [u8p, u8p, u8p, ctypes.POINTER(ctypes.c_uint32),
+                                                  ctypes.c_size_t, ctypes.POINTER(ctypes.c_int8), ctypes.c_int]
+        L.oracle_sr25519_verify.argtypes = [u8p, u8p, ctypes.c_size_t, u8p]
+        L.oracle_sr25519_add_check.argtypes = [u8p, u8p]
+        L.oracle_sha512.argtypes = [u8p, ctypes.c_size_t, u8p]
+        L.oracle_sc_reduce64.argtypes = [u8p, u8p]
+        L.oracle_merlin_test.argtypes = [u8p]
+        L.oracle_ge_decode_lax.argtypes = [u8p, u8p, u8p]
+        L.oracle_ristretto_decode.argtypes = [u8p, u8p, u8p]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray, t=ctypes.c_uint8):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _buf(b: bytes):
+    a = np.frombuffer(b, dtype=np.uint8).copy() if len(b) else np.zeros(1, np.uint8)
+    return a
+
+
+def ed25519_verify(pk: bytes, msg: bytes, sig: bytes) -> bool:
+    if len(sig) != 64 or len(pk) != 32:
+        return False
+    a, m, s = _buf(pk), _buf(msg), _buf(sig)
+    return bool(lib().oracle_ed25519_verify(_p(a), _p(m), len(msg), _p(s)))
+
+
+def ed25519_verify_packed(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, off: np.ndarray,
+                          threads: int = 1):
+    """Packed layout (see include/tmverify.h).  Returns (ok, uint8 vector)."""
+    n = len(off) - 1
+    out = np.zeros(max(n, 1), np.uint8)
+    msg = msg if len(msg) else np.zeros(1, np.uint8)
+    ok = lib().oracle_ed25519_verify_batch(_p(pk), _p(sig), _p(msg), _p(off, ctypes.c_uint32), n,
+                                           _p(out), threads)
+    return bool(ok), out[:n]
+
+
+def sr25519_status_packed(pk, sig, msg, off, threads: int = 1) -> np.ndarray:
+    n = len(off) - 1
+    out = np.zeros(max(n, 1), np.int8)
+    msg = msg if len(msg) else np.zeros(1, np.uint8)
+    lib().oracle_sr25519_status_batch(_p(pk), _p(sig), _p(msg), _p(off, ctypes.c_uint32), n,
+                                      _p(out, ctypes.c_int8), threads)
+    return out[:n]
+
+
+def sr25519_verify(pk: bytes, msg: bytes, sig: bytes) -> bool:
+    if len(sig) != 64 or len(pk) != 32:
+        return False
+    a, m, s = _buf(pk), _buf(msg), _buf(sig)
+    return bool(lib().oracle_sr25519_verify(_p(a), _p(m), len(msg), _p(s)))
+
+
+def sha512(m: bytes) -> bytes:
+    out = np.zeros(64, np.uint8)
+    lib().oracle_sha512(_p(_buf(m)), len(m), _p(out))
+    return out.tobytes()
+
+
+def merlin_test_vector() -> bytes:
+    out = np.zeros(32, np.uint8)
+    lib().oracle_merlin_test(_p(out))
+    return out.tobytes()
+
+
+def pack(entries):
+    """[(pk, msg, sig)] -> (pk[n*32], sig[n*64], msg[], off[n+1]) numpy arrays."""
+    n = len(entries)
+    pk = np.frombuffer(b"".join(e[0] for e in entries), np.uint8).copy() if n else np.zeros(0, np.uint8)
+    sig = np.frombuffer(b"".join(e[2] for e in entries), np.uint8).copy() if n else np.zeros(0, np.uint8)
+    msgs = [e[1] for e in entries]
+    off = np.zeros(n + 1, np.uint32)
+    if n:
+        off[1:] = np.cumsum([len(m) for m in msgs])
+    msg = np.frombuffer(b"".join(msgs), np.uint8).copy() if sum(len(m) for m in msgs) else np.zeros(0, np.uint8)
+    return pk, sig, msg, off

@@ -1,0 +1,189 @@
+"""ctypes binding of libtmgpu.so (include/tmverify.h).
+
+Loads the in-tree build (tendermint_amd/_build/libtmgpu.so).  Fails loudly
+when it is missing — there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libtmgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tmverify.h")
+
+TMV_ALL_VALID = 1
+TMV_NOT_ALL = 0
+TMV_ERR_ARG = -1
+TMV_ERR_NO_DEVICE = -2
+TMV_ERR_NOMEM = -3
+TMV_ERR_LAUNCH = -4
+TMV_SR_ADDERR_PUBKEY = -1
+TMV_SR_ADDERR_SIG = -2
+TMV_KIND_ED25519 = 0
+TMV_KIND_SR25519 = 1
+
+# Every symbol include/tmverify.h declares (checked by tests/test_boundary.py).
+EXPORTS = [
+    "tmv_open", "tmv_close", "tmv_num_devices", "tmv_last_error", "tmv_version",
+    "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
+    "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
+]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def build() -> str:
+    """Compile libtmgpu.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc")], check=True)
+    return LIB_PATH
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """Load libtmgpu.so; raises NativeError if it has not been built."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"{LIB_PATH} missing: run tendermint_amd._native.build() "
+                              "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        i8p = ctypes.POINTER(ctypes.c_int8)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        vp = ctypes.c_void_p
+        L.tmv_open.restype = vp
+        L.tmv_open.argtypes = [ctypes.c_uint32]
+        L.tmv_close.argtypes = [vp]
+        L.tmv_num_devices.argtypes = [vp]
+        L.tmv_last_error.restype = ctypes.c_char_p
+        L.tmv_version.restype = ctypes.c_char_p
+        L.tmv_ed25519_verify_batch.argtypes = [vp, u8p, u8p, u8p, u32p, ctypes.c_uint32, u8p]
+        L.tmv_ed25519_verify.argtypes = [vp, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        L.tmv_sr25519_verify_batch.argtypes = [vp, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
+        L.tmv_verify_mixed_batch.argtypes = [vp, u8p, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
+        L.tmv_ed25519_verify_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
+        L.tmv_verify_mixed_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    return lib().tmv_last_error().decode(errors="replace")
+
+
+def _p(a: np.ndarray, t=ctypes.c_uint8):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+class Context:
+    """A tmv_ctx on the devices in ``device_mask`` (0 = all visible)."""
+
+    def __init__(self, device_mask: int = 0):
+        self._lib = lib()
+        self._h = self._lib.tmv_open(device_mask)
+        if not self._h:
+            raise NativeError("tmv_open failed: " + last_error())
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            self._lib.tmv_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def num_devices(self) -> int:
+        return self._lib.tmv_num_devices(self._h)
+
+    @staticmethod
+    def _check(rc: int, what: str) -> int:
+        if rc < 0:
+            raise NativeError(f"{what} failed ({rc}): {last_error()}")
+        return rc
+
+    def ed25519_verify_batch(self, pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, off: np.ndarray):
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), np.uint8)
+        msg = msg if len(msg) else np.zeros(1, np.uint8)
+        pk = pk if len(pk) else np.zeros(1, np.uint8)
+        sig = sig if len(sig) else np.zeros(1, np.uint8)
+        rc = self._check(self._lib.tmv_ed25519_verify_batch(self._h, _p(pk), _p(sig), _p(msg),
+                                                            _p(off, ctypes.c_uint32), n, _p(out)),
+                         "tmv_ed25519_verify_batch")
+        return rc == TMV_ALL_VALID, out[:n]
+
+    def ed25519_verify(self, pk: bytes, msg: bytes, sig: bytes) -> bool:
+        a = np.frombuffer(pk, np.uint8).copy()
+        m = np.frombuffer(msg + b"\0", np.uint8).copy()
+        s = np.frombuffer(sig + b"\0", np.uint8).copy()
+        rc = self._check(self._lib.tmv_ed25519_verify(self._h, _p(a), _p(m), len(msg), _p(s), len(sig)),
+                         "tmv_ed25519_verify")
+        return rc == 1
+
+    def sr25519_verify_batch(self, pk, sig, msg, off):
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), np.int8)
+        msg = msg if len(msg) else np.zeros(1, np.uint8)
+        pk = pk if len(pk) else np.zeros(1, np.uint8)
+        sig = sig if len(sig) else np.zeros(1, np.uint8)
+        rc = self._check(self._lib.tmv_sr25519_verify_batch(self._h, _p(pk), _p(sig), _p(msg),
+                                                            _p(off, ctypes.c_uint32), n,
+                                                            _p(out, ctypes.c_int8)),
+                         "tmv_sr25519_verify_batch")
+        return rc == TMV_ALL_VALID, out[:n]
+
+    def verify_mixed_batch(self, kind, pk, sig, msg, off):
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), np.int8)
+        msg = msg if len(msg) else np.zeros(1, np.uint8)
+        kind = kind if len(kind) else np.zeros(1, np.uint8)
+        pk = pk if len(pk) else np.zeros(1, np.uint8)
+        sig = sig if len(sig) else np.zeros(1, np.uint8)
+        rc = self._check(self._lib.tmv_verify_mixed_batch(self._h, _p(kind), _p(pk), _p(sig), _p(msg),
+                                                          _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
+                         "tmv_verify_mixed_batch")
+        return rc == TMV_ALL_VALID, out[:n]
+
+    def ed25519_verify_batch_device(self, device: int, d_pk: int, d_sig: int, d_msg: int, d_off: int, n: int,
+                                    d_valid: int, stream: int = 0) -> None:
+        self._check(self._lib.tmv_ed25519_verify_batch_device(self._h, device, d_pk, d_sig, d_msg, d_off, n,
+                                                              d_valid, stream or None),
+                    "tmv_ed25519_verify_batch_device")
+
+    def verify_mixed_batch_device(self, device: int, d_kind: int, d_pk: int, d_sig: int, d_msg: int, d_off: int,
+                                  n: int, d_status: int, stream: int = 0) -> None:
+        self._check(self._lib.tmv_verify_mixed_batch_device(self._h, device, d_kind, d_pk, d_sig, d_msg, d_off, n,
+                                                            d_status, stream or None),
+                    "tmv_verify_mixed_batch_device")
+
+
+_default_ctx = None
+_ctx_lock = threading.Lock()
+
+
+def default_context() -> Context:
+    """Process-wide context on all visible GPUs (like voi's global verifier)."""
+    global _default_ctx
+    with _ctx_lock:
+        if _default_ctx is None:
+            _default_ctx = Context(0)
+        return _default_ctx

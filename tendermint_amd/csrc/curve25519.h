@@ -1,0 +1,575 @@
+// GF(2^255-19) field, edwards25519 group and scalar-mod-l arithmetic for the
+// MI355X verification kernels.  Compiled for gfx950 (device) and, unchanged,
+// for the host (the runtime precomputes the base-point table with it and the
+// CPU test tests/native/test_arith.cpp runs it with limb-bound assertions).
+//
+// Replaces the field/point/scalar internals of the absent third-party module
+// curve25519-voi (go.mod:22) that sit behind crypto/ed25519/ed25519.go:173-233
+// and crypto/sr25519/{pubkey.go:49-62,batch.go:23-47}.
+//
+// Representation: radix 2^25.5 — ten signed 32-bit limbs alternating 26/25
+// bits.  One field multiply = 100 32x32->64 multiply-adds (v_mad_i64_i32 on
+// CDNA4's VALU; this is integer work, MFMA does not apply).
+//
+// Limb-magnitude discipline ("level"): every mul/sq output is carried
+// (|limb| <= 2^25 on 26-bit positions, 2^24 on 25-bit positions, level 1).
+// Sums/differences add levels.  Multiply inputs must be level <= 3 so that
+// 19*g fits int32 and the 64-bit column sums cannot overflow.  Each formula
+// below is annotated with the level of its intermediates; TMV_BOUNDS_CHECK
+// (host only) asserts it.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define TMV_HD __host__ __device__ __forceinline__
+#define TMV_DEV __device__ __forceinline__
+#else
+#define TMV_HD inline
+#define TMV_DEV inline
+#endif
+
+#ifdef TMV_BOUNDS_CHECK
+#include <cassert>
+#include <cstdlib>
+#define TMV_ASSERT_LEVEL(f, lvl)                                               \
+  do {                                                                         \
+    for (int _i = 0; _i < 10; _i++) {                                          \
+      int64_t _b = (int64_t)(lvl) << ((_i & 1) ? 24 : 25);                     \
+      int64_t _x = (f).v[_i];                                                  \
+      if (_x > _b + ((int64_t)1 << 20) || _x < -_b - ((int64_t)1 << 20)) {     \
+        assert(!"field limb exceeds level bound");                             \
+      }                                                                        \
+    }                                                                          \
+  } while (0)
+#else
+#define TMV_ASSERT_LEVEL(f, lvl) do { } while (0)
+#endif
+
+namespace tmv {
+
+struct fe { int32_t v[10]; };
+
+TMV_HD void fe_zero(fe &h) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = 0;
+}
+TMV_HD void fe_one(fe &h) { fe_zero(h); h.v[0] = 1; }
+
+TMV_HD void fe_add(fe &h, const fe &f, const fe &g) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] + g.v[i];
+}
+TMV_HD void fe_sub(fe &h, const fe &f, const fe &g) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] - g.v[i];
+}
+TMV_HD void fe_neg(fe &h, const fe &f) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = -f.v[i];
+}
+// branch-free conditional move: h = b ? g : h
+TMV_HD void fe_cmov(fe &h, const fe &g, bool b) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = b ? g.v[i] : h.v[i];
+}
+
+// Carry a column-sum vector back to level 1.  Two interleaved chains
+// (0->1->2->3->4 and 4->5->...->9->0->1) for ILP.
+TMV_HD void fe_carry_wide(fe &h, int64_t c[10]) {
+  const int64_t R25 = (int64_t)1 << 25, R24 = (int64_t)1 << 24;
+  int64_t k;
+  k = (c[0] + R25) >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
+  k = (c[4] + R25) >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
+  k = (c[1] + R24) >> 25; c[2] += k; c[1] -= k * ((int64_t)1 << 25);
+  k = (c[5] + R24) >> 25; c[6] += k; c[5] -= k * ((int64_t)1 << 25);
+  k = (c[2] + R25) >> 26; c[3] += k; c[2] -= k * ((int64_t)1 << 26);
+  k = (c[6] + R25) >> 26; c[7] += k; c[6] -= k * ((int64_t)1 << 26);
+  k = (c[3] + R24) >> 25; c[4] += k; c[3] -= k * ((int64_t)1 << 25);
+  k = (c[7] + R24) >> 25; c[8] += k; c[7] -= k * ((int64_t)1 << 25);
+  k = (c[4] + R25) >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
+  k = (c[8] + R25) >> 26; c[9] += k; c[8] -= k * ((int64_t)1 << 26);
+  k = (c[9] + R24) >> 25; c[0] += k * 19; c[9] -= k * ((int64_t)1 << 25);
+  k = (c[0] + R25) >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)c[i];
+}
+
+// Re-carry any level <= 3 value to level 1.
+TMV_HD void fe_carry(fe &h, const fe &f) {
+  int64_t c[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) c[i] = f.v[i];
+  fe_carry_wide(h, c);
+}
+
+// h = f * g.  Column k collects f_i g_j with i+j == k, plus 19 f_i g_j for
+// i+j == k+10 (2^255 == 19).  Odd*odd limb products carry an extra factor 2
+// (25.5-bit radix).
+TMV_HD void fe_mul(fe &h, const fe &f, const fe &g) {
+  TMV_ASSERT_LEVEL(f, 3);
+  TMV_ASSERT_LEVEL(g, 3);
+  int32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g19[i] = 19 * g.v[i];
+    f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
+  }
+  int64_t c[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      if (i + j < 10) c[i + j] += (int64_t)a * g.v[j];
+      else            c[i + j - 10] += (int64_t)a * g19[j];
+    }
+  }
+  fe_carry_wide(h, c);
+}
+
+// h = f^2 (55 products via symmetry)
+TMV_HD void fe_sq(fe &h, const fe &f) {
+  TMV_ASSERT_LEVEL(f, 3);
+  int32_t f2[10], f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = 19 * f.v[i]; }
+  int64_t c[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      // f_i f_j appears twice for i != j; odd*odd carries another factor 2
+      const int oddodd = (i & 1) && (j & 1);
+      int32_t a = (i == j) ? f.v[i] : f2[i];
+      if (oddodd) a = 2 * a;
+      if (i + j < 10) c[i + j] += (int64_t)a * f.v[j];
+      else            c[i + j - 10] += (int64_t)a * f19[j];
+    }
+  }
+  fe_carry_wide(h, c);
+}
+
+// h = 2 f^2
+TMV_HD void fe_sq2(fe &h, const fe &f) {
+  fe t;
+  fe_sq(t, f);
+  fe_add(t, t, t);  // level 2
+  fe_carry(h, t);   // callers treat the result as level 1
+}
+
+TMV_HD void fe_sqn(fe &h, const fe &f, int n) {
+  fe_sq(h, f);
+  for (int i = 1; i < n; i++) fe_sq(h, h);
+}
+
+// Bit positions of the ten limbs.
+#define TMV_LIMB_POS {0, 26, 51, 77, 102, 128, 153, 179, 204, 230}
+
+// Load 255 bits (bit 255 ignored) from eight little-endian 32-bit words.
+// The value may be >= p (lax decoding accepts it); limbs are exact, level 1.
+TMV_HD void fe_from_words(fe &h, const uint32_t w[8]) {
+  const int pos[10] = TMV_LIMB_POS;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int p = pos[i], width = (i & 1) ? 25 : 26;
+    const int wi = p >> 5, sh = p & 31;
+    uint64_t x = w[wi];
+    if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << 32;
+    uint32_t limb = (uint32_t)(x >> sh) & ((1u << width) - 1);
+    h.v[i] = (int32_t)limb;
+  }
+  // limb 9 covers bits 230..254; bit 255 was masked by width (25 bits)
+}
+
+TMV_HD void fe_from_bytes(fe &h, const uint8_t s[32]) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    w[i] = (uint32_t)s[4 * i] | ((uint32_t)s[4 * i + 1] << 8) |
+           ((uint32_t)s[4 * i + 2] << 16) | ((uint32_t)s[4 * i + 3] << 24);
+  fe_from_words(h, w);
+}
+
+// Canonical (fully reduced) little-endian words.  Input level <= 3.
+TMV_HD void fe_to_words(uint32_t w[8], const fe &f) {
+  int64_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = f.v[i];
+  // bring to level 1 first (handles level-3 inputs)
+  {
+    fe t;
+    fe_carry_wide(t, h);
+#pragma unroll
+    for (int i = 0; i < 10; i++) h[i] = t.v[i];
+  }
+  // q = floor((h + 19) / 2^255) in {0, 1} (h in (-2^255, 2^256) after carry)
+  int64_t q = (19 * h[9] + ((int64_t)1 << 24)) >> 25;
+#pragma unroll
+  for (int i = 0; i < 10; i++) q = (h[i] + q) >> ((i & 1) ? 25 : 26);
+  h[0] += 19 * q;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int sh = (i & 1) ? 25 : 26;
+    int64_t k = h[i] >> sh;
+    h[i + 1] += k;
+    h[i] -= k * ((int64_t)1 << sh);
+  }
+  h[9] -= (h[9] >> 25) * ((int64_t)1 << 25);
+  // pack: limbs are now in [0, 2^width)
+  const int pos[10] = TMV_LIMB_POS;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint64_t limb = (uint64_t)h[i];
+    const int wi = pos[i] >> 5, sh = pos[i] & 31;
+    w[wi] |= (uint32_t)(limb << sh);
+    if (wi + 1 < 8 && sh) w[wi + 1] |= (uint32_t)(limb >> (32 - sh));
+  }
+}
+
+TMV_HD bool fe_is_zero(const fe &f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r |= w[i];
+  return r == 0;
+}
+TMV_HD bool fe_is_negative(const fe &f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  return w[0] & 1;
+}
+TMV_HD bool fe_eq(const fe &a, const fe &b) {
+  fe d;
+  fe_sub(d, a, b);
+  return fe_is_zero(d);
+}
+
+// h = z^((p-5)/8) = z^(2^252 - 3)
+TMV_HD void fe_pow22523(fe &h, const fe &z) {
+  fe t0, t1, t2;
+  fe_sq(t0, z);            // 2
+  fe_sqn(t1, t0, 2);       // 8
+  fe_mul(t1, z, t1);       // 9
+  fe_mul(t0, t0, t1);      // 11
+  fe_sq(t0, t0);           // 22
+  fe_mul(t0, t1, t0);      // 2^5 - 1
+  fe_sqn(t1, t0, 5);
+  fe_mul(t0, t1, t0);      // 2^10 - 1
+  fe_sqn(t1, t0, 10);
+  fe_mul(t1, t1, t0);      // 2^20 - 1
+  fe_sqn(t2, t1, 20);
+  fe_mul(t1, t2, t1);      // 2^40 - 1
+  fe_sqn(t1, t1, 10);
+  fe_mul(t0, t1, t0);      // 2^50 - 1
+  fe_sqn(t1, t0, 50);
+  fe_mul(t1, t1, t0);      // 2^100 - 1
+  fe_sqn(t2, t1, 100);
+  fe_mul(t1, t2, t1);      // 2^200 - 1
+  fe_sqn(t1, t1, 50);
+  fe_mul(t0, t1, t0);      // 2^250 - 1
+  fe_sqn(t0, t0, 2);       // 2^252 - 4
+  fe_mul(h, t0, z);        // 2^252 - 3
+}
+
+// h = z^(p-2) = z^-1
+TMV_HD void fe_invert(fe &h, const fe &z) {
+  fe t0, t1, t2, t3;
+  fe_sq(t0, z);            // 2
+  fe_sqn(t1, t0, 2);       // 8
+  fe_mul(t1, z, t1);       // 9
+  fe_mul(t0, t0, t1);      // 11
+  fe_sq(t2, t0);           // 22
+  fe_mul(t1, t1, t2);      // 2^5 - 1
+  fe_sqn(t2, t1, 5);
+  fe_mul(t1, t2, t1);      // 2^10 - 1
+  fe_sqn(t2, t1, 10);
+  fe_mul(t2, t2, t1);      // 2^20 - 1
+  fe_sqn(t3, t2, 20);
+  fe_mul(t2, t3, t2);      // 2^40 - 1
+  fe_sqn(t2, t2, 10);
+  fe_mul(t1, t2, t1);      // 2^50 - 1
+  fe_sqn(t2, t1, 50);
+  fe_mul(t2, t2, t1);      // 2^100 - 1
+  fe_sqn(t3, t2, 100);
+  fe_mul(t2, t3, t2);      // 2^200 - 1
+  fe_sqn(t2, t2, 50);
+  fe_mul(t1, t2, t1);      // 2^250 - 1
+  fe_sqn(t1, t1, 5);       // 2^255 - 32
+  fe_mul(h, t1, t0);       // 2^255 - 21
+}
+
+// ---------------------------------------------------------------- constants
+// Limb images (level 1) of the curve constants; derived in
+// tests/test_arith_constants.py from the integers they encode.
+struct consts {
+  static TMV_HD fe d()      { return fe{{-10913610, 13857413, -15372611, 6949391, 114729, -8787816, -6275908, -3247719, -18696448, -12055116}}; }
+  static TMV_HD fe d2()     { return fe{{-21827239, -5839606, -30745221, 13898782, 229458, 15978800, -12551817, -6495438, 29715968, 9444199}}; }
+  static TMV_HD fe sqrtm1() { return fe{{-32595792, -7943725, 9377950, 3500415, 12389472, -272473, -25146209, -2005654, 326686, 11406482}}; }
+  static TMV_HD fe invsqrt_a_minus_d() { return fe{{6111485, 4156064, -27798727, 12243468, -25904040, 120897, 20826367, -7060776, 6093568, -1986012}}; }
+};
+
+// ---------------------------------------------------------------- points
+// Extended twisted Edwards (a = -1): x = X/Z, y = Y/Z, xy = T/Z.
+struct ge_p2 { fe X, Y, Z; };
+struct ge_p3 { fe X, Y, Z, T; };
+struct ge_p1p1 { fe X, Y, Z, T; };            // completed: x = X/Z, y = Y/T
+struct ge_cached { fe YpX, YmX, Z, T2d; };
+struct ge_precomp { fe ypx, ymx, xy2d; };      // affine Niels form, Z = 1
+
+TMV_HD void ge_p3_identity(ge_p3 &h) { fe_zero(h.X); fe_one(h.Y); fe_one(h.Z); fe_zero(h.T); }
+TMV_HD void ge_precomp_identity(ge_precomp &h) { fe_one(h.ypx); fe_one(h.ymx); fe_zero(h.xy2d); }
+
+TMV_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+}
+TMV_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+}
+TMV_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
+
+TMV_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
+  fe_add(r.YpX, p.Y, p.X);            // level 2
+  fe_sub(r.YmX, p.Y, p.X);            // level 2
+  r.Z = p.Z;
+  fe_mul(r.T2d, p.T, consts::d2());
+}
+
+// dbl-2008-hwcd, a = -1; output is the negation of (E, H, G, F) on every
+// coordinate, which is the same projective point.
+TMV_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
+  fe XX, YY, ZZ2, S, AA;
+  fe_sq(XX, p.X);
+  fe_sq(YY, p.Y);
+  fe_sq2(ZZ2, p.Z);
+  fe_add(S, p.X, p.Y);                 // level <= 2
+  fe_sq(AA, S);
+  fe_add(r.Y, YY, XX);                 // 2
+  fe_sub(r.Z, YY, XX);                 // 2
+  fe_sub(r.X, AA, r.Y);                // 3
+  fe_sub(r.T, ZZ2, r.Z);               // 3
+}
+TMV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {
+  ge_p2 q;
+  ge_p3_to_p2(q, p);
+  ge_p2_dbl(r, q);
+}
+
+// add-2008-hwcd-3 (k = 2d): p + q
+TMV_HD void ge_add(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
+  fe a, b, c, dd, t;
+  fe_sub(t, p.Y, p.X); fe_mul(a, t, q.YmX);
+  fe_add(t, p.Y, p.X); fe_mul(b, t, q.YpX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(dd, p.Z, q.Z);
+  fe_add(dd, dd, dd);                  // 2
+  fe_sub(r.X, b, a);                   // 2  E
+  fe_add(r.Y, b, a);                   // 2  H
+  fe_add(r.Z, dd, c);                  // 3  G
+  fe_sub(r.T, dd, c);                  // 3  F
+}
+// p - q
+TMV_HD void ge_sub(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
+  fe a, b, c, dd, t;
+  fe_sub(t, p.Y, p.X); fe_mul(a, t, q.YpX);
+  fe_add(t, p.Y, p.X); fe_mul(b, t, q.YmX);
+  fe_mul(c, p.T, q.T2d);
+  fe_mul(dd, p.Z, q.Z);
+  fe_add(dd, dd, dd);
+  fe_sub(r.X, b, a);
+  fe_add(r.Y, b, a);
+  fe_sub(r.Z, dd, c);
+  fe_add(r.T, dd, c);
+}
+// mixed add with an affine Niels point (Z = 1)
+TMV_HD void ge_madd(ge_p1p1 &r, const ge_p3 &p, const ge_precomp &q) {
+  fe a, b, c, dd, t;
+  fe_sub(t, p.Y, p.X); fe_mul(a, t, q.ymx);
+  fe_add(t, p.Y, p.X); fe_mul(b, t, q.ypx);
+  fe_mul(c, p.T, q.xy2d);
+  fe_add(dd, p.Z, p.Z);                // 2
+  fe_sub(r.X, b, a);
+  fe_add(r.Y, b, a);
+  fe_add(r.Z, dd, c);
+  fe_sub(r.T, dd, c);
+}
+
+TMV_HD void ge_p3_neg(ge_p3 &r, const ge_p3 &p) {
+  fe_neg(r.X, p.X); r.Y = p.Y; r.Z = p.Z; fe_neg(r.T, p.T);
+}
+
+TMV_HD bool ge_p3_is_identity(const ge_p3 &p) {
+  return fe_is_zero(p.X) && fe_eq(p.Y, p.Z);
+}
+
+// Cofactored identity test: [8]p == O.
+TMV_HD bool ge_p3_is_small_order_or_identity_times8(const ge_p3 &p) {
+  ge_p1p1 t;
+  ge_p2 q;
+  ge_p3_dbl(t, p);
+  ge_p1p1_to_p2(q, t);
+  ge_p2_dbl(t, q);
+  ge_p1p1_to_p2(q, t);
+  ge_p2_dbl(t, q);
+  ge_p1p1_to_p2(q, t);
+  return fe_is_zero(q.X) && fe_eq(q.Y, q.Z);
+}
+
+// ZIP-215 lax decoding of an edwards25519 point (crypto/ed25519/ed25519.go:27-29
+// options): y is taken mod p (y >= p accepted), x recovered from
+// x^2 = (y^2-1)/(d y^2+1); non-square -> reject; x == 0 with sign bit 1 is
+// accepted ("negative zero").
+TMV_HD bool ge_decode_zip215(ge_p3 &h, const uint32_t w[8]) {
+  fe u, v, v3, vxx, chk, x, one;
+  fe_from_words(h.Y, w);
+  fe_carry(h.Y, h.Y);                  // exact limbs are level 2; bring to 1
+  fe_one(h.Z);
+  fe_one(one);
+  fe_sq(u, h.Y);
+  fe_mul(v, u, consts::d());
+  fe_sub(u, u, one);                   // u = y^2 - 1      (2)
+  fe_add(v, v, one);                   // v = d y^2 + 1    (2)
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);                   // v^3
+  fe_sq(x, v3);
+  fe_mul(x, x, v);                     // v^7
+  fe_mul(x, x, u);                     // u v^7
+  fe_pow22523(x, x);
+  fe_mul(x, x, v3);
+  fe_mul(x, x, u);                     // x = u v^3 (u v^7)^((p-5)/8)
+  fe_sq(vxx, x);
+  fe_mul(vxx, vxx, v);
+  fe_sub(chk, vxx, u);                 // 3
+  if (!fe_is_zero(chk)) {
+    fe_add(chk, vxx, u);
+    if (!fe_is_zero(chk)) return false;
+    fe_mul(x, x, consts::sqrtm1());
+  }
+  const bool sign = (w[7] >> 31) & 1;
+  if (fe_is_negative(x) != sign) fe_neg(x, x);
+  h.X = x;
+  fe_mul(h.T, h.X, h.Y);
+  return true;
+}
+
+// ---------------------------------------------------------------- scalars
+// l = 2^252 + 27742317777372353535851937790883648493, little-endian words.
+struct scl {
+  static TMV_HD uint32_t l(int i) {
+    const uint32_t L[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0u, 0u, 0u, 0x10000000u};
+    return L[i];
+  }
+  static TMV_HD uint32_t mu(int i) {  // floor(2^512 / l), 9 words
+    const uint32_t M[9] = {0x0a2c131bu, 0xed9ce5a3u, 0x086329a7u, 0x2106215du, 0xffffffebu,
+                           0xffffffffu, 0xffffffffu, 0xffffffffu, 0x0000000fu};
+    return M[i];
+  }
+};
+
+// s < l ?  (strict canonical scalar, ZIP-215 rule for S)
+TMV_HD bool sc_is_canonical(const uint32_t s[8]) {
+  for (int i = 7; i >= 0; i--) {
+    if (s[i] < scl::l(i)) return true;
+    if (s[i] > scl::l(i)) return false;
+  }
+  return false;
+}
+
+// r = x mod l for a 512-bit x (16 little-endian words); Barrett (HAC 14.42)
+// with b = 2^32, k = 8.
+TMV_HD void sc_reduce512(uint32_t r[8], const uint32_t x[16]) {
+  // q2 = floor(x / b^7) * mu ; only words 9..17 (q3) are needed, but the
+  // full product keeps the carries exact.
+  uint32_t q2[18];
+#pragma unroll
+  for (int i = 0; i < 18; i++) q2[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    uint64_t carry = 0;
+    const uint64_t a = x[7 + i];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      uint64_t t = a * scl::mu(j) + q2[i + j] + carry;
+      q2[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    q2[i + 9] = (uint32_t)carry;
+  }
+  // r2 = (q3 * l) mod b^9
+  uint32_t r2[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) r2[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    uint64_t carry = 0;
+    const uint64_t a = q2[9 + i];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (i + j >= 9) break;
+      uint64_t t = a * scl::l(j) + r2[i + j] + carry;
+      r2[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    if (i == 0) r2[8] = (uint32_t)carry;  // rows i >= 1 carry past word 8
+  }
+  // t = (x mod b^9) - r2 mod b^9
+  uint32_t t[9];
+  int64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    int64_t d = (int64_t)x[i] - r2[i] + borrow;
+    t[i] = (uint32_t)d;
+    borrow = d >> 32;  // 0 or -1
+  }
+  // at most two subtractions of l
+  for (int it = 0; it < 2; it++) {
+    bool ge = t[8] != 0;
+    if (!ge) {
+      ge = true;
+      for (int i = 7; i >= 0; i--) {
+        if (t[i] > scl::l(i)) { ge = true; break; }
+        if (t[i] < scl::l(i)) { ge = false; break; }
+      }
+    }
+    if (ge) {
+      int64_t b = 0;
+#pragma unroll
+      for (int i = 0; i < 9; i++) {
+        int64_t d = (int64_t)t[i] - (i < 8 ? scl::l(i) : 0u) + b;
+        t[i] = (uint32_t)d;
+        b = d >> 32;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = t[i];
+}
+
+// Signed radix-16 recoding: 64 digits in [-8, 8], sum e_i 16^i = s.
+// Requires s < 2^255 (true for s < l and any reduced scalar).
+TMV_HD void sc_signed_radix16(int8_t e[64], const uint32_t s[8]) {
+#pragma unroll
+  for (int i = 0; i < 64; i++) e[i] = (int8_t)((s[i >> 3] >> (4 * (i & 7))) & 15);
+  int carry = 0;
+#pragma unroll
+  for (int i = 0; i < 63; i++) {
+    e[i] = (int8_t)(e[i] + carry);
+    carry = (e[i] + 8) >> 4;
+    e[i] = (int8_t)(e[i] - carry * 16);
+  }
+  e[63] = (int8_t)(e[63] + carry);
+}
+
+}  // namespace tmv

@@ -1,0 +1,259 @@
+// Host runtime behind include/tmverify.h: device discovery, per-device
+// base-point tables, pinned staging, streams and the shard-by-index
+// multi-GPU split.  Compiled by hipcc into libtmgpu.so.
+//
+// There is deliberately no CPU fallback in this library: if the device path
+// fails the call returns < 0 and the caller decides (the Go shim
+// re-verifies on CPU).  Product code never links the test oracle.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/tmverify.h"
+#include "ed25519_core.h"
+#include "verify_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const char *where, hipError_t e) {
+  g_last_error = std::string(where) + ": " + hipGetErrorString(e);
+}
+void set_error(const std::string &s) { g_last_error = s; }
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+struct DeviceBuf {
+  void *ptr = nullptr;
+  size_t cap = 0;
+  bool pinned = false;
+  hipError_t ensure(size_t bytes, bool host_pinned) {
+    if (bytes <= cap) return hipSuccess;
+    release();
+    size_t want = std::max<size_t>(bytes, 1 << 20);
+    want = want + want / 4;
+    hipError_t e = host_pinned ? hipHostMalloc(&ptr, want, hipHostMallocDefault) : hipMalloc(&ptr, want);
+    if (e != hipSuccess) { ptr = nullptr; cap = 0; return e; }
+    cap = want;
+    pinned = host_pinned;
+    return hipSuccess;
+  }
+  void release() {
+    if (!ptr) return;
+    if (pinned) (void)hipHostFree(ptr); else (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+  }
+};
+
+struct Device {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  tmv::ge_precomp *d_btable = nullptr;
+  DeviceBuf d_in, d_out, h_in, h_out;
+  std::mutex mu;
+};
+
+// Packed staging layout for one shard: pk | sig | off | msg (16-B aligned).
+struct Layout {
+  size_t pk, sig, off, msg, total;
+  Layout(uint32_t n, size_t msg_bytes) {
+    pk = 0;
+    sig = align16(pk + 32ull * n);
+    off = align16(sig + 64ull * n);
+    msg = align16(off + 4ull * (n + 1));
+    total = align16(msg + std::max<size_t>(msg_bytes, 1));
+  }
+};
+
+}  // namespace
+
+struct tmv_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+};
+
+static int init_device(Device &d) {
+  hipError_t e = hipSetDevice(d.id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
+  std::vector<tmv::ge_precomp> table(tmv::kBaseTableRows * tmv::kBaseTableCols);
+  tmv::build_base_table(table.data());
+  const size_t bytes = table.size() * sizeof(tmv::ge_precomp);
+  e = hipMalloc(&d.d_btable, bytes);
+  if (e != hipSuccess) { set_error("hipMalloc(btable)", e); return TMV_ERR_NOMEM; }
+  e = hipMemcpy(d.d_btable, table.data(), bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) { set_error("hipMemcpy(btable)", e); return TMV_ERR_NO_DEVICE; }
+  return 0;
+}
+
+extern "C" {
+
+const char *tmv_last_error(void) { return g_last_error.c_str(); }
+const char *tmv_version(void) { return "tmverify-mi355x 0.1 (gfx950)"; }
+
+tmv_ctx *tmv_open(uint32_t device_mask) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) {
+    set_error(e != hipSuccess ? std::string("hipGetDeviceCount: ") + hipGetErrorString(e)
+                              : std::string("no HIP device visible"));
+    return nullptr;
+  }
+  auto ctx = std::make_unique<tmv_ctx>();
+  for (int i = 0; i < count && i < 32; i++) {
+    if (device_mask != 0 && !(device_mask & (1u << i))) continue;
+    auto d = std::make_unique<Device>();
+    d->id = i;
+    if (init_device(*d) != 0) return nullptr;
+    ctx->devs.push_back(std::move(d));
+  }
+  if (ctx->devs.empty()) {
+    set_error("device_mask selects no visible device");
+    return nullptr;
+  }
+  return ctx.release();
+}
+
+void tmv_close(tmv_ctx *ctx) {
+  if (!ctx) return;
+  for (auto &d : ctx->devs) {
+    (void)hipSetDevice(d->id);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    d->d_in.release();
+    d->d_out.release();
+    d->h_in.release();
+    d->h_out.release();
+    if (d->d_btable) (void)hipFree(d->d_btable);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+  }
+  delete ctx;
+}
+
+int tmv_num_devices(const tmv_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+}  // extern "C"
+
+// Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
+static int stage_and_launch_ed25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                    const uint32_t *msg_off, uint32_t lo, uint32_t hi) {
+  const uint32_t n = hi - lo;
+  const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
+  Layout L(n, mbytes);
+  hipError_t e = hipSetDevice(d.id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  if ((e = d.h_in.ensure(L.total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.d_in.ensure(L.total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  uint8_t *h = static_cast<uint8_t *>(d.h_in.ptr);
+  std::memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
+  std::memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
+  uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
+  const uint32_t base = msg_off[lo];
+  for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
+  if (mbytes) std::memcpy(h + L.msg, msg + base, mbytes);
+  if ((e = hipMemcpyAsync(d.d_in.ptr, h, L.total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
+    set_error("hipMemcpyAsync(H2D)", e);
+    return TMV_ERR_LAUNCH;
+  }
+  uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
+  e = tmv::launch_ed25519_verify(dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<uint32_t *>(dd + L.off), n,
+                                 d.d_btable, static_cast<uint8_t *>(d.d_out.ptr), d.stream);
+  if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
+  if ((e = hipMemcpyAsync(d.h_out.ptr, d.d_out.ptr, n, hipMemcpyDeviceToHost, d.stream)) != hipSuccess) {
+    set_error("hipMemcpyAsync(D2H)", e);
+    return TMV_ERR_LAUNCH;
+  }
+  return 0;
+}
+
+extern "C" {
+
+int tmv_ed25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                             const uint32_t *msg_off, uint32_t n, uint8_t *valid_out) {
+  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
+  if (n == 0) return TMV_NOT_ALL;
+  if (!pk || !sig || !msg_off || !valid_out || (!msg && msg_off[n] != msg_off[0])) {
+    set_error("null argument");
+    return TMV_ERR_ARG;
+  }
+  const uint32_t ndev = (uint32_t)ctx->devs.size();
+  // Shard by contiguous index ranges; tiny batches stay on one device.
+  const uint32_t shards = std::max<uint32_t>(1, std::min<uint32_t>(ndev, n / 1024));
+  std::vector<std::unique_lock<std::mutex>> locks;
+  std::vector<uint32_t> bounds(shards + 1);
+  for (uint32_t s = 0; s <= shards; s++) bounds[s] = (uint32_t)((uint64_t)n * s / shards);
+  for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
+  int rc = 0;
+  for (uint32_t s = 0; s < shards && rc == 0; s++)
+    rc = stage_and_launch_ed25519(*ctx->devs[s], pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
+  for (uint32_t s = 0; s < shards; s++) {
+    Device &d = *ctx->devs[s];
+    (void)hipSetDevice(d.id);
+    hipError_t e = hipStreamSynchronize(d.stream);
+    if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
+    if (rc == 0) std::memcpy(valid_out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
+  }
+  if (rc != 0) return rc;
+  for (uint32_t i = 0; i < n; i++)
+    if (!valid_out[i]) return TMV_NOT_ALL;
+  return TMV_ALL_VALID;
+}
+
+int tmv_ed25519_verify(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *msg, size_t msg_len, const uint8_t *sig,
+                       size_t sig_len) {
+  if (sig_len != 64) return 0;  // crypto/ed25519/ed25519.go:175-177
+  if (msg_len > 0xffffffffu) { set_error("message too long"); return TMV_ERR_ARG; }
+  uint32_t off[2] = {0, (uint32_t)msg_len};
+  uint8_t v = 0;
+  static const uint8_t empty = 0;
+  int rc = tmv_ed25519_verify_batch(ctx, pk, sig, msg ? msg : &empty, off, 1, &v);
+  return rc < 0 ? rc : (int)v;
+}
+
+int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_pk, const uint8_t *d_sig,
+                                    const uint8_t *d_msg, const uint32_t *d_msg_off, uint32_t n, uint8_t *d_valid,
+                                    void *stream) {
+  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
+  Device *dev = nullptr;
+  for (auto &d : ctx->devs)
+    if (d->id == device) dev = d.get();
+  if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (n == 0) return TMV_NOT_ALL;
+  hipError_t e = hipSetDevice(dev->id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  e = tmv::launch_ed25519_verify(d_pk, d_sig, d_msg, d_msg_off, n, dev->d_btable, d_valid, s);
+  if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
+  return TMV_NOT_ALL;
+}
+
+}  // extern "C"
+
+// sr25519 / mixed entry points: implemented in the sr25519 milestone.
+extern "C" {
+int tmv_sr25519_verify_batch(tmv_ctx *, const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
+                             uint32_t, int8_t *) {
+  set_error("sr25519 path not built yet");
+  return TMV_ERR_ARG;
+}
+int tmv_verify_mixed_batch(tmv_ctx *, const uint8_t *, const uint8_t *, const uint8_t *, const uint8_t *,
+                           const uint32_t *, uint32_t, int8_t *) {
+  set_error("mixed path not built yet");
+  return TMV_ERR_ARG;
+}
+int tmv_verify_mixed_batch_device(tmv_ctx *, int, const uint8_t *, const uint8_t *, const uint8_t *,
+                                  const uint8_t *, const uint32_t *, uint32_t, int8_t *, void *) {
+  set_error("mixed path not built yet");
+  return TMV_ERR_ARG;
+}
+}

@@ -1,0 +1,68 @@
+// Host build of the exact device arithmetic (tendermint_amd/csrc/*.h) with
+// limb-bound assertions (TMV_BOUNDS_CHECK).  Loaded by tests/test_arith_host.py
+// and compared with the CPU oracle; no GPU needed.
+#include <cstdint>
+#include <cstring>
+#include <vector>
+#include "../../tendermint_amd/csrc/ed25519_core.h"
+
+using namespace tmv;
+
+static std::vector<ge_precomp> g_table;
+
+static void load_words(uint32_t w[8], const uint8_t *b) {
+  for (int i = 0; i < 8; i++)
+    w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+           ((uint32_t)b[4 * i + 3] << 24);
+}
+
+extern "C" int hostcheck_ed25519_verify_batch(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                              const uint32_t *off, uint32_t n, uint8_t *out) {
+  if (g_table.empty()) {
+    g_table.resize(kBaseTableRows * kBaseTableCols);
+    build_base_table(g_table.data());
+  }
+  int all = n > 0;
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t a[8], r[8], s[8];
+    load_words(a, pk + 32 * i);
+    load_words(r, sig + 64 * i);
+    load_words(s, sig + 64 * i + 32);
+    out[i] = ed25519_verify_core(a, r, s, msg + off[i], off[i + 1] - off[i], g_table.data());
+    all &= out[i];
+  }
+  return all;
+}
+
+extern "C" void hostcheck_sc_reduce512(const uint8_t in[64], uint8_t out[32]) {
+  uint32_t x[16], r[8];
+  for (int i = 0; i < 16; i++)
+    x[i] = (uint32_t)in[4 * i] | ((uint32_t)in[4 * i + 1] << 8) | ((uint32_t)in[4 * i + 2] << 16) |
+           ((uint32_t)in[4 * i + 3] << 24);
+  sc_reduce512(r, x);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(r[i] >> (8 * j));
+}
+
+extern "C" void hostcheck_fe_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  fe x, y, z;
+  fe_from_bytes(x, a);
+  fe_from_bytes(y, b);
+  fe_carry(x, x);
+  fe_carry(y, y);
+  fe_mul(z, x, y);
+  uint32_t w[8];
+  fe_to_words(w, z);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
+}
+
+extern "C" void hostcheck_sha512_pq_msg(const uint8_t *p, const uint8_t *q, const uint8_t *m, uint32_t mlen,
+                                        uint8_t out[64]) {
+  uint32_t P[8], Q[8], h[16];
+  load_words(P, p);
+  load_words(Q, q);
+  sha512_pq_msg(h, P, Q, m, mlen);
+  for (int i = 0; i < 16; i++)
+    for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
