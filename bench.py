@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark: ed25519 ZIP-215 verification on MI355X (BASELINE.json metric).
+
+  python bench.py --gpus N --steps K --warmup W
+
+A *step* = one pass of the hot path over one synthetic C2 batch
+(BASELINE.json configs[1]: 10,000 ed25519 signatures over commit-vote
+sign-bytes, 1% corrupted / ZIP-215 edge cases) already resident in HBM:
+one launch of k_ed25519_verify producing the exact validity vector.  With
+N > 1 (one process per GPU, torchrun) every rank verifies its own 10k shard
+(weak scaling) and the packed validity bitmaps are all-gathered over RCCL,
+which is the only cross-GPU exchange the path has.
+
+Printed (rank 0, one JSON line): value = verifies/s of the whole job
+(kernel path, inputs resident), plus end-to-end (host buffers, PCIe
+included), p50/p99 of a 150-validator commit batch through the host C-ABI,
+the roofline object for k_ed25519_verify and a CPU baseline (the C oracle
+"port" on the host's cores; the Go reference cannot be built here).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from tendermint_amd import _native as N  # noqa: E402
+from tendermint_amd.testing.factory import make_c2_batch, make_commit_batch  # noqa: E402
+
+METRIC = "ed25519 verifies/sec at 1/2/4/8 GPUs + p50 VerifyCommit latency, 150 vals"
+# Canonical algorithmic work per verified signature:
+# 2,700 field multiplications x 100 32x32->64 partial products.
+MULS_PER_SIG = 2.7e5
+# Peak 32x32->64 multiply-add rate of one MI355X, measured by
+# tools/mulbench.hip (v_mad_i64_i32, 256 CUs): profiles/mulbench_r01.json.
+PEAK_MUL_PER_S = 1.6989e13
+
+
+def _load_peak() -> float:
+    p = os.path.join(REPO, "profiles", "mulbench_r01.json")
+    try:
+        with open(p) as f:
+            return float(json.load(f)["mad_i64_i32_per_s"])
+    except Exception:
+        return PEAK_MUL_PER_S
+
+
+def _load_traffic():
+    p = os.path.join(REPO, "profiles", "traffic_r01.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(batch, seconds_target: float = 12.0):
+    """Oracle C port on the host cores, bounded sample (rank 0, N=1 only)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_c  # noqa: E402  (test infrastructure; checker/baseline only)
+    threads = int(os.environ.get("TMV_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    # calibrate on 1,000 sigs, then size the sample to ~seconds_target of CPU time
+    sub = batch.off[:1001]
+    t0 = time.perf_counter()
+    oracle_c.ed25519_verify_packed(batch.pk[:32000], batch.sig[:64000], batch.msg, sub, threads=1)
+    per_sig_cpu = (time.perf_counter() - t0) / 1000
+    reps = max(1, int(seconds_target / (per_sig_cpu * batch.n)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle_c.ed25519_verify_packed(batch.pk, batch.sig, batch.msg, batch.off, threads=threads)
+    wall = time.perf_counter() - t0
+    return {"value": round(reps * batch.n / wall, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
+            "sample": f"C2 batch ({batch.n} sigs) x {reps} passes, oracle/c/ed25519_oracle.c, "
+                      f"{threads} pthreads; Go/curve25519-voi not buildable here (no toolchain)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=10_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    ctx = N.Context(1 << local_rank)
+    # each rank gets its own shard of signatures (distinct keys/messages)
+    batch = make_c2_batch(args.batch, seed=0xED25519 + rank)
+    n = batch.n
+    d_pk = torch.from_numpy(batch.pk).to(dev)
+    d_sig = torch.from_numpy(batch.sig).to(dev)
+    d_msg = torch.from_numpy(batch.msg).to(dev)
+    d_off = torch.from_numpy(batch.off.view(np.int32)).to(dev)
+    d_valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nbytes_bitmap = (n + 7) // 8
+    weights = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=dev)
+    pad = nbytes_bitmap * 8 - n
+    gathered = [torch.zeros(nbytes_bitmap, dtype=torch.uint8, device=dev) for _ in range(world)]
+    stream = torch.cuda.Stream(dev)
+    sp = stream.cuda_stream
+
+    def step(ev_pair=None):
+        with torch.cuda.stream(stream):
+            if ev_pair is not None:
+                ev_pair[0].record(stream)
+            ctx.ed25519_verify_batch_device(local_rank, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                            d_off.data_ptr(), n, d_valid.data_ptr(), sp)
+            if ev_pair is not None:
+                ev_pair[1].record(stream)
+            if world > 1:
+                v = torch.nn.functional.pad(d_valid, (0, pad)).view(-1, 8).to(torch.int32)
+                bitmap = (v * weights).sum(1).to(torch.uint8)
+                dist.all_gather(gathered, bitmap)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
+    valid_count = int(d_valid.sum().item())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    result = None
+    if rank == 0:
+        total = n * world * args.steps
+        value = total / elapsed
+        kernel_rate = n / (kern_ms * 1e-3)
+        # end-to-end through the host C-ABI (pinned staging, H2D, kernel, D2H)
+        e2e = []
+        for _ in range(max(3, min(args.steps, 10))):
+            t1 = time.perf_counter()
+            ctx.ed25519_verify_batch(batch.pk, batch.sig, batch.msg, batch.off)
+            e2e.append(time.perf_counter() - t1)
+        e2e_rate = n / statistics.median(e2e)
+        # p50 / p99 of a 150-validator commit batch through the host C-ABI
+        cb = make_commit_batch(150)
+        lat = []
+        for _ in range(200):
+            t1 = time.perf_counter()
+            ok, _v = ctx.ed25519_verify_batch(cb.pk, cb.sig, cb.msg, cb.off)
+            lat.append((time.perf_counter() - t1) * 1e3)
+            assert ok
+        lat.sort()
+        peak = _load_peak()
+        achieved = kernel_rate * MULS_PER_SIG
+        result = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (deterministic C2 generator, OpenSSL-signed commit-vote sign-bytes)",
+            "config": {"workload": "C2: 10k ed25519 ZIP-215 batch, 1% corrupted/edge-case sigs (BASELINE configs[1])",
+                       "batch_per_gpu": n, "msg_bytes_avg": round(float(batch.msg.size) / n, 1),
+                       "parallelism": f"shard{world}" if world > 1 else "single"},
+            "valid_count": valid_count,
+            "kernel_only_verifies_per_s": round(kernel_rate, 1),
+            "end_to_end_verifies_per_s": round(e2e_rate, 1),
+            "verify_commit_150_p50_ms": round(lat[len(lat) // 2], 4),
+            "verify_commit_150_p99_ms": round(lat[int(len(lat) * 0.99) - 1], 4),
+            "roofline": {"bound": "valu-int-mul", "achieved": round(achieved / 1e12, 4),
+                         "peak": round(peak / 1e12, 4), "unit": "Tmul/s", "frac": round(achieved / peak, 4),
+                         "traffic": _load_traffic(),
+                         "kernel": "k_ed25519_verify", "kernel_avg_ms": round(kern_ms, 4),
+                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d))"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(batch)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+// Quad-lane edwards25519 arithmetic: one point spread over the 4 lanes of a
+// DPP quad (lane c holds coordinate c), so a point doubling costs each lane
+// one squaring + one multiply and an addition two multiplies — 4-way
+// parallel twisted-Edwards formulas (add-2008-hwcd-3 / dbl-2008-hwcd, a=-1)
+// with the linear glue done by quad_perm DPP moves (free cross-lane reads
+// inside a quad, no LDS).  Used by the latency kernel k_ed25519_verify_quad.
+//
+// Lane layouts (c = lane & 3):
+//   P3Q      (X, Y, Z, T)                 extended point
+//   P1P1Q    (E, H, G, F)                 completed point (x = E/G, y = H/F)
+//   CachedQ  (Y-X, Y+X, 2dT, Z)           addend; B-table entries have Z = 1
+// Every branch below is quad-uniform or lane-select only: DPP requires all
+// four lanes of a quad to be active.
+#pragma once
+#include "curve25519.h"
+
+namespace tmv {
+namespace quad {
+
+constexpr int qp(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
+
+template <int CTRL>
+TMV_DEV void fe_dpp(fe &h, const fe &f) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = __builtin_amdgcn_mov_dpp(f.v[i], CTRL, 0xF, 0xF, false);
+}
+
+// h = s * f for a per-lane s in {-1, 0, +1}
+TMV_DEV void fe_signed(fe &h, const fe &f, int s) {
+  const int32_t m = s < 0 ? -1 : 0;
+  const int32_t keep = s != 0 ? -1 : 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = ((f.v[i] ^ m) - m) & keep;
+}
+
+// h = f^2 << sh (sh in {0, 1}, per lane), carried to level 1
+TMV_DEV void fe_sq_shift(fe &h, const fe &f, int sh) {
+  int32_t f2[10], f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = 19 * f.v[i]; }
+  int64_t c[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      const int oddodd = (i & 1) && (j & 1);
+      int32_t a = (i == j) ? f.v[i] : f2[i];
+      if (oddodd) a = 2 * a;
+      if (i + j < 10) c[i + j] += (int64_t)a * f.v[j];
+      else            c[i + j - 10] += (int64_t)a * f19[j];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; k++) c[k] = c[k] << sh;
+  fe_carry_wide(h, c);
+}
+
+TMV_DEV int lane4() { return (int)(threadIdx.x & 3); }
+
+TMV_DEV void p3_identity(fe &p) {
+  const int c = lane4();
+  fe_zero(p);
+  p.v[0] = (c == 1 || c == 2) ? 1 : 0;
+}
+TMV_DEV void cached_identity(fe &q) {
+  const int c = lane4();
+  fe_zero(q);
+  q.v[0] = (c == 2) ? 0 : 1;
+}
+
+// P1P1Q -> P3Q: (E F, H G, G F, E H)
+TMV_DEV void p1p1_to_p3(fe &p, const fe &r) {
+  fe o1, o2;
+  fe_dpp<qp(0, 1, 2, 0)>(o1, r);
+  fe_dpp<qp(3, 2, 3, 1)>(o2, r);
+  fe_mul(p, o1, o2);
+}
+
+// P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
+// E = S3 - S1 - S0, H = S1 + S0, G = S1 - S0, F = S2 - S1 + S0 (all negated
+// relative to dbl-2008-hwcd, same projective point).
+TMV_DEV void dbl(fe &r, const fe &p) {
+  const int c = lane4();
+  fe a, b, s;
+  fe_dpp<qp(0, 1, 2, 0)>(a, p);
+  fe_dpp<qp(1, 1, 1, 1)>(b, p);
+  fe_signed(b, b, c == 3 ? 1 : 0);
+  fe_add(s, a, b);                          // lane 3: X + Y (level 2)
+  fe S;
+  fe_sq_shift(S, s, c == 2 ? 1 : 0);
+  fe base, s1, s0;
+  fe_dpp<qp(3, 3, 2, 2)>(base, S);
+  fe_signed(base, base, (c == 0 || c == 3) ? 1 : 0);
+  fe_dpp<qp(1, 1, 1, 1)>(s1, S);
+  fe_signed(s1, s1, (c == 0 || c == 3) ? -1 : 1);
+  fe_dpp<qp(0, 0, 0, 0)>(s0, S);
+  fe_signed(s0, s0, (c == 0 || c == 2) ? -1 : 1);
+  fe_add(r, base, s1);
+  fe_add(r, r, s0);                         // level 3
+}
+
+// P3Q + CachedQ -> P1P1Q
+TMV_DEV void add(fe &r, const fe &p, const fe &q) {
+  const int c = lane4();
+  fe a, b, op1, M;
+  fe_dpp<qp(1, 1, 3, 2)>(a, p);             // Y, Y, T, Z
+  fe_dpp<qp(0, 0, 0, 0)>(b, p);             // X
+  fe_signed(b, b, c == 0 ? -1 : (c == 1 ? 1 : 0));
+  fe_add(op1, a, b);                        // Y-X, Y+X, T, Z (level 2)
+  fe_mul(M, op1, q);                        // A, B, C, D
+  fe u, v;
+  fe_dpp<qp(1, 1, 3, 3)>(u, M);             // B, B, D, D
+  fe_dpp<qp(0, 0, 2, 2)>(v, M);             // A, A, C, C
+  if (c >= 2) fe_add(u, u, u);              // 2D (lane select, no DPP inside)
+  fe_signed(v, v, (c == 0 || c == 3) ? -1 : 1);
+  fe_add(r, u, v);                          // B-A, B+A, 2D+C, 2D-C (level 3)
+}
+
+// q -> -q in CachedQ when neg (quad-uniform flag): swap lanes 0/1, negate lane 2
+TMV_DEV void cached_cneg(fe &q, bool neg) {
+  const int c = lane4();
+  fe t;
+  fe_dpp<qp(1, 0, 2, 3)>(t, q);
+  fe_signed(t, t, c == 2 ? -1 : 1);
+  fe_cmov(q, t, neg);
+}
+
+// P3Q -> CachedQ: (Y-X, Y+X, 2dT, Z)
+TMV_DEV void to_cached(fe &q, const fe &p) {
+  const int c = lane4();
+  fe a, b, t, k;
+  fe_dpp<qp(1, 1, 3, 2)>(a, p);
+  fe_dpp<qp(0, 0, 0, 0)>(b, p);
+  fe_signed(b, b, c == 0 ? -1 : (c == 1 ? 1 : 0));
+  fe_add(t, a, b);
+  if (c == 2) {
+    k = consts::d2();
+  } else {
+    fe_one(k);
+  }
+  fe_mul(q, t, k);                          // lane 2 scales by 2d; others re-carry
+}
+
+// [8]P == O on a P3Q point: X == 0 and Y == Z.  Returns the quad verdict on
+// every lane of the quad.
+TMV_DEV bool is_identity_times8(const fe &p) {
+  const int c = lane4();
+  fe q = p, r;
+  for (int i = 0; i < 3; i++) {
+    dbl(r, q);
+    p1p1_to_p3(q, r);
+  }
+  fe z;
+  fe_dpp<qp(2, 2, 2, 2)>(z, q);
+  fe_signed(z, z, c == 1 ? 1 : 0);
+  fe d;
+  fe_sub(d, q, z);                          // lane 0: X, lane 1: Y - Z
+  const int zero = fe_is_zero(d) ? 1 : 0;
+  const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
+  const int z1 = __builtin_amdgcn_mov_dpp(zero, qp(1, 1, 1, 1), 0xF, 0xF, false);
+  return (z0 & z1) != 0;
+}
+
+}  // namespace quad
+}  // namespace tmv

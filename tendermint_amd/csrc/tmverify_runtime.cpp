@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -57,10 +58,30 @@ struct DeviceBuf {
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
-  tmv::ge_precomp *d_btable = nullptr;
-  DeviceBuf d_in, d_out, h_in, h_out;
+  tmv::ge_precomp *d_btable = nullptr;   // 32x8 comb (single-lane kernel)
+  tmv::fe *d_btab_q = nullptr;           // 8 x CachedQ multiples of B (quad kernel)
+  DeviceBuf d_in, d_out, h_in, h_out, d_work;
+  hipEvent_t work_done = nullptr;        // orders workspace reuse across streams
   std::mutex mu;
 };
+
+// Kernel choice: the quad (4 lanes / signature) path wins while the batch is
+// too small to fill the chip one lane per signature; the single-lane kernel
+// has less glue per signature and wins on large batches.
+// TMV_KERNEL=quad|single overrides (A/B measurement).
+uint32_t g_quad_max = 0;
+int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
+
+void read_env() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char *k = getenv("TMV_KERNEL");
+    if (k && !strcmp(k, "quad")) g_kernel_override = 1;
+    if (k && !strcmp(k, "single")) g_kernel_override = 0;
+    const char *t = getenv("TMV_QUAD_MAX");
+    g_quad_max = t ? (uint32_t)strtoul(t, nullptr, 10) : 49152u;
+  });
+}
 
 // Packed staging layout for one shard: pk | sig | off | msg (16-B aligned).
 struct Layout {
@@ -92,6 +113,51 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipMalloc(btable)", e); return TMV_ERR_NOMEM; }
   e = hipMemcpy(d.d_btable, table.data(), bytes, hipMemcpyHostToDevice);
   if (e != hipSuccess) { set_error("hipMemcpy(btable)", e); return TMV_ERR_NO_DEVICE; }
+  // quad B table: entry m = (m+1)B as (ymx, ypx, xy2d, 1)
+  std::vector<tmv::fe> bq(32);
+  for (int m = 0; m < 8; m++) {
+    bq[4 * m + 0] = table[m].ymx;
+    bq[4 * m + 1] = table[m].ypx;
+    bq[4 * m + 2] = table[m].xy2d;
+    tmv::fe_one(bq[4 * m + 3]);
+  }
+  e = hipMalloc(&d.d_btab_q, bq.size() * sizeof(tmv::fe));
+  if (e != hipSuccess) { set_error("hipMalloc(btab_q)", e); return TMV_ERR_NOMEM; }
+  e = hipMemcpy(d.d_btab_q, bq.data(), bq.size() * sizeof(tmv::fe), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { set_error("hipMemcpy(btab_q)", e); return TMV_ERR_NO_DEVICE; }
+  e = hipEventCreateWithFlags(&d.work_done, hipEventDisableTiming);
+  if (e != hipSuccess) { set_error("hipEventCreate", e); return TMV_ERR_NO_DEVICE; }
+  return 0;
+}
+
+// Enqueue ed25519 verification of n device-resident entries on stream s.
+// Caller holds d.mu.  Chooses the quad or single-lane kernel.
+static int launch_ed25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                          const uint32_t *off, uint32_t n, uint8_t *valid, hipStream_t s) {
+  read_env();
+  const bool quad = g_kernel_override == 1 || (g_kernel_override == -1 && n <= g_quad_max);
+  hipError_t e;
+  if (!quad) {
+    e = tmv::launch_ed25519_verify(pk, sig, msg, off, n, d.d_btable, valid, s);
+    if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
+    return 0;
+  }
+  const size_t need = tmv::Ed25519Work::bytes(n);
+  if (need > d.d_work.cap) {
+    // the old workspace may still be in use by an earlier launch
+    (void)hipEventSynchronize(d.work_done);
+    if ((e = d.d_work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); return TMV_ERR_NOMEM; }
+  }
+  (void)hipStreamWaitEvent(s, d.work_done, 0);
+  uint8_t *base = static_cast<uint8_t *>(d.d_work.ptr);
+  tmv::Ed25519Work w;
+  w.negA = reinterpret_cast<tmv::fe *>(base);
+  w.Rc = reinterpret_cast<tmv::fe *>(base + 160ull * n);
+  w.k = reinterpret_cast<uint32_t *>(base + 320ull * n);
+  w.flags = base + 352ull * n;
+  e = tmv::launch_ed25519_verify_quad(pk, sig, msg, off, n, d.d_btab_q, w, valid, s);
+  if (e != hipSuccess) { set_error("k_ed25519_verify_quad launch", e); return TMV_ERR_LAUNCH; }
+  (void)hipEventRecord(d.work_done, s);
   return 0;
 }
 
@@ -130,6 +196,9 @@ void tmv_close(tmv_ctx *ctx) {
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     d->d_in.release();
     d->d_out.release();
+    d->d_work.release();
+    if (d->d_btab_q) (void)hipFree(d->d_btab_q);
+    if (d->work_done) (void)hipEventDestroy(d->work_done);
     d->h_in.release();
     d->h_out.release();
     if (d->d_btable) (void)hipFree(d->d_btable);
@@ -166,9 +235,9 @@ static int stage_and_launch_ed25519(Device &d, const uint8_t *pk, const uint8_t 
     return TMV_ERR_LAUNCH;
   }
   uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
-  e = tmv::launch_ed25519_verify(dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<uint32_t *>(dd + L.off), n,
-                                 d.d_btable, static_cast<uint8_t *>(d.d_out.ptr), d.stream);
-  if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
+  int rc = launch_ed25519(d, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<uint32_t *>(dd + L.off), n,
+                          static_cast<uint8_t *>(d.d_out.ptr), d.stream);
+  if (rc != 0) return rc;
   if ((e = hipMemcpyAsync(d.h_out.ptr, d.d_out.ptr, n, hipMemcpyDeviceToHost, d.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(D2H)", e);
     return TMV_ERR_LAUNCH;
@@ -232,9 +301,9 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
-  e = tmv::launch_ed25519_verify(d_pk, d_sig, d_msg, d_msg_off, n, dev->d_btable, d_valid, s);
-  if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
-  return TMV_NOT_ALL;
+  std::lock_guard<std::mutex> lk(dev->mu);
+  int rc = launch_ed25519(*dev, d_pk, d_sig, d_msg, d_msg_off, n, d_valid, s);
+  return rc != 0 ? rc : TMV_NOT_ALL;
 }
 
 }  // extern "C"

@@ -1,0 +1,192 @@
+"""Deterministic synthetic workloads for the configs of BASELINE.json.
+
+Keys follow the reference's test convention GenPrivKeyFromSecret
+(crypto/ed25519/ed25519.go:162-165: seed = SHA-256(secret)) with secrets
+"key: %x" (types/validator_set_test.go:1621-1631).  Messages are real
+commit-vote sign-bytes (types/block.go:859-862), 109-125 bytes.
+
+C2: 10,000 ed25519 signatures, seed 0xED25519, 9,900 honest
+plus 100 edge cases: 20 bit flips (R/S/M), 15 S+l, 15 undecodable R or A
+(all invalid), 20 small-order (A, R) with S = 0, 15 non-canonical (y >= p)
+torsion encodings, 15 "-0" sign-bit encodings (all VALID under ZIP-215).
+"""
+from __future__ import annotations
+
+import hashlib
+import random
+from dataclasses import dataclass, field
+from typing import List, Tuple
+
+import numpy as np
+
+from ..types.canonical import BlockID, PartSetHeader, Timestamp, vote_sign_bytes, PRECOMMIT_TYPE
+from ._openssl import Ed25519Signer
+
+P = 2**255 - 19
+L = 2**252 + 27742317777372353535851937790883648493
+_D = (-121665 * pow(121666, P - 2, P)) % P
+
+# The 14 ZIP-215 small-order encodings, derived by
+# oracle/ed25519_ref.small_order_encodings() and pinned in
+# tests/golden/zip215_small_order.json.
+SMALL_ORDER_CANONICAL = [
+    bytes(32),                                   # (0, 0) order 4 family: y = 0
+    bytes.fromhex("01" + "00" * 31),             # identity
+    bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05"),
+    bytes.fromhex("26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85"),
+    bytes.fromhex("c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a"),
+    bytes.fromhex("c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa"),
+    bytes.fromhex("ec" + "ff" * 30 + "7f"),      # order 2 (y = -1)
+    bytes.fromhex("00" * 31 + "80"),             # y = 0, sign 1
+]
+SMALL_ORDER_NONCANONICAL_Y = [                   # y >= p
+    bytes.fromhex("ed" + "ff" * 30 + "7f"),
+    bytes.fromhex("ed" + "ff" * 31),
+    bytes.fromhex("ee" + "ff" * 30 + "7f"),
+    bytes.fromhex("ee" + "ff" * 31),
+]
+SMALL_ORDER_NEG_ZERO = [                          # x = 0 with the sign bit set
+    bytes.fromhex("01" + "00" * 30 + "80"),
+    bytes.fromhex("ec" + "ff" * 31),
+]
+
+
+def key_seed(i: int, tag: str = "key") -> bytes:
+    """GenPrivKeyFromSecret([]byte(fmt.Sprintf("key: %x", i))) seed."""
+    return hashlib.sha256(f"{tag}: {i:x}".encode()).digest()
+
+
+def _is_square(x: int) -> bool:
+    return x == 0 or pow(x, (P - 1) // 2, P) == 1
+
+
+def undecodable_encodings(count: int, rng: random.Random) -> List[bytes]:
+    """Encodings whose y gives a non-square (y^2-1)/(d y^2+1): rejected by ZIP-215 decoding."""
+    out = []
+    while len(out) < count:
+        y = rng.randrange(P)
+        u = (y * y - 1) % P
+        v = (_D * y * y + 1) % P
+        if not _is_square(u * pow(v, P - 2, P) % P):
+            out.append(int.to_bytes(y | (rng.randrange(2) << 255), 32, "little"))
+    return out
+
+
+@dataclass
+class Batch:
+    pk: np.ndarray        # n*32 uint8
+    sig: np.ndarray       # n*64 uint8
+    msg: np.ndarray       # concatenated uint8
+    off: np.ndarray       # n+1 uint32
+    kinds: List[str] = field(default_factory=list)  # per-entry label (for tests)
+
+    @property
+    def n(self) -> int:
+        return len(self.off) - 1
+
+    @staticmethod
+    def from_entries(entries: List[Tuple[bytes, bytes, bytes]], kinds=None) -> "Batch":
+        n = len(entries)
+        pk = np.frombuffer(b"".join(e[0] for e in entries), np.uint8).copy() if n else np.zeros(0, np.uint8)
+        sig = np.frombuffer(b"".join(e[2] for e in entries), np.uint8).copy() if n else np.zeros(0, np.uint8)
+        off = np.zeros(n + 1, np.uint32)
+        if n:
+            off[1:] = np.cumsum([len(e[1]) for e in entries])
+        m = b"".join(e[1] for e in entries)
+        msg = np.frombuffer(m, np.uint8).copy() if m else np.zeros(0, np.uint8)
+        return Batch(pk, sig, msg, off, list(kinds) if kinds else ["honest"] * n)
+
+    def entry(self, i: int) -> Tuple[bytes, bytes, bytes]:
+        return (self.pk[32 * i:32 * i + 32].tobytes(), self.msg[self.off[i]:self.off[i + 1]].tobytes(),
+                self.sig[64 * i:64 * i + 64].tobytes())
+
+    def tile(self, n: int) -> "Batch":
+        """Repeat entries cyclically up to n (throughput runs on >10k)."""
+        idx = np.arange(n) % self.n
+        pk = self.pk.reshape(-1, 32)[idx].reshape(-1)
+        sig = self.sig.reshape(-1, 64)[idx].reshape(-1)
+        lens = (self.off[1:] - self.off[:-1])[idx]
+        off = np.zeros(n + 1, np.uint32)
+        off[1:] = np.cumsum(lens)
+        msg = np.concatenate([self.msg[self.off[i]:self.off[i + 1]] for i in idx]) if n else np.zeros(0, np.uint8)
+        return Batch(pk, sig, msg, off, [self.kinds[i] for i in idx])
+
+
+def commit_vote_message(chain_id: str, height: int, round_: int, block_id: BlockID, secs: int, nanos: int) -> bytes:
+    return vote_sign_bytes(chain_id, PRECOMMIT_TYPE, height, round_, block_id, Timestamp(secs, nanos))
+
+
+def random_block_id(rng: random.Random) -> BlockID:
+    return BlockID(bytes(rng.randrange(256) for _ in range(32)),
+                   PartSetHeader(rng.randrange(1, 1 << 16), bytes(rng.randrange(256) for _ in range(32))))
+
+
+def make_c2_batch(n: int = 10_000, seed: int = 0xED25519, chain_id: str = "test_chain_id",
+                  edge_scale: float = 1.0) -> Batch:
+    """Config 2: n ed25519 signatures over commit-vote sign-bytes, 1% edge cases."""
+    rng = random.Random(seed)
+    counts = {"bitflip": 20, "s_plus_l": 15, "undecodable": 15, "small_order": 20,
+              "noncanonical_y": 15, "neg_zero": 15}
+    counts = {k: max(1, int(round(v * edge_scale * n / 10_000))) if n >= 100 else 0 for k, v in counts.items()}
+    kinds = []
+    for k, c in counts.items():
+        kinds += [k] * c
+    kinds += ["honest"] * (n - len(kinds))
+    rng.shuffle(kinds)
+    block_id = random_block_id(rng)
+    base_secs = 1577836800  # 2020-01-01T00:00:00Z
+    undec = undecodable_encodings(counts.get("undecodable", 0) or 1, rng)
+    undec_i = 0
+    entries = []
+    for i, kind in enumerate(kinds):
+        height = 1 + rng.randrange(1 << 20)
+        msg = commit_vote_message(chain_id, height, rng.randrange(3), block_id,
+                                  base_secs + rng.randrange(1 << 24), rng.randrange(10**9))
+        if kind in ("small_order", "noncanonical_y", "neg_zero"):
+            pool = {"small_order": SMALL_ORDER_CANONICAL, "noncanonical_y": SMALL_ORDER_NONCANONICAL_Y,
+                    "neg_zero": SMALL_ORDER_NEG_ZERO}[kind]
+            a = rng.choice(pool if rng.randrange(2) else SMALL_ORDER_CANONICAL)
+            r = rng.choice(pool)
+            if rng.randrange(2):
+                a, r = r, a
+            entries.append((a, msg, r + bytes(32)))
+            continue
+        signer = Ed25519Signer(key_seed(i))
+        sig = signer.sign(msg)
+        pk = signer.public_key
+        if kind == "bitflip":
+            where = rng.randrange(3)
+            if where == 0:
+                b = bytearray(sig); b[rng.randrange(32)] ^= 1 << rng.randrange(8); sig = bytes(b)
+            elif where == 1:
+                b = bytearray(sig); b[32 + rng.randrange(31)] ^= 1 << rng.randrange(8); sig = bytes(b)
+            else:
+                b = bytearray(msg); b[rng.randrange(len(b))] ^= 1 << rng.randrange(8); msg = bytes(b)
+        elif kind == "s_plus_l":
+            s = int.from_bytes(sig[32:], "little") + L
+            sig = sig[:32] + s.to_bytes(32, "little")
+        elif kind == "undecodable":
+            bad = undec[undec_i % len(undec)]
+            undec_i += 1
+            if rng.randrange(2):
+                sig = bad + sig[32:]
+            else:
+                pk = bad
+        entries.append((pk, msg, sig))
+    return Batch.from_entries(entries, kinds)
+
+
+def make_commit_batch(n_vals: int, chain_id: str = "test_chain_id", height: int = 3, round_: int = 0,
+                      seed: int = 1) -> Batch:
+    """Config 1 shape: one commit of n_vals validators, all flags Commit,
+    timestamps 2020-01-01T00:00:00Z + i ms."""
+    rng = random.Random(seed)
+    block_id = random_block_id(rng)
+    entries = []
+    base = 1577836800
+    for i in range(n_vals):
+        signer = Ed25519Signer(key_seed(i))
+        ms = i
+        msg = commit_vote_message(chain_id, height, round_, block_id, base + ms // 1000, (ms % 1000) * 1_000_000)
+        entries.append((signer.public_key, msg, signer.sign(msg)))
+    return Batch.from_entries(entries)

@@ -1,0 +1,126 @@
+"""GPU parity: libtmgpu.so (k_ed25519_verify on gfx950, through the C-ABI)
+vs the CPU oracle and the committed golden vectors.  Bit-exact validity
+vectors are required (integer work)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle_c as C
+from tendermint_amd.testing.factory import make_c2_batch, make_commit_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(vs):
+    return C.pack([(bytes.fromhex(v["pk"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])) for v in vs])
+
+
+def test_rfc8032(ctx, golden):
+    for v in golden("ed25519_rfc8032.json")["vectors"]:
+        assert ctx.ed25519_verify(bytes.fromhex(v["pk"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"]))
+
+
+def test_golden_vectors(ctx, golden):
+    vs = golden("ed25519_vectors.json")["vectors"]
+    ok, vec = ctx.ed25519_verify_batch(*_pack(vs))
+    assert [bool(x) for x in vec] == [v["valid"] for v in vs]
+    assert ok is False
+
+
+def test_zip215_small_order_matrix(ctx, golden):
+    g = golden("zip215_small_order.json")
+    msg = bytes.fromhex(g["msg"])
+    ents = [(bytes.fromhex(a), msg, bytes.fromhex(r) + bytes(32)) for a, r in g["pairs_all_valid_with_S0"]]
+    ok, vec = ctx.ed25519_verify_batch(*C.pack(ents))
+    assert ok and vec.all() and len(vec) == 196
+
+
+def test_c2_full_size_bit_exact(ctx, golden):
+    g = golden("c2_expected.json")
+    b = make_c2_batch()
+    ok, vec = ctx.ed25519_verify_batch(b.pk, b.sig, b.msg, b.off)
+    bits = np.packbits(vec.astype(np.uint8), bitorder="little").tobytes().hex()
+    assert bits == g["valid_bits_hex"] and not ok
+    assert int(vec.sum()) == 9950
+
+
+def test_random_vs_oracle(ctx):
+    b = make_c2_batch(3000, seed=99, edge_scale=5.0)
+    ok, vec = ctx.ed25519_verify_batch(b.pk, b.sig, b.msg, b.off)
+    ok_o, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    assert np.array_equal(vec, ref) and ok == ok_o
+
+
+def test_all_valid_commit(ctx):
+    b = make_commit_batch(150)
+    ok, vec = ctx.ed25519_verify_batch(b.pk, b.sig, b.msg, b.off)
+    assert ok and vec.all()
+
+
+def test_empty_batch_false(ctx):
+    ok, vec = ctx.ed25519_verify_batch(np.zeros(0, np.uint8), np.zeros(0, np.uint8), np.zeros(0, np.uint8),
+                                       np.zeros(1, np.uint32))
+    assert ok is False and len(vec) == 0
+
+
+def test_single_verify_length_rules(ctx, golden):
+    v = golden("ed25519_rfc8032.json")["vectors"][1]
+    pk, m, s = bytes.fromhex(v["pk"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])
+    assert ctx.ed25519_verify(pk, m, s)
+    assert not ctx.ed25519_verify(pk, m, s[:63])          # crypto/ed25519/ed25519.go:175-177
+    assert not ctx.ed25519_verify(pk, m, s + b"\0")
+    b = bytearray(s); b[7] ^= 1                            # crypto/ed25519/ed25519_test.go:25-29
+    assert not ctx.ed25519_verify(pk, m, bytes(b))
+
+
+def test_message_lengths_and_block_boundaries(ctx):
+    """Messages whose R||A||M straddles SHA-512 block boundaries (0..300 B)."""
+    from tendermint_amd.testing._openssl import Ed25519Signer
+    ents = []
+    for n in list(range(0, 70)) + [110, 111, 112, 113, 127, 128, 129, 175, 176, 177, 239, 240, 241, 300]:
+        s = Ed25519Signer(hashlib.sha256(b"len %d" % n).digest())
+        m = bytes((i * 7 + n) & 255 for i in range(n))
+        ents.append((s.public_key, m, s.sign(m)))
+    ok, vec = ctx.ed25519_verify_batch(*C.pack(ents))
+    assert ok and vec.all()
+
+
+def test_unaligned_device_path(ctx):
+    """Odd-offset device pointers take the unaligned-load path."""
+    import torch
+    b = make_c2_batch(500, seed=5)
+    dev = torch.device("cuda:0")
+    raw_pk = torch.zeros(b.pk.size + 1, dtype=torch.uint8, device=dev)
+    raw_sig = torch.zeros(b.sig.size + 1, dtype=torch.uint8, device=dev)
+    raw_pk[1:] = torch.from_numpy(b.pk).to(dev)
+    raw_sig[1:] = torch.from_numpy(b.sig).to(dev)
+    d_msg = torch.from_numpy(b.msg).to(dev)
+    d_off = torch.from_numpy(b.off.view(np.int32)).to(dev)
+    out = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream()
+    ctx.ed25519_verify_batch_device(0, raw_pk.data_ptr() + 1, raw_sig.data_ptr() + 1, d_msg.data_ptr(),
+                                    d_off.data_ptr(), b.n, out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=4)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kernel", ["single", "quad"])
+def test_both_kernels_c2_subprocess(kernel, golden):
+    """Each kernel (TMV_KERNEL override) reproduces the C2 vector bit for bit."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, sys; sys.path.insert(0, '.');"
+        "from tendermint_amd import _native as N;"
+        "from tendermint_amd.testing.factory import make_c2_batch;"
+        "b = make_c2_batch(); ok, v = N.Context(1).ed25519_verify_batch(b.pk, b.sig, b.msg, b.off);"
+        "print(np.packbits(v.astype(np.uint8), bitorder='little').tobytes().hex())")
+    env = dict(os.environ, TMV_KERNEL=kernel)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == golden("c2_expected.json")["valid_bits_hex"]
