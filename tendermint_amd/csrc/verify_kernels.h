@@ -6,7 +6,7 @@
 namespace tmv {
 
 constexpr int kVerifyBlock = 256;
-constexpr int kQuadBlock = 128;   // 32 signatures per block
+constexpr int kQuadBlock = 64;    // one wave = 16 signatures per block
 
 // Per-signature workspace of the latency path (device memory).
 struct Ed25519Work {

@@ -52,36 +52,29 @@ k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig
 // Latency path: prep kernel (one lane per point) + quad kernel (4 lanes per
 // signature).
 //
-// k_ed25519_prep: lane 2i decodes A_i, hashes k_i = SHA-512(R||A||M) mod l and
-// stores -A in P3Q layout; lane 2i+1 decodes R_i and stores it in CachedQ
-// layout.  Decode failures are recorded in flags (2 bytes per signature).
+// k_ed25519_prep stores -A in P3Q layout, R in CachedQ layout and k; decode
+// failures are recorded in flags (2 bytes per signature).
 
+// Task-uniform waves: lanes [0, n) decode A_i, [n, 2n) decode R_i and
+// [2n, 3n) hash k_i = SHA-512(R||A||M) mod l, so no wave mixes the
+// decompression and SHA-512 code paths and the three run side by side.
 __global__ void __launch_bounds__(kVerifyBlock)
 k_ed25519_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
                const uint32_t *__restrict__ msg_off, uint32_t n, Ed25519Work w, int aligned) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2 * n) return;
-  const uint32_t i = j >> 1;
-  const bool isA = (j & 1) == 0;
+  if (j >= 3 * n) return;
+  const uint32_t task = j / n;
+  const uint32_t i = j - task * n;
   uint32_t a_w[8], r_w[8];
-  if (aligned) {
-    load_words_aligned(a_w, pk + 32ull * i);
-    load_words_aligned(r_w, sig + 64ull * i);
-  } else {
-    load_words_unaligned(a_w, pk + 32ull * i);
-    load_words_unaligned(r_w, sig + 64ull * i);
+  if (task != 1) {
+    if (aligned) load_words_aligned(a_w, pk + 32ull * i);
+    else load_words_unaligned(a_w, pk + 32ull * i);
   }
-  ge_p3 P;
-  const bool ok = ge_decode_zip215(P, isA ? a_w : r_w);
-  if (!ok) ge_p3_identity(P);  // keep limbs bounded; the flag rejects the entry
-  w.flags[j] = ok ? 1 : 0;
-  fe *dst = (isA ? w.negA : w.Rc) + 4ull * i;
-  if (isA) {
-    fe t;
-    fe_neg(t, P.X); dst[0] = t;
-    dst[1] = P.Y;
-    fe_one(t); dst[2] = t;
-    fe_neg(t, P.T); dst[3] = t;
+  if (task != 0) {
+    if (aligned) load_words_aligned(r_w, sig + 64ull * i);
+    else load_words_unaligned(r_w, sig + 64ull * i);
+  }
+  if (task == 2) {
     uint32_t h[16], k[8];
     const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
     sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
@@ -89,6 +82,20 @@ k_ed25519_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, 
     uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * i);
     kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
     kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
+    return;
+  }
+  const bool isA = task == 0;
+  ge_p3 P;
+  const bool ok = ge_decode_zip215(P, isA ? a_w : r_w);
+  if (!ok) ge_p3_identity(P);  // keep limbs bounded; the flag rejects the entry
+  w.flags[2 * i + (isA ? 0 : 1)] = ok ? 1 : 0;
+  fe *dst = (isA ? w.negA : w.Rc) + 4ull * i;
+  if (isA) {
+    fe t;
+    fe_neg(t, P.X); dst[0] = t;
+    dst[1] = P.Y;
+    fe_one(t); dst[2] = t;
+    fe_neg(t, P.T); dst[3] = t;
   } else {
     ge_cached c;
     ge_p3_to_cached(c, P);
@@ -206,7 +213,7 @@ hipError_t launch_ed25519_verify_quad(const uint8_t *pk, const uint8_t *sig, con
                                       uint8_t *valid, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
-  const uint32_t pblocks = (2 * n + kVerifyBlock - 1) / kVerifyBlock;
+  const uint32_t pblocks = (3 * n + kVerifyBlock - 1) / kVerifyBlock;
   hipLaunchKernelGGL(k_ed25519_prep, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w,
                      aligned);
   hipError_t e = hipGetLastError();
