@@ -464,6 +464,110 @@ TMV_HD bool ge_decode_zip215(ge_p3 &h, const uint32_t w[8]) {
   return true;
 }
 
+// ---------------------------------------------------------------- ristretto255
+// (crypto/sr25519 -> curve25519-voi primitives/sr25519, go.mod:22)
+
+// (was_square, r): r = sqrt(u/v) or sqrt(i u/v), r non-negative.
+TMV_HD bool fe_sqrt_ratio_i(fe &r, const fe &u, const fe &v) {
+  fe v3, v7, t, check, nu, nui, rp;
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);
+  fe_sq(v7, v3);
+  fe_mul(v7, v7, v);
+  fe_mul(t, u, v7);
+  fe_pow22523(t, t);
+  fe_mul(t, t, v3);
+  fe_mul(r, t, u);
+  fe_sq(check, r);
+  fe_mul(check, check, v);
+  fe_neg(nu, u);
+  fe_mul(nui, nu, consts::sqrtm1());
+  const bool correct = fe_eq(check, u);
+  const bool flipped = fe_eq(check, nu);
+  const bool flipped_i = fe_eq(check, nui);
+  fe_mul(rp, r, consts::sqrtm1());
+  if (flipped || flipped_i) r = rp;
+  if (fe_is_negative(r)) fe_neg(r, r);
+  return correct || flipped;
+}
+
+// Canonical Ristretto255 decoding (non-canonical or negative s, non-square,
+// negative t or y == 0 reject).
+TMV_HD bool ristretto_decode(ge_p3 &h, const uint32_t w[8]) {
+  fe s, ss, u1, u2, u2sq, v, t, I, Dx, Dy, x, y, one;
+  fe_from_words(s, w);
+  uint32_t chk[8];
+  fe_to_words(chk, s);
+  bool canon = true;
+  for (int i = 0; i < 8; i++) canon = canon && (chk[i] == w[i]);
+  if (!canon || (chk[0] & 1)) return false;  // >= p, bit 255 set, or negative
+  fe_carry(s, s);
+  fe_one(one);
+  fe_sq(ss, s);
+  fe_sub(u1, one, ss);                 // 2
+  fe_add(u2, one, ss);                 // 2
+  fe_sq(u2sq, u2);
+  fe_sq(t, u1);
+  fe_mul(t, t, consts::d());
+  fe_neg(t, t);
+  fe_sub(v, t, u2sq);                  // -(d u1^2) - u2^2   (2)
+  fe_mul(t, v, u2sq);
+  const bool ok = fe_sqrt_ratio_i(I, one, t);
+  fe_mul(Dx, I, u2);
+  fe_mul(Dy, I, Dx);
+  fe_mul(Dy, Dy, v);
+  fe_add(x, s, s);
+  fe_mul(x, x, Dx);
+  if (fe_is_negative(x)) fe_neg(x, x);
+  fe_mul(y, u1, Dy);
+  fe_mul(t, x, y);
+  if (!ok || fe_is_negative(t) || fe_is_zero(y)) return false;
+  h.X = x; h.Y = y; fe_one(h.Z); h.T = t;
+  return true;
+}
+
+// Ristretto255 encoding (used by the host-side test factory to make keys and
+// signatures; verification never encodes).
+TMV_HD void ristretto_encode(uint32_t out[8], const ge_p3 &p) {
+  fe u1, u2, t, invsqrt, den1, den2, zinv, ix, iy, ench, X, Y, den_inv, one, s;
+  fe_add(t, p.Z, p.Y);
+  fe_sub(u1, p.Z, p.Y);
+  fe_mul(u1, t, u1);                   // (Z+Y)(Z-Y)
+  fe_mul(u2, p.X, p.Y);
+  fe_sq(t, u2);
+  fe_mul(t, t, u1);
+  fe_one(one);
+  (void)fe_sqrt_ratio_i(invsqrt, one, t);
+  fe_mul(den1, invsqrt, u1);
+  fe_mul(den2, invsqrt, u2);
+  fe_mul(zinv, den1, den2);
+  fe_mul(zinv, zinv, p.T);
+  fe_mul(ix, p.X, consts::sqrtm1());
+  fe_mul(iy, p.Y, consts::sqrtm1());
+  fe_mul(ench, den1, consts::invsqrt_a_minus_d());
+  fe_mul(t, p.T, zinv);
+  const bool rotate = fe_is_negative(t);
+  if (rotate) { X = iy; Y = ix; den_inv = ench; }
+  else { X = p.X; Y = p.Y; den_inv = den2; }
+  fe_mul(t, X, zinv);
+  if (fe_is_negative(t)) fe_neg(Y, Y);
+  fe_sub(t, p.Z, Y);
+  fe_mul(s, den_inv, t);
+  if (fe_is_negative(s)) fe_neg(s, s);
+  fe_to_words(out, s);
+}
+
+// Ristretto equality: X1 Y2 == Y1 X2 or Y1 Y2 == X1 X2.
+TMV_HD bool ristretto_equal(const ge_p3 &a, const ge_p3 &b) {
+  fe l, r;
+  fe_mul(l, a.X, b.Y);
+  fe_mul(r, a.Y, b.X);
+  if (fe_eq(l, r)) return true;
+  fe_mul(l, a.Y, b.Y);
+  fe_mul(r, a.X, b.X);
+  return fe_eq(l, r);
+}
+
 // ---------------------------------------------------------------- scalars
 // l = 2^252 + 27742317777372353535851937790883648493, little-endian words.
 struct scl {

@@ -1,0 +1,184 @@
+// Keccak-f[1600], STROBE-128 (the subset merlin uses) and the schnorrkel
+// signing transcript, for the sr25519 challenge
+//   k = merlin("SigningContext"; "" -> ctx ""; "sign-bytes" -> M;
+//              "proto-name" -> "Schnorr-sig"; "sign:pk" -> A; "sign:R" -> R;
+//              challenge "sign:c", 64 bytes) mod l
+// (crypto/sr25519/{privkey.go:18,batch.go:39}; curve25519-voi
+// primitives/merlin + primitives/sr25519, go.mod:22).  Host+device: the
+// constant prefix (through the empty context) is absorbed once on the host
+// and handed to the kernels as a 203-byte state.
+#pragma once
+#include "curve25519.h"
+
+namespace tmv {
+
+struct keccak_rc {
+  static TMV_HD uint64_t rc(int i) {
+    const uint64_t RC[24] = {
+        0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+        0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+        0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+        0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+        0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+        0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+    return RC[i];
+  }
+};
+
+TMV_HD uint64_t rotl64(uint64_t x, int n) { return n ? ((x << n) | (x >> (64 - n))) : x; }
+
+// Keccak-f[1600] on 25 lanes (lane x + 5y), fully unrolled theta/rho/pi/chi.
+TMV_HD void keccak_f1600_lanes(uint64_t a[25]) {
+  const int rho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  for (int round = 0; round < 24; round++) {
+    uint64_t c[5], b[25];
+#pragma unroll
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      const uint64_t d = c[(x + 4) % 5] ^ rotl64(c[(x + 1) % 5], 1);
+#pragma unroll
+      for (int y = 0; y < 25; y += 5) a[y + x] ^= d;
+    }
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+#pragma unroll
+      for (int y = 0; y < 5; y++) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(a[x + 5 * y], rho[x + 5 * y]);
+#pragma unroll
+    for (int y = 0; y < 25; y += 5)
+#pragma unroll
+      for (int x = 0; x < 5; x++) a[y + x] = b[y + x] ^ (~b[y + (x + 1) % 5] & b[y + (x + 2) % 5]);
+    a[0] ^= keccak_rc::rc(round);
+  }
+}
+
+constexpr int kStrobeR = 166;
+
+// STROBE-128 state as bytes + the three position registers.
+struct strobe_t {
+  uint8_t st[200];
+  uint8_t pos, pos_begin, cur_flags;
+};
+
+TMV_HD void strobe_run_f(strobe_t &s) {
+  s.st[s.pos] ^= s.pos_begin;
+  s.st[s.pos + 1] ^= 0x04;
+  s.st[kStrobeR + 1] ^= 0x80;
+  uint64_t a[25];
+  for (int i = 0; i < 25; i++) {
+    uint64_t v = 0;
+    for (int j = 7; j >= 0; j--) v = (v << 8) | s.st[8 * i + j];
+    a[i] = v;
+  }
+  keccak_f1600_lanes(a);
+  for (int i = 0; i < 25; i++)
+    for (int j = 0; j < 8; j++) s.st[8 * i + j] = (uint8_t)(a[i] >> (8 * j));
+  s.pos = 0;
+  s.pos_begin = 0;
+}
+
+TMV_HD void strobe_absorb(strobe_t &s, const uint8_t *d, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) {
+    s.st[s.pos++] ^= d[i];
+    if (s.pos == kStrobeR) strobe_run_f(s);
+  }
+}
+TMV_HD void strobe_absorb_byte(strobe_t &s, uint8_t b) {
+  s.st[s.pos++] ^= b;
+  if (s.pos == kStrobeR) strobe_run_f(s);
+}
+
+// begin_op for a fresh (more == false) operation
+TMV_HD void strobe_begin_op(strobe_t &s, uint8_t flags) {
+  const uint8_t old_begin = s.pos_begin;
+  s.pos_begin = (uint8_t)(s.pos + 1);
+  s.cur_flags = flags;
+  strobe_absorb_byte(s, old_begin);
+  strobe_absorb_byte(s, flags);
+  if ((flags & (4 | 32)) && s.pos != 0) strobe_run_f(s);  // C or K forces F
+}
+
+// merlin append_message(label, message): meta_ad(label); meta_ad(le32(len), more); ad(message)
+TMV_HD void merlin_append(strobe_t &s, const char *label, uint32_t llen, const uint8_t *m, uint32_t n) {
+  strobe_begin_op(s, 16 | 2);  // M | A
+  strobe_absorb(s, reinterpret_cast<const uint8_t *>(label), llen);
+  const uint8_t len[4] = {(uint8_t)n, (uint8_t)(n >> 8), (uint8_t)(n >> 16), (uint8_t)(n >> 24)};
+  strobe_absorb(s, len, 4);    // meta_ad(..., more = true): no begin_op
+  strobe_begin_op(s, 2);       // A
+  strobe_absorb(s, m, n);
+}
+
+// merlin append with the message given as 8 little-endian words (32 bytes)
+TMV_HD void merlin_append_words(strobe_t &s, const char *label, uint32_t llen, const uint32_t w[8]) {
+  uint8_t b[32];
+  for (int i = 0; i < 32; i++) b[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  merlin_append(s, label, llen, b, 32);
+}
+
+// challenge_bytes(label, 64) -> out (64 bytes as 16 LE words)
+TMV_HD void merlin_challenge64(strobe_t &s, const char *label, uint32_t llen, uint32_t out[16]) {
+  strobe_begin_op(s, 16 | 2);
+  strobe_absorb(s, reinterpret_cast<const uint8_t *>(label), llen);
+  const uint8_t len[4] = {64, 0, 0, 0};
+  strobe_absorb(s, len, 4);
+  strobe_begin_op(s, 1 | 2 | 4);  // I | A | C  (prf)
+  for (int i = 0; i < 16; i++) out[i] = 0;
+  for (int i = 0; i < 64; i++) {
+    out[i >> 2] |= (uint32_t)s.st[s.pos] << (8 * (i & 3));
+    s.st[s.pos++] = 0;
+    if (s.pos == kStrobeR) strobe_run_f(s);
+  }
+}
+
+// Transcript state after merlin("SigningContext") + append("", ctx = "")
+// (crypto/sr25519/privkey.go:18): computed once on the host.
+inline void sr25519_context_prefix(strobe_t &s) {
+  for (int i = 0; i < 200; i++) s.st[i] = 0;
+  const uint8_t hdr[6] = {1, kStrobeR + 2, 1, 0, 1, 96};
+  for (int i = 0; i < 6; i++) s.st[i] = hdr[i];
+  const char *v = "STROBEv1.0.2";
+  for (int i = 0; i < 12; i++) s.st[6 + i] = (uint8_t)v[i];
+  s.pos = 0; s.pos_begin = 0; s.cur_flags = 0;
+  {
+    uint64_t a[25];
+    for (int i = 0; i < 25; i++) {
+      uint64_t w = 0;
+      for (int j = 7; j >= 0; j--) w = (w << 8) | s.st[8 * i + j];
+      a[i] = w;
+    }
+    keccak_f1600_lanes(a);
+    for (int i = 0; i < 25; i++)
+      for (int j = 0; j < 8; j++) s.st[8 * i + j] = (uint8_t)(a[i] >> (8 * j));
+  }
+  // Strobe128::new("Merlin v1.0"): meta_ad(label, false)
+  strobe_begin_op(s, 16 | 2);
+  strobe_absorb(s, reinterpret_cast<const uint8_t *>("Merlin v1.0"), 11);
+  // Transcript::new("SigningContext"): append_message("dom-sep", label)
+  merlin_append(s, "dom-sep", 7, reinterpret_cast<const uint8_t *>("SigningContext"), 14);
+  // SigningContext::new(ctx = ""): append_message("", "")
+  merlin_append(s, "", 0, reinterpret_cast<const uint8_t *>(""), 0);
+}
+
+// k = challenge mod l for (pk, R, M) starting from the context prefix.
+TMV_HD void sr25519_challenge(uint32_t k[8], const strobe_t &prefix, const uint32_t pk_w[8],
+                              const uint32_t r_w[8], const uint8_t *m, uint32_t mlen) {
+  strobe_t s = prefix;
+  merlin_append(s, "sign-bytes", 10, m, mlen);
+  merlin_append(s, "proto-name", 10, reinterpret_cast<const uint8_t *>("Schnorr-sig"), 11);
+  merlin_append_words(s, "sign:pk", 7, pk_w);
+  merlin_append_words(s, "sign:R", 6, r_w);
+  uint32_t wide[16];
+  merlin_challenge64(s, "sign:c", 6, wide);
+  sc_reduce512(k, wide);
+}
+
+// Signature.UnmarshalBinary checks: schnorrkel marker bit, canonical s.
+// s_out = s with the marker cleared.  Returns false on an Add-time error.
+TMV_HD bool sr25519_decode_s(uint32_t s_out[8], const uint32_t s_w[8]) {
+  for (int i = 0; i < 8; i++) s_out[i] = s_w[i];
+  if (!(s_w[7] & 0x80000000u)) return false;
+  s_out[7] &= 0x7fffffffu;
+  return sc_is_canonical(s_out);
+}
+
+}  // namespace tmv

@@ -163,5 +163,20 @@ TMV_DEV bool is_identity_times8(const fe &p) {
   return (z0 & z1) != 0;
 }
 
+// Ristretto equality of two P3Q points a (acc) and b (R):
+// X1 Y2 == Y1 X2 or Y1 Y2 == X1 X2.  Quad verdict on every lane.
+TMV_DEV bool ristretto_equal(const fe &a, const fe &b) {
+  fe o1, o2, p, d;
+  fe_dpp<qp(0, 1, 1, 0)>(o1, a);            // X1, Y1, Y1, X1
+  fe_dpp<qp(1, 0, 1, 0)>(o2, b);            // Y2, X2, Y2, X2
+  fe_mul(p, o1, o2);
+  fe_dpp<qp(1, 1, 3, 3)>(d, p);
+  fe_sub(d, p, d);                          // lane 0: X1Y2 - Y1X2, lane 2: Y1Y2 - X1X2
+  const int zero = fe_is_zero(d) ? 1 : 0;
+  const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
+  const int z2 = __builtin_amdgcn_mov_dpp(zero, qp(2, 2, 2, 2), 0xF, 0xF, false);
+  return (z0 | z2) != 0;
+}
+
 }  // namespace quad
 }  // namespace tmv

@@ -19,6 +19,7 @@
 
 #include "../../include/tmverify.h"
 #include "ed25519_core.h"
+#include "merlin_dev.h"
 #include "verify_kernels.h"
 
 namespace {
@@ -60,7 +61,8 @@ struct Device {
   hipStream_t stream = nullptr;
   tmv::ge_precomp *d_btable = nullptr;   // 32x8 comb (single-lane kernel)
   tmv::fe *d_btab_q = nullptr;           // 8 x CachedQ multiples of B (quad kernel)
-  DeviceBuf d_in, d_out, h_in, h_out, d_work;
+  tmv::strobe_t *d_prefix = nullptr;     // sr25519 transcript prefix (empty context)
+  DeviceBuf d_in, d_out, h_in, h_out, d_work, d_work2, d_idx;
   hipEvent_t work_done = nullptr;        // orders workspace reuse across streams
   std::mutex mu;
 };
@@ -125,8 +127,58 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipMalloc(btab_q)", e); return TMV_ERR_NOMEM; }
   e = hipMemcpy(d.d_btab_q, bq.data(), bq.size() * sizeof(tmv::fe), hipMemcpyHostToDevice);
   if (e != hipSuccess) { set_error("hipMemcpy(btab_q)", e); return TMV_ERR_NO_DEVICE; }
+  tmv::strobe_t prefix;
+  tmv::sr25519_context_prefix(prefix);
+  e = hipMalloc(&d.d_prefix, sizeof(prefix));
+  if (e != hipSuccess) { set_error("hipMalloc(prefix)", e); return TMV_ERR_NOMEM; }
+  e = hipMemcpy(d.d_prefix, &prefix, sizeof(prefix), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { set_error("hipMemcpy(prefix)", e); return TMV_ERR_NO_DEVICE; }
   e = hipEventCreateWithFlags(&d.work_done, hipEventDisableTiming);
   if (e != hipSuccess) { set_error("hipEventCreate", e); return TMV_ERR_NO_DEVICE; }
+  return 0;
+}
+
+// Make the workspace(s) big enough for n entries and order this launch after
+// the previous user of the workspace.  Caller holds d.mu.
+static int reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s) {
+  const size_t need = tmv::Ed25519Work::bytes(n);
+  const size_t idx_need = 2ull * 4 * n + 64;
+  if (need > d.d_work.cap || (mixed && (need > d.d_work2.cap || idx_need > d.d_idx.cap))) {
+    (void)hipEventSynchronize(d.work_done);  // old buffers may still be in use
+    hipError_t e;
+    if ((e = d.d_work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); return TMV_ERR_NOMEM; }
+    if (mixed) {
+      if ((e = d.d_work2.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work2)", e); return TMV_ERR_NOMEM; }
+      if ((e = d.d_idx.ensure(idx_need, false)) != hipSuccess) { set_error("hipMalloc(idx)", e); return TMV_ERR_NOMEM; }
+    }
+  }
+  (void)hipStreamWaitEvent(s, d.work_done, 0);
+  return 0;
+}
+
+static int launch_sr25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
+                          uint32_t n, int8_t *status, hipStream_t s) {
+  int rc = reserve_work(d, n, false, s);
+  if (rc != 0) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(d.d_work.ptr, n);
+  hipError_t e = tmv::launch_sr25519_verify_quad(pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w, status, s);
+  if (e != hipSuccess) { set_error("sr25519 launch", e); return TMV_ERR_LAUNCH; }
+  (void)hipEventRecord(d.work_done, s);
+  return 0;
+}
+
+static int launch_mixed(Device &d, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                        const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
+  int rc = reserve_work(d, n, true, s);
+  if (rc != 0) return rc;
+  tmv::Ed25519Work w1 = tmv::Ed25519Work::carve(d.d_work.ptr, n);
+  tmv::Ed25519Work w2 = tmv::Ed25519Work::carve(d.d_work2.ptr, n);
+  uint32_t *ib = static_cast<uint32_t *>(d.d_idx.ptr);
+  uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n;
+  hipError_t e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed,
+                                          idx_sr, status, s);
+  if (e != hipSuccess) { set_error("mixed launch", e); return TMV_ERR_LAUNCH; }
+  (void)hipEventRecord(d.work_done, s);
   return 0;
 }
 
@@ -142,19 +194,9 @@ static int launch_ed25519(Device &d, const uint8_t *pk, const uint8_t *sig, cons
     if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
     return 0;
   }
-  const size_t need = tmv::Ed25519Work::bytes(n);
-  if (need > d.d_work.cap) {
-    // the old workspace may still be in use by an earlier launch
-    (void)hipEventSynchronize(d.work_done);
-    if ((e = d.d_work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); return TMV_ERR_NOMEM; }
-  }
-  (void)hipStreamWaitEvent(s, d.work_done, 0);
-  uint8_t *base = static_cast<uint8_t *>(d.d_work.ptr);
-  tmv::Ed25519Work w;
-  w.negA = reinterpret_cast<tmv::fe *>(base);
-  w.Rc = reinterpret_cast<tmv::fe *>(base + 160ull * n);
-  w.k = reinterpret_cast<uint32_t *>(base + 320ull * n);
-  w.flags = base + 352ull * n;
+  int rc = reserve_work(d, n, false, s);
+  if (rc != 0) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(d.d_work.ptr, n);
   e = tmv::launch_ed25519_verify_quad(pk, sig, msg, off, n, d.d_btab_q, w, valid, s);
   if (e != hipSuccess) { set_error("k_ed25519_verify_quad launch", e); return TMV_ERR_LAUNCH; }
   (void)hipEventRecord(d.work_done, s);
@@ -197,6 +239,9 @@ void tmv_close(tmv_ctx *ctx) {
     d->d_in.release();
     d->d_out.release();
     d->d_work.release();
+    d->d_work2.release();
+    d->d_idx.release();
+    if (d->d_prefix) (void)hipFree(d->d_prefix);
     if (d->d_btab_q) (void)hipFree(d->d_btab_q);
     if (d->work_done) (void)hipEventDestroy(d->work_done);
     d->h_in.release();
@@ -211,16 +256,21 @@ int tmv_num_devices(const tmv_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0
 
 }  // extern "C"
 
+enum class Scheme { Ed25519, Sr25519, Mixed };
+
 // Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
-static int stage_and_launch_ed25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
-                                    const uint32_t *msg_off, uint32_t lo, uint32_t hi) {
+// Layout: pk | sig | off | msg | kind (16-B aligned pieces).
+static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
+                            const uint8_t *msg, const uint32_t *msg_off, uint32_t lo, uint32_t hi) {
   const uint32_t n = hi - lo;
   const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
   Layout L(n, mbytes);
+  const size_t kind_at = L.total;
+  const size_t total = L.total + (sch == Scheme::Mixed ? align16(n) : 0);
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
-  if ((e = d.h_in.ensure(L.total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
-  if ((e = d.d_in.ensure(L.total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.h_in.ensure(total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.d_in.ensure(total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   uint8_t *h = static_cast<uint8_t *>(d.h_in.ptr);
@@ -230,13 +280,26 @@ static int stage_and_launch_ed25519(Device &d, const uint8_t *pk, const uint8_t 
   const uint32_t base = msg_off[lo];
   for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
   if (mbytes) std::memcpy(h + L.msg, msg + base, mbytes);
-  if ((e = hipMemcpyAsync(d.d_in.ptr, h, L.total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
+  if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
+  if ((e = hipMemcpyAsync(d.d_in.ptr, h, total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
   }
   uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
-  int rc = launch_ed25519(d, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<uint32_t *>(dd + L.off), n,
-                          static_cast<uint8_t *>(d.d_out.ptr), d.stream);
+  const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
+  uint8_t *out = static_cast<uint8_t *>(d.d_out.ptr);
+  int rc;
+  switch (sch) {
+    case Scheme::Ed25519:
+      rc = launch_ed25519(d, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, out, d.stream);
+      break;
+    case Scheme::Sr25519:
+      rc = launch_sr25519(d, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out), d.stream);
+      break;
+    default:
+      rc = launch_mixed(d, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out),
+                        d.stream);
+  }
   if (rc != 0) return rc;
   if ((e = hipMemcpyAsync(d.h_out.ptr, d.d_out.ptr, n, hipMemcpyDeviceToHost, d.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(D2H)", e);
@@ -245,18 +308,18 @@ static int stage_and_launch_ed25519(Device &d, const uint8_t *pk, const uint8_t 
   return 0;
 }
 
-extern "C" {
-
-int tmv_ed25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
-                             const uint32_t *msg_off, uint32_t n, uint8_t *valid_out) {
+// Host-buffer batch: shard by contiguous index ranges over the context's
+// devices, stage, launch, gather.  out gets 1 byte per entry.
+static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
+                     const uint8_t *msg, const uint32_t *msg_off, uint32_t n, uint8_t *out) {
   if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
   if (n == 0) return TMV_NOT_ALL;
-  if (!pk || !sig || !msg_off || !valid_out || (!msg && msg_off[n] != msg_off[0])) {
+  if (!pk || !sig || !msg_off || !out || (sch == Scheme::Mixed && !kind) || (!msg && msg_off[n] != msg_off[0])) {
     set_error("null argument");
     return TMV_ERR_ARG;
   }
   const uint32_t ndev = (uint32_t)ctx->devs.size();
-  // Shard by contiguous index ranges; tiny batches stay on one device.
+  // tiny batches stay on one device
   const uint32_t shards = std::max<uint32_t>(1, std::min<uint32_t>(ndev, n / 1024));
   std::vector<std::unique_lock<std::mutex>> locks;
   std::vector<uint32_t> bounds(shards + 1);
@@ -264,19 +327,61 @@ int tmv_ed25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
   int rc = 0;
   for (uint32_t s = 0; s < shards && rc == 0; s++)
-    rc = stage_and_launch_ed25519(*ctx->devs[s], pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
+    rc = stage_and_launch(*ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
   for (uint32_t s = 0; s < shards; s++) {
     Device &d = *ctx->devs[s];
     (void)hipSetDevice(d.id);
     hipError_t e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
-    if (rc == 0) std::memcpy(valid_out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
+    if (rc == 0) std::memcpy(out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
   }
   if (rc != 0) return rc;
   for (uint32_t i = 0; i < n; i++)
-    if (!valid_out[i]) return TMV_NOT_ALL;
+    if (out[i] != 1) return TMV_NOT_ALL;
   return TMV_ALL_VALID;
 }
+
+static Device *find_device(tmv_ctx *ctx, int device) {
+  if (!ctx) return nullptr;
+  for (auto &d : ctx->devs)
+    if (d->id == device) return d.get();
+  return nullptr;
+}
+
+extern "C" {
+
+int tmv_ed25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                             const uint32_t *msg_off, uint32_t n, uint8_t *valid_out) {
+  return run_batch(ctx, Scheme::Ed25519, nullptr, pk, sig, msg, msg_off, n, valid_out);
+}
+
+int tmv_sr25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                             const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
+  return run_batch(ctx, Scheme::Sr25519, nullptr, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out));
+}
+
+int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
+                           const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
+  return run_batch(ctx, Scheme::Mixed, kind, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out));
+}
+
+int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kind, const uint8_t *d_pk,
+                                  const uint8_t *d_sig, const uint8_t *d_msg, const uint32_t *d_msg_off, uint32_t n,
+                                  int8_t *d_status, void *stream) {
+  Device *dev = find_device(ctx, device);
+  if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (n == 0) return TMV_NOT_ALL;
+  hipError_t e = hipSetDevice(dev->id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  std::lock_guard<std::mutex> lk(dev->mu);
+  int rc = launch_mixed(*dev, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
+  return rc != 0 ? rc : TMV_NOT_ALL;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 int tmv_ed25519_verify(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *msg, size_t msg_len, const uint8_t *sig,
                        size_t sig_len) {
@@ -292,10 +397,7 @@ int tmv_ed25519_verify(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *msg, size
 int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_pk, const uint8_t *d_sig,
                                     const uint8_t *d_msg, const uint32_t *d_msg_off, uint32_t n, uint8_t *d_valid,
                                     void *stream) {
-  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
-  Device *dev = nullptr;
-  for (auto &d : ctx->devs)
-    if (d->id == device) dev = d.get();
+  Device *dev = find_device(ctx, device);
   if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
   if (n == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
@@ -308,21 +410,3 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
 
 }  // extern "C"
 
-// sr25519 / mixed entry points: implemented in the sr25519 milestone.
-extern "C" {
-int tmv_sr25519_verify_batch(tmv_ctx *, const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
-                             uint32_t, int8_t *) {
-  set_error("sr25519 path not built yet");
-  return TMV_ERR_ARG;
-}
-int tmv_verify_mixed_batch(tmv_ctx *, const uint8_t *, const uint8_t *, const uint8_t *, const uint8_t *,
-                           const uint32_t *, uint32_t, int8_t *) {
-  set_error("mixed path not built yet");
-  return TMV_ERR_ARG;
-}
-int tmv_verify_mixed_batch_device(tmv_ctx *, int, const uint8_t *, const uint8_t *, const uint8_t *,
-                                  const uint8_t *, const uint32_t *, uint32_t, int8_t *, void *) {
-  set_error("mixed path not built yet");
-  return TMV_ERR_ARG;
-}
-}

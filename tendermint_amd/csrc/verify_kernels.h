@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "curve25519.h"
+#include "merlin_dev.h"
 
 namespace tmv {
 
@@ -13,13 +14,32 @@ struct Ed25519Work {
   fe *negA;        // n x 4 fe, P3Q layout of -A
   fe *Rc;          // n x 4 fe, CachedQ layout of R
   uint32_t *k;     // n x 8 words, k mod l
-  uint8_t *flags;  // 2n bytes: decode ok for A (2i) and R (2i+1)
-  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 2) + 64; }
+  uint8_t *flags;  // 4n bytes: decode ok for A (4e), R (4e+1)
+  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4) + 256; }
+  // carve a workspace for n entries out of base (16-byte aligned pieces)
+  static Ed25519Work carve(void *base, uint32_t n) {
+    uint8_t *b = static_cast<uint8_t *>(base);
+    Ed25519Work w;
+    w.negA = reinterpret_cast<fe *>(b);
+    w.Rc = reinterpret_cast<fe *>(b + 160ull * n);
+    w.k = reinterpret_cast<uint32_t *>(b + 320ull * n);
+    w.flags = b + 352ull * n;
+    return w;
+  }
 };
 
 hipError_t launch_ed25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                       const uint32_t *msg_off, uint32_t n, const fe *btab_q, Ed25519Work w,
                                       uint8_t *valid, hipStream_t stream);
+
+hipError_t launch_sr25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                      const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
+                                      Ed25519Work w, int8_t *status, hipStream_t stream);
+
+hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                               const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
+                               Ed25519Work w_ed, Ed25519Work w_sr, uint32_t *counts, uint32_t *idx_ed,
+                               uint32_t *idx_sr, int8_t *status, hipStream_t stream);
 
 hipError_t launch_ed25519_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                  const uint32_t *msg_off, uint32_t n, const ge_precomp *btable,

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include "ed25519_core.h"
 #include "quad.h"
+#include "sr25519_core.h"
 #include "verify_kernels.h"
 
 namespace tmv {
@@ -49,22 +50,33 @@ k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig
 }
 
 // ---------------------------------------------------------------------------
-// Latency path: prep kernel (one lane per point) + quad kernel (4 lanes per
-// signature).
+// Latency path: prep kernel (one lane per point / hash) + quad kernel (4
+// lanes per signature), templated on the scheme (SR = false: ed25519 ZIP-215,
+// SR = true: sr25519).  Entries may be addressed through an index list
+// (mixed batches): entry e of this launch is original signature idx[e], and
+// the entry count may live in device memory (count_ptr) so the partition
+// kernel never has to round-trip to the host.
 //
-// k_ed25519_prep stores -A in P3Q layout, R in CachedQ layout and k; decode
-// failures are recorded in flags (2 bytes per signature).
+// k_prep stores -A in P3Q layout, R (ed25519: CachedQ; sr25519: P3Q) and k;
+// decode failures go to flags (4 bytes per entry: A ok, R ok, s ok, -).
 
-// Task-uniform waves: lanes [0, n) decode A_i, [n, 2n) decode R_i and
-// [2n, 3n) hash k_i = SHA-512(R||A||M) mod l, so no wave mixes the
-// decompression and SHA-512 code paths and the three run side by side.
+__device__ __forceinline__ uint32_t entry_count(const uint32_t *count_ptr, uint32_t n) {
+  return count_ptr ? *count_ptr : n;
+}
+
+// Task-uniform waves: lanes [0, m) decode A, [m, 2m) decode R and [2m, 3m)
+// compute the challenge, so no wave mixes decompression with hashing.
+template <bool SR>
 __global__ void __launch_bounds__(kVerifyBlock)
-k_ed25519_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
-               const uint32_t *__restrict__ msg_off, uint32_t n, Ed25519Work w, int aligned) {
+k_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
+       const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
+       Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned) {
+  const uint32_t m = entry_count(count_ptr, n);
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 3 * n) return;
-  const uint32_t task = j / n;
-  const uint32_t i = j - task * n;
+  if (j >= 3 * m) return;
+  const uint32_t task = j / m;
+  const uint32_t e = j - task * m;
+  const uint32_t i = idx ? idx[e] : e;
   uint32_t a_w[8], r_w[8];
   if (task != 1) {
     if (aligned) load_words_aligned(a_w, pk + 32ull * i);
@@ -75,27 +87,36 @@ k_ed25519_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, 
     else load_words_unaligned(r_w, sig + 64ull * i);
   }
   if (task == 2) {
-    uint32_t h[16], k[8];
+    uint32_t k[8];
     const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
-    sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
-    sc_reduce512(k, h);
-    uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * i);
+    if (SR) {
+      sr25519_challenge(k, *prefix, a_w, r_w, msg + o0, o1 - o0);
+    } else {
+      uint32_t h[16];
+      sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
+      sc_reduce512(k, h);
+    }
+    uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
     kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
     kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
     return;
   }
   const bool isA = task == 0;
   ge_p3 P;
-  const bool ok = ge_decode_zip215(P, isA ? a_w : r_w);
+  bool ok;
+  if (SR) ok = ristretto_decode(P, isA ? a_w : r_w);
+  else ok = ge_decode_zip215(P, isA ? a_w : r_w);
   if (!ok) ge_p3_identity(P);  // keep limbs bounded; the flag rejects the entry
-  w.flags[2 * i + (isA ? 0 : 1)] = ok ? 1 : 0;
-  fe *dst = (isA ? w.negA : w.Rc) + 4ull * i;
-  if (isA) {
+  w.flags[4 * e + (isA ? 0 : 1)] = ok ? 1 : 0;
+  fe *dst = (isA ? w.negA : w.Rc) + 4ull * e;
+  if (isA || SR) {
     fe t;
-    fe_neg(t, P.X); dst[0] = t;
+    if (isA) fe_neg(t, P.X); else t = P.X;
+    dst[0] = t;
     dst[1] = P.Y;
     fe_one(t); dst[2] = t;
-    fe_neg(t, P.T); dst[3] = t;
+    if (isA) fe_neg(t, P.T); else t = P.T;
+    dst[3] = t;
   } else {
     ge_cached c;
     ge_p3_to_cached(c, P);
@@ -123,29 +144,44 @@ __device__ __forceinline__ void recode16_store(int8_t *dst, const uint32_t s[8],
 
 constexpr int kQuadSigs = kQuadBlock / 4;
 
-// k_ed25519_verify_quad: acc = sum over 64 signed radix-16 windows of
-// 16*acc + e_i(k)(-A) + e_i(S)B (Straus, shared doublings), then
-// [8](acc - R) == O.  Each signature occupies one quad.
+// k_verify_quad: acc = sum over 64 signed radix-16 windows of
+// 16*acc + e_i(k)(-A) + e_i(s)B (Straus, shared doublings), then
+//   ed25519: [8](acc - R) == O          (ZIP-215 cofactored)
+//   sr25519: acc == R (Ristretto equality)
+// Each signature occupies one quad; writes out[i] (ed25519 1/0; sr25519
+// 1/0/-1/-2 as int8).
+template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
-k_ed25519_verify_quad(const uint8_t *__restrict__ sig, Ed25519Work w, const fe *__restrict__ btab_q, uint32_t n,
-                      uint8_t *__restrict__ valid, int aligned) {
+k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+              uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned) {
   __shared__ fe tabA[kQuadSigs * 8 * 4];
   __shared__ fe tabB[8 * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
+  const uint32_t m = entry_count(count_ptr, n);
+  if (blockIdx.x * kQuadSigs >= m) return;  // block-uniform
   const int c = threadIdx.x & 3;
   const int q = threadIdx.x >> 2;
   const uint32_t raw = blockIdx.x * kQuadSigs + q;
-  const bool live = raw < n;
-  const uint32_t i = live ? raw : n - 1;
+  const bool live = raw < m;
+  const uint32_t e = live ? raw : m - 1;
+  const uint32_t i = idx ? idx[e] : e;
   for (int t = threadIdx.x; t < 32; t += kQuadBlock) tabB[t] = btab_q[t];
 
-  uint32_t s_w[8];
-  if (aligned) load_words_aligned(s_w, sig + 64ull * i + 32);
-  else load_words_unaligned(s_w, sig + 64ull * i + 32);
-  const bool s_ok = sc_is_canonical(s_w);
+  uint32_t s_raw[8], s_w[8];
+  if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+  else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+  bool s_ok;
+  if (SR) {
+    s_ok = sr25519_decode_s(s_w, s_raw);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
+    s_ok = sc_is_canonical(s_w);
+  }
+  if (!s_ok) s_w[7] &= 0x0fffffffu;  // keep the recoding in range; entry is rejected anyway
   {
     uint32_t k_w[8];
-    const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * i);
+    const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * e);
     const uint4 k0 = kp[0], k1 = kp[1];
     k_w[0] = k0.x; k_w[1] = k0.y; k_w[2] = k0.z; k_w[3] = k0.w;
     k_w[4] = k1.x; k_w[5] = k1.y; k_w[6] = k1.z; k_w[7] = k1.w;
@@ -154,10 +190,11 @@ k_ed25519_verify_quad(const uint8_t *__restrict__ sig, Ed25519Work w, const fe *
     for (int t = 0; t < 8; t++) sc[t] = (c & 1) ? s_w[t] : k_w[t];
     recode16_store(&dig[q][c & 1][0], sc, c < 2);
   }
-  const bool dec_ok = w.flags[2 * i] && w.flags[2 * i + 1];
+  const bool a_ok = w.flags[4 * e] != 0;
+  const bool r_ok = w.flags[4 * e + 1] != 0;
 
   // table of (m+1)(-A), m < 8, in CachedQ layout
-  fe P = w.negA[4ull * i + c];
+  fe P = w.negA[4ull * e + c];
   fe r, Pm, Q, Q0;
   quad::to_cached(Q0, P);
   tabA[(q * 8 + 0) * 4 + c] = Q0;
@@ -165,11 +202,11 @@ k_ed25519_verify_quad(const uint8_t *__restrict__ sig, Ed25519Work w, const fe *
   quad::p1p1_to_p3(Pm, r);
   quad::to_cached(Q, Pm);
   tabA[(q * 8 + 1) * 4 + c] = Q;
-  for (int m = 2; m < 8; m++) {
+  for (int t = 2; t < 8; t++) {
     quad::add(r, Pm, Q0);
     quad::p1p1_to_p3(Pm, r);
     quad::to_cached(Q, Pm);
-    tabA[(q * 8 + m) * 4 + c] = Q;
+    tabA[(q * 8 + t) * 4 + c] = Q;
   }
   __syncthreads();
 
@@ -185,43 +222,98 @@ k_ed25519_verify_quad(const uint8_t *__restrict__ sig, Ed25519Work w, const fe *
     }
     const int da = dig[q][0][wdx];
     const int db = dig[q][1][wdx];
-    fe e, idq;
+    fe ent, idq;
     quad::cached_identity(idq);
     const int aa = da < 0 ? -da : da;
-    e = tabA[(q * 8 + (aa ? aa - 1 : 0)) * 4 + c];
-    fe_cmov(e, idq, aa == 0);
-    quad::cached_cneg(e, da < 0);
-    quad::add(r, acc, e);
+    ent = tabA[(q * 8 + (aa ? aa - 1 : 0)) * 4 + c];
+    fe_cmov(ent, idq, aa == 0);
+    quad::cached_cneg(ent, da < 0);
+    quad::add(r, acc, ent);
     quad::p1p1_to_p3(acc, r);
     const int ab = db < 0 ? -db : db;
-    e = tabB[(ab ? ab - 1 : 0) * 4 + c];
-    fe_cmov(e, idq, ab == 0);
-    quad::cached_cneg(e, db < 0);
-    quad::add(r, acc, e);
+    ent = tabB[(ab ? ab - 1 : 0) * 4 + c];
+    fe_cmov(ent, idq, ab == 0);
+    quad::cached_cneg(ent, db < 0);
+    quad::add(r, acc, ent);
     quad::p1p1_to_p3(acc, r);
   }
-  fe Rq = w.Rc[4ull * i + c];
-  quad::cached_cneg(Rq, true);
-  quad::add(r, acc, Rq);
-  quad::p1p1_to_p3(acc, r);
-  const bool ok = quad::is_identity_times8(acc) && s_ok && dec_ok;
-  if (live && c == 0) valid[i] = ok ? 1 : 0;
+  int status;
+  if (SR) {
+    const fe Rq = w.Rc[4ull * e + c];
+    const bool eq = quad::ristretto_equal(acc, Rq);
+    status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
+  } else {
+    fe Rq = w.Rc[4ull * e + c];
+    quad::cached_cneg(Rq, true);
+    quad::add(r, acc, Rq);
+    quad::p1p1_to_p3(acc, r);
+    const bool ok = quad::is_identity_times8(acc) && s_ok && a_ok && r_ok;
+    status = ok ? 1 : 0;
+  }
+  if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
+}
+
+// Mixed batches: split indices by key kind (TMV_KIND_ED25519 = 0,
+// TMV_KIND_SR25519 = 1).  Order inside a list is irrelevant: results are
+// scattered back by original index.  Unknown kinds get status 0.
+__global__ void k_partition(const uint8_t *__restrict__ kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed,
+                            uint32_t *idx_sr, uint8_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t k = kind[i];
+  if (k == 0) idx_ed[atomicAdd(&counts[0], 1u)] = i;
+  else if (k == 1) idx_sr[atomicAdd(&counts[1], 1u)] = i;
+  else out[i] = 0;
+}
+
+static int is_aligned(const void *a, const void *b) {
+  return ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
+}
+
+template <bool SR>
+static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                  const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr,
+                                  uint32_t n, const fe *btab_q, const strobe_t *prefix, Ed25519Work w,
+                                  uint8_t *out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int aligned = is_aligned(pk, sig);
+  const uint32_t pblocks = (uint32_t)((3ull * n + kVerifyBlock - 1) / kVerifyBlock);
+  hipLaunchKernelGGL(k_prep<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
+                     count_ptr, n, w, prefix, aligned);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
+  hipLaunchKernelGGL(k_verify_quad<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
+                     btab_q, out, aligned);
+  return hipGetLastError();
 }
 
 hipError_t launch_ed25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                       const uint32_t *msg_off, uint32_t n, const fe *btab_q, Ed25519Work w,
                                       uint8_t *valid, hipStream_t stream) {
+  return launch_pipeline<false>(pk, sig, msg, msg_off, nullptr, nullptr, n, btab_q, nullptr, w, valid, stream);
+}
+
+hipError_t launch_sr25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                      const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
+                                      Ed25519Work w, int8_t *status, hipStream_t stream) {
+  return launch_pipeline<true>(pk, sig, msg, msg_off, nullptr, nullptr, n, btab_q, prefix, w,
+                               reinterpret_cast<uint8_t *>(status), stream);
+}
+
+hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                               const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
+                               Ed25519Work w_ed, Ed25519Work w_sr, uint32_t *counts, uint32_t *idx_ed,
+                               uint32_t *idx_sr, int8_t *status, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
-  const uint32_t pblocks = (3 * n + kVerifyBlock - 1) / kVerifyBlock;
-  hipLaunchKernelGGL(k_ed25519_prep, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w,
-                     aligned);
-  hipError_t e = hipGetLastError();
+  hipError_t e = hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
-  const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  hipLaunchKernelGGL(k_ed25519_verify_quad, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, w, btab_q, n, valid,
-                     aligned);
-  return hipGetLastError();
+  uint8_t *out = reinterpret_cast<uint8_t *>(status);
+  hipLaunchKernelGGL(k_partition, dim3((n + 255) / 256), dim3(256), 0, stream, kind, n, counts, idx_ed, idx_sr, out);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  e = launch_pipeline<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, out, stream);
+  if (e != hipSuccess) return e;
+  return launch_pipeline<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, out, stream);
 }
 
 hipError_t launch_ed25519_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,

@@ -190,3 +190,56 @@ def make_commit_batch(n_vals: int, chain_id: str = "test_chain_id", height: int 
         msg = commit_vote_message(chain_id, height, round_, block_id, base + ms // 1000, (ms % 1000) * 1_000_000)
         entries.append((signer.public_key, msg, signer.sign(msg)))
     return Batch.from_entries(entries)
+
+
+def make_sr25519_batch(n: int, seed: int = 0x5125519, chain_id: str = "test_chain_id",
+                       bad_frac: float = 0.01) -> Batch:
+    """sr25519 signatures over commit-vote sign-bytes; ~bad_frac corrupted
+    (bit flips / missing marker / bad key encodings)."""
+    from .sr25519_factory import Sr25519Signer, mini_from_secret
+    rng = random.Random(seed)
+    block_id = random_block_id(rng)
+    entries, kinds = [], []
+    base_secs = 1577836800
+    for i in range(n):
+        signer = Sr25519Signer(mini_from_secret(f"key: {i:x}".encode()))
+        msg = commit_vote_message(chain_id, 1 + rng.randrange(1 << 20), rng.randrange(3), block_id,
+                                  base_secs + rng.randrange(1 << 24), rng.randrange(10**9))
+        sig = signer.sign(msg, b"%d" % i)
+        pk = signer.public_key
+        kind = "honest"
+        if rng.random() < bad_frac:
+            kind = rng.choice(["flip_r", "flip_s", "flip_m", "no_marker", "bad_pk"])
+            if kind == "flip_r":
+                b = bytearray(sig); b[rng.randrange(32)] ^= 1 << rng.randrange(8); sig = bytes(b)
+            elif kind == "flip_s":
+                b = bytearray(sig); b[32 + rng.randrange(31)] ^= 1 << rng.randrange(8); sig = bytes(b)
+            elif kind == "flip_m":
+                b = bytearray(msg); b[rng.randrange(len(b))] ^= 1 << rng.randrange(8); msg = bytes(b)
+            elif kind == "no_marker":
+                b = bytearray(sig); b[63] &= 0x7F; sig = bytes(b)
+            else:
+                pk = (int.from_bytes(pk, "little") | 1).to_bytes(32, "little")
+        entries.append((pk, msg, sig))
+        kinds.append(kind)
+    return Batch.from_entries(entries, kinds)
+
+
+def make_mixed_batch(n: int, seed: int = 0xC5, sr_frac: float = 0.5):
+    """Config 5 shape: interleaved ed25519 + sr25519 entries.  Returns
+    (kind uint8 array, Batch)."""
+    rng = random.Random(seed)
+    n_sr = int(n * sr_frac)
+    ed = make_c2_batch(n - n_sr, seed=seed) if n - n_sr else Batch.from_entries([])
+    sr = make_sr25519_batch(n_sr, seed=seed + 1) if n_sr else Batch.from_entries([])
+    order = [0] * (n - n_sr) + [1] * n_sr
+    rng.shuffle(order)
+    entries, kinds, labels = [], [], []
+    ie = isr = 0
+    for k in order:
+        if k == 0:
+            entries.append(ed.entry(ie)); labels.append(ed.kinds[ie]); ie += 1
+        else:
+            entries.append(sr.entry(isr)); labels.append("sr:" + sr.kinds[isr]); isr += 1
+        kinds.append(k)
+    return np.array(kinds, np.uint8), Batch.from_entries(entries, labels)
