@@ -1,0 +1,108 @@
+/*
+ * tmhost.h — C-ABI of the host layer above the verification engine
+ * (libtmgpu.so): the crypto.BatchVerifier object, canonical vote sign-bytes
+ * and the commit verifiers, implemented in C++ (tendermint_amd/csrc/host/)
+ * over include/tmverify.h.  Plain pointers and sizes only.
+ *
+ * These are the entry points a Go cgo shim binds:
+ *   tmv_batch_*        crypto.BatchVerifier (crypto/crypto.go:66-76) created
+ *                      by batch.CreateBatchVerifier (crypto/batch/batch.go:11-21)
+ *   tmv_vote_sign_bytes types.VoteSignBytes (types/vote.go:149-157)
+ *   tmv_verify_commit  types.VerifyCommit / VerifyCommitLight /
+ *                      VerifyCommitLightTrusting (types/validation.go:27,61,96)
+ */
+#ifndef TMHOST_H
+#define TMHOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "tmverify.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Key kinds: TMV_KIND_ED25519, TMV_KIND_SR25519; anything else is a key type
+ * without batch support (e.g. secp256k1, crypto/batch/batch.go:13-20). */
+#define TMV_KIND_OTHER 255
+
+/* ---- crypto.BatchVerifier ---- */
+typedef struct tmv_batch tmv_batch;
+
+/* batch.CreateBatchVerifier: NULL when key_kind has no batch verifier. */
+tmv_batch *tmv_batch_new(tmv_ctx *ctx, uint8_t key_kind);
+/* Add: returns 0, or 1 with the reference's error text in err (type and
+ * length checks: crypto/ed25519/ed25519.go:209-224,
+ * crypto/sr25519/batch.go:23-28).  Curve-decoding failures of sr25519 keys
+ * and signatures are reported by tmv_batch_verify (deferred Add error). */
+int tmv_batch_add(tmv_batch *b, uint8_t key_kind, const uint8_t *pk, size_t pk_len, const uint8_t *msg,
+                  size_t msg_len, const uint8_t *sig, size_t sig_len, char *err, size_t err_cap);
+size_t tmv_batch_len(const tmv_batch *b);
+/* Verify: 1 all valid, 0 not (or empty), 2 a deferred Add error (index in
+ * *add_err_index, text in err), < 0 infrastructure error.  valid_out gets
+ * one byte per entry in Add order. */
+int tmv_batch_verify(tmv_batch *b, uint8_t *valid_out, int64_t *add_err_index, char *err, size_t err_cap);
+void tmv_batch_free(tmv_batch *b);
+
+/* ---- commit data ---- */
+typedef struct {
+  const uint8_t *hash;
+  uint32_t hash_len;
+  uint32_t psh_total;
+  const uint8_t *psh_hash;
+  uint32_t psh_hash_len;
+} tmv_block_id;
+
+typedef struct {
+  const uint8_t *address;
+  uint32_t address_len;
+  const uint8_t *pub_key;
+  uint32_t pub_key_len;
+  uint8_t key_kind;
+  int64_t voting_power;
+  int64_t proposer_priority;
+} tmv_validator;
+
+typedef struct {
+  uint8_t block_id_flag; /* 1 absent, 2 commit, 3 nil */
+  const uint8_t *validator_address;
+  uint32_t validator_address_len;
+  int64_t ts_seconds;
+  int32_t ts_nanos;
+  const uint8_t *signature;
+  uint32_t signature_len;
+} tmv_commit_sig;
+
+typedef struct {
+  int64_t height;
+  int32_t round;
+  tmv_block_id block_id;
+  const tmv_commit_sig *sigs;
+  uint32_t n_sigs;
+} tmv_commit;
+
+/* types.VoteSignBytes for (chain_id, type, height, round, block_id or NULL
+ * for nil, timestamp).  Returns the length; writes min(len, cap) bytes. */
+size_t tmv_vote_sign_bytes(const char *chain_id, int32_t vote_type, int64_t height, int32_t round,
+                           const tmv_block_id *block_id, int64_t ts_seconds, int32_t ts_nanos, uint8_t *out,
+                           size_t cap);
+
+#define TMV_COMMIT_FULL 0           /* types.VerifyCommit */
+#define TMV_COMMIT_LIGHT 1          /* types.VerifyCommitLight */
+#define TMV_COMMIT_LIGHT_TRUSTING 2 /* types.VerifyCommitLightTrusting */
+
+/* Verify a commit against a validator set.  vals == NULL means a nil
+ * validator set, commit == NULL a nil commit.  proposer_index < 0 derives
+ * the proposer from priorities.  block_id / height are ignored for
+ * LIGHT_TRUSTING; trust_num / trust_den only apply to it.
+ * Returns 0 (ok), 1 (verification error; text in err, byte-identical to the
+ * reference's error), < 0 infrastructure error. */
+int tmv_verify_commit(tmv_ctx *ctx, int mode, const char *chain_id, const tmv_validator *vals, uint32_t n_vals,
+                      int32_t proposer_index, const tmv_block_id *block_id, int64_t height, const tmv_commit *commit,
+                      int64_t trust_num, int64_t trust_den, char *err, size_t err_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMHOST_H */

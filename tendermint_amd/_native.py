@@ -15,6 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libtmgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tmverify.h")
+HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(_HERE), "include", "tmhost.h")]
 
 TMV_ALL_VALID = 1
 TMV_NOT_ALL = 0
@@ -32,6 +33,9 @@ EXPORTS = [
     "tmv_open", "tmv_close", "tmv_num_devices", "tmv_last_error", "tmv_version",
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
+    # include/tmhost.h
+    "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
+    "tmv_vote_sign_bytes", "tmv_verify_commit",
 ]
 
 

@@ -1,0 +1,463 @@
+// Host-side mirror of the reference's commit-verification layer, in C++
+// (the reference is compiled Go; no Go toolchain exists here).  Header-only
+// so the CPU test harness (tests/native/commit_check.cpp) can instantiate the
+// same control flow with a test-double verifier, while libtmgpu.so
+// instantiates it with the GPU batch verifier.
+//
+//   types/validation.go        VerifyCommit / VerifyCommitLight /
+//                              VerifyCommitLightTrusting / verifyCommitBatch /
+//                              verifyCommitSingle / verifyBasicValsAndCommit
+//   types/block.go:584-694     CommitSig (+ String), BlockIDFlag
+//   types/block.go:815-862     Commit, GetVote, VoteSignBytes
+//   types/block.go:1398-1418   BlockID IsNil / String
+//   types/part_set.go:103-113  PartSetHeader String / IsZero / Equals
+//   types/validator.go:129-138 Validator.String
+//   types/validator_set.go     GetByAddress, TotalVotingPower, GetProposer,
+//                              ErrNotEnoughVotingPowerSigned, safeMul
+//   types/errors.go            ErrInvalidCommitHeight / Signatures
+//   types/vote.go:149-157, types/canonical.go, canonical.pb.go  sign-bytes
+//   crypto/batch/batch.go      CreateBatchVerifier / SupportsBatchVerifier
+// Error strings are byte-identical to the Go originals (tests assert the
+// substrings the reference's types/validation_test.go asserts).
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace tmh {
+
+using Bytes = std::vector<uint8_t>;
+using Error = std::optional<std::string>;
+
+// ---------------------------------------------------------------- Go-style formatting
+inline std::string HexUpper(const uint8_t *p, size_t n) {
+  static const char *d = "0123456789ABCDEF";
+  std::string s;
+  s.reserve(2 * n);
+  for (size_t i = 0; i < n; i++) {
+    s.push_back(d[p[i] >> 4]);
+    s.push_back(d[p[i] & 15]);
+  }
+  return s;
+}
+inline std::string HexUpper(const Bytes &b) { return HexUpper(b.data(), b.size()); }
+inline std::string HexUpper(const std::string &s) {
+  return HexUpper(reinterpret_cast<const uint8_t *>(s.data()), s.size());
+}
+// libs/bytes.Fingerprint: first 6 bytes, zero padded
+inline Bytes Fingerprint(const Bytes &b) {
+  Bytes f(6, 0);
+  std::memcpy(f.data(), b.data(), std::min<size_t>(6, b.size()));
+  return f;
+}
+
+struct Timestamp {
+  int64_t seconds = -62135596800LL;  // Go's zero time.Time
+  int32_t nanos = 0;
+};
+
+// time.RFC3339Nano of a UTC instant (CanonicalTime, types/canonical.go:61-66)
+inline std::string CanonicalTime(const Timestamp &t) {
+  int64_t secs = t.seconds;
+  int64_t days = secs / 86400, rem = secs % 86400;
+  if (rem < 0) { rem += 86400; days -= 1; }
+  // civil_from_days (proleptic Gregorian)
+  int64_t z = days + 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const int64_t doe = z - era * 146097;
+  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  int64_t y = yoe + era * 400;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const int64_t mp = (5 * doy + 2) / 153;
+  const int64_t dd = doy - (153 * mp + 2) / 5 + 1;
+  const int64_t mm = mp + (mp < 10 ? 3 : -9);
+  if (mm <= 2) y += 1;
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%04lld-%02lld-%02lldT%02lld:%02lld:%02lld", (long long)y, (long long)mm,
+                (long long)dd, (long long)(rem / 3600), (long long)((rem / 60) % 60), (long long)(rem % 60));
+  std::string s(buf);
+  if (t.nanos != 0) {
+    char f[16];
+    std::snprintf(f, sizeof f, "%09d", t.nanos);
+    std::string frac(f);
+    while (!frac.empty() && frac.back() == '0') frac.pop_back();
+    s += "." + frac;
+  }
+  return s + "Z";
+}
+
+// ---------------------------------------------------------------- keys
+enum class KeyType : uint8_t { Ed25519 = 0, Sr25519 = 1, Other = 255 };
+
+struct PubKey {
+  KeyType type = KeyType::Ed25519;
+  Bytes bytes;
+  std::string Type() const {
+    return type == KeyType::Ed25519 ? "ed25519" : type == KeyType::Sr25519 ? "sr25519" : "other";
+  }
+  std::string String() const {  // crypto/ed25519/ed25519.go:182, crypto/sr25519/pubkey.go:68
+    if (type == KeyType::Ed25519) return "PubKeyEd25519{" + HexUpper(bytes) + "}";
+    if (type == KeyType::Sr25519) return "PubKeySr25519{" + HexUpper(bytes) + "}";
+    return "PubKey{" + HexUpper(bytes) + "}";
+  }
+};
+
+// ---------------------------------------------------------------- crypto.BatchVerifier
+// crypto/crypto.go:66-76.  Add appends; Verify returns (all ok, vector in
+// Add order).  Add-time failures that need curve decoding (sr25519 public
+// key / signature encoding, crypto/sr25519/batch.go:30-37) are detected on
+// the device and surfaced by DeferredAddError() after Verify; the commit
+// verifier below orders them exactly where the reference's Add would have
+// returned them.
+class BatchVerifier {
+ public:
+  virtual ~BatchVerifier() = default;
+  virtual Error Add(const PubKey &key, const Bytes &msg, const Bytes &sig) = 0;
+  virtual std::pair<bool, std::vector<bool>> Verify() = 0;
+  // (batch index, message) of the first entry whose Add would have failed
+  virtual std::optional<std::pair<size_t, std::string>> DeferredAddError() const { return std::nullopt; }
+  // true when DeferredAddError() can be non-empty (sr25519)
+  virtual bool MayDeferAddErrors() const { return false; }
+};
+
+using BatchVerifierFactory = std::function<std::unique_ptr<BatchVerifier>(KeyType)>;
+using SingleVerifier = std::function<bool(const PubKey &, const Bytes &msg, const Bytes &sig)>;
+
+// crypto/batch/batch.go:26-33
+inline bool SupportsBatchVerifier(const PubKey &pk) {
+  return pk.type == KeyType::Ed25519 || pk.type == KeyType::Sr25519;
+}
+
+// ---------------------------------------------------------------- types
+enum BlockIDFlag : uint8_t { BlockIDFlagAbsent = 1, BlockIDFlagCommit = 2, BlockIDFlagNil = 3 };
+
+struct PartSetHeader {
+  uint32_t total = 0;
+  Bytes hash;
+  bool IsZero() const { return total == 0 && hash.empty(); }
+  bool Equals(const PartSetHeader &o) const { return total == o.total && hash == o.hash; }
+  std::string String() const { return std::to_string(total) + ":" + HexUpper(Fingerprint(hash)); }
+};
+
+struct BlockID {
+  Bytes hash;
+  PartSetHeader part_set_header;
+  bool IsNil() const { return hash.empty() && part_set_header.IsZero(); }
+  bool Equals(const BlockID &o) const { return hash == o.hash && part_set_header.Equals(o.part_set_header); }
+  std::string String() const { return HexUpper(hash) + ":" + part_set_header.String(); }
+};
+
+struct CommitSig {
+  BlockIDFlag block_id_flag = BlockIDFlagAbsent;
+  Bytes validator_address;
+  Timestamp timestamp;
+  Bytes signature;
+  // types/block.go:633-639
+  std::string String() const {
+    return "CommitSig{" + HexUpper(Fingerprint(signature)) + " by " + HexUpper(Fingerprint(validator_address)) +
+           " on " + std::to_string((int)block_id_flag) + " @ " + CanonicalTime(timestamp) + "}";
+  }
+  // types/block.go:643-657
+  BlockID BlockIDFor(const BlockID &commit_block_id) const {
+    return block_id_flag == BlockIDFlagCommit ? commit_block_id : BlockID{};
+  }
+};
+
+constexpr int32_t kPrevoteType = 1;
+constexpr int32_t kPrecommitType = 2;
+
+inline void PutUvarint(Bytes &out, uint64_t x) {
+  while (x >= 0x80) {
+    out.push_back((uint8_t)(x | 0x80));
+    x >>= 7;
+  }
+  out.push_back((uint8_t)x);
+}
+inline void PutFixed64(Bytes &out, int64_t v) {
+  for (int i = 0; i < 8; i++) out.push_back((uint8_t)((uint64_t)v >> (8 * i)));
+}
+
+// types.VoteSignBytes: MarshalDelimited(CanonicalizeVote(chainID, vote)).
+// block_id == nullptr or a nil BlockID omits field 4 (types/canonical.go:18-32).
+inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t height, int32_t round,
+                           const BlockID *block_id, const Timestamp &ts) {
+  Bytes body;
+  body.reserve(128);
+  if (type != 0) { body.push_back(0x08); PutUvarint(body, (uint64_t)(uint32_t)type); }
+  if (height != 0) { body.push_back(0x11); PutFixed64(body, height); }
+  if (round != 0) { body.push_back(0x19); PutFixed64(body, (int64_t)round); }
+  if (block_id && !block_id->IsNil()) {
+    Bytes psh;
+    if (block_id->part_set_header.total != 0) { psh.push_back(0x08); PutUvarint(psh, block_id->part_set_header.total); }
+    if (!block_id->part_set_header.hash.empty()) {
+      psh.push_back(0x12);
+      PutUvarint(psh, block_id->part_set_header.hash.size());
+      psh.insert(psh.end(), block_id->part_set_header.hash.begin(), block_id->part_set_header.hash.end());
+    }
+    Bytes cb;
+    if (!block_id->hash.empty()) {
+      cb.push_back(0x0a);
+      PutUvarint(cb, block_id->hash.size());
+      cb.insert(cb.end(), block_id->hash.begin(), block_id->hash.end());
+    }
+    cb.push_back(0x12);
+    PutUvarint(cb, psh.size());
+    cb.insert(cb.end(), psh.begin(), psh.end());
+    body.push_back(0x22);
+    PutUvarint(body, cb.size());
+    body.insert(body.end(), cb.begin(), cb.end());
+  }
+  Bytes t;
+  if (ts.seconds != 0) { t.push_back(0x08); PutUvarint(t, (uint64_t)ts.seconds); }
+  if (ts.nanos != 0) { t.push_back(0x10); PutUvarint(t, (uint64_t)(int64_t)ts.nanos); }
+  body.push_back(0x2a);
+  PutUvarint(body, t.size());
+  body.insert(body.end(), t.begin(), t.end());
+  if (!chain_id.empty()) {
+    body.push_back(0x32);
+    PutUvarint(body, chain_id.size());
+    body.insert(body.end(), chain_id.begin(), chain_id.end());
+  }
+  Bytes out;
+  out.reserve(body.size() + 2);
+  PutUvarint(out, body.size());
+  out.insert(out.end(), body.begin(), body.end());
+  return out;
+}
+
+struct Commit {
+  int64_t height = 0;
+  int32_t round = 0;
+  BlockID block_id;
+  std::vector<CommitSig> signatures;
+  // types/block.go:836-862: only the timestamp and the flag differ per index
+  Bytes VoteSignBytes(const std::string &chain_id, int32_t idx) const {
+    const CommitSig &cs = signatures[(size_t)idx];
+    const BlockID bid = cs.BlockIDFor(block_id);
+    return tmh::VoteSignBytes(chain_id, kPrecommitType, height, round, &bid, cs.timestamp);
+  }
+};
+
+struct Validator {
+  Bytes address;
+  PubKey pub_key;
+  int64_t voting_power = 0;
+  int64_t proposer_priority = 0;
+  std::string String() const {  // types/validator.go:129-138
+    return "Validator{" + HexUpper(address) + " " + pub_key.String() + " VP:" + std::to_string(voting_power) +
+           " A:" + std::to_string(proposer_priority) + "}";
+  }
+};
+
+struct ValidatorSet {
+  std::vector<Validator> validators;
+  int proposer = -1;  // index of the current proposer, -1 = derive from priorities
+  mutable int64_t total_voting_power = 0;
+
+  size_t Size() const { return validators.size(); }
+  int64_t TotalVotingPower() const {
+    if (total_voting_power == 0)
+      for (const auto &v : validators) total_voting_power += v.voting_power;
+    return total_voting_power;
+  }
+  // types/validator_set.go:267-274 (linear scan, like the reference)
+  std::pair<int32_t, const Validator *> GetByAddress(const Bytes &addr) const {
+    for (size_t i = 0; i < validators.size(); i++)
+      if (validators[i].address == addr) return {(int32_t)i, &validators[i]};
+    return {-1, nullptr};
+  }
+  // types/validator_set.go:322-344: highest priority, ties to the smaller address
+  const Validator *GetProposer() const {
+    if (validators.empty()) return nullptr;
+    if (proposer >= 0 && (size_t)proposer < validators.size()) return &validators[(size_t)proposer];
+    const Validator *best = nullptr;
+    for (const auto &v : validators) {
+      if (!best || v.proposer_priority > best->proposer_priority ||
+          (v.proposer_priority == best->proposer_priority && v.address < best->address))
+        best = &v;
+    }
+    return best;
+  }
+};
+
+// ---------------------------------------------------------------- errors
+inline std::string ErrNotEnoughVotingPowerSigned(int64_t got, int64_t needed) {
+  return "invalid commit -- insufficient voting power: got " + std::to_string(got) + ", needed more than " +
+         std::to_string(needed);
+}
+inline std::string ErrInvalidCommitSignatures(size_t expected, size_t actual) {
+  return "Invalid commit -- wrong set size: " + std::to_string(expected) + " vs " + std::to_string(actual);
+}
+inline std::string ErrInvalidCommitHeight(int64_t expected, int64_t actual) {
+  return "Invalid commit -- wrong height: " + std::to_string(expected) + " vs " + std::to_string(actual);
+}
+
+// types/validator_set.go:910-931
+inline std::pair<int64_t, bool> SafeMul(int64_t a, int64_t b) {
+  if (a == 0 || b == 0) return {0, false};
+  const int64_t ab = b < 0 ? -b : b, aa = a < 0 ? -a : a;
+  if (aa > INT64_MAX / ab) return {0, true};
+  return {a * b, false};
+}
+
+// ---------------------------------------------------------------- commit verification
+constexpr int kBatchVerifyThreshold = 2;  // types/validation.go:12
+
+struct CommitVerifier {
+  BatchVerifierFactory make_batch;  // batch.CreateBatchVerifier
+  SingleVerifier verify_single;     // PubKey.VerifySignature
+
+  bool ShouldBatchVerify(const ValidatorSet &vals, const Commit &commit) const {
+    const Validator *p = vals.GetProposer();
+    return commit.signatures.size() >= (size_t)kBatchVerifyThreshold && p && SupportsBatchVerifier(p->pub_key);
+  }
+
+  using SigPred = bool (*)(const CommitSig &);
+
+  Error VerifyBatch(const std::string &chain_id, const ValidatorSet &vals, const Commit &commit, int64_t needed,
+                    SigPred ignore, SigPred count, bool count_all, bool by_index) const {
+    const Validator *proposer = vals.GetProposer();
+    std::unique_ptr<BatchVerifier> bv =
+        (proposer && SupportsBatchVerifier(proposer->pub_key)) ? make_batch(proposer->pub_key.type) : nullptr;
+    if (!bv || commit.signatures.size() < (size_t)kBatchVerifyThreshold)
+      return std::string("unsupported signature algorithm or insufficient signatures for batch verification");
+    int64_t tallied = 0;
+    std::unordered_map<int32_t, int> seen;
+    std::vector<int> batch_idx;
+    batch_idx.reserve(commit.signatures.size());
+    for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
+      const CommitSig &cs = commit.signatures[idx];
+      if (ignore(cs)) continue;
+      const Validator *val;
+      if (by_index) {
+        val = &vals.validators[idx];
+      } else {
+        auto [vi, v] = vals.GetByAddress(cs.validator_address);
+        if (!v) continue;
+        auto it = seen.find(vi);
+        if (it != seen.end())
+          return "double vote from " + v->String() + " (" + std::to_string(it->second) + " and " +
+                 std::to_string(idx) + ")";
+        seen[vi] = (int)idx;
+        val = v;
+      }
+      Bytes sb = commit.VoteSignBytes(chain_id, (int32_t)idx);
+      if (Error e = bv->Add(val->pub_key, sb, cs.signature)) return e;
+      batch_idx.push_back((int)idx);
+      if (count(cs)) tallied += val->voting_power;
+      if (!count_all && tallied > needed) break;
+    }
+    // A device-detected Add error (sr25519) must win over the power check, as
+    // the reference's Add would have returned it inside the loop above; for
+    // ed25519 the reference order (power check, then Verify) is kept.
+    std::pair<bool, std::vector<bool>> res;
+    if (bv->MayDeferAddErrors()) {
+      res = bv->Verify();
+      if (auto de = bv->DeferredAddError()) return de->second;
+      if (tallied <= needed) return ErrNotEnoughVotingPowerSigned(tallied, needed);
+    } else {
+      if (tallied <= needed) return ErrNotEnoughVotingPowerSigned(tallied, needed);
+      res = bv->Verify();
+    }
+    const bool ok = res.first;
+    const std::vector<bool> &valid = res.second;
+    if (ok) return std::nullopt;
+    for (size_t i = 0; i < valid.size(); i++) {
+      if (!valid[i]) {
+        const int idx = batch_idx[i];
+        return "wrong signature (#" + std::to_string(idx) + "): " + HexUpper(commit.signatures[(size_t)idx].String());
+      }
+    }
+    return std::string("BUG: batch verification failed with no invalid signatures");
+  }
+
+  Error VerifySingle(const std::string &chain_id, const ValidatorSet &vals, const Commit &commit, int64_t needed,
+                     SigPred ignore, SigPred count, bool count_all, bool by_index) const {
+    int64_t tallied = 0;
+    std::unordered_map<int32_t, int> seen;
+    for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
+      const CommitSig &cs = commit.signatures[idx];
+      if (ignore(cs)) continue;
+      const Validator *val;
+      if (by_index) {
+        val = &vals.validators[idx];
+      } else {
+        auto [vi, v] = vals.GetByAddress(cs.validator_address);
+        if (!v) continue;
+        auto it = seen.find(vi);
+        if (it != seen.end())
+          return "double vote from " + v->String() + " (" + std::to_string(it->second) + " and " +
+                 std::to_string(idx) + ")";
+        seen[vi] = (int)idx;
+        val = v;
+      }
+      Bytes sb = commit.VoteSignBytes(chain_id, (int32_t)idx);
+      if (!verify_single(val->pub_key, sb, cs.signature))
+        return "wrong signature (#" + std::to_string(idx) + "): " + HexUpper(cs.signature);
+      if (count(cs)) tallied += val->voting_power;
+      if (!count_all && tallied > needed) return std::nullopt;
+    }
+    if (tallied <= needed) return ErrNotEnoughVotingPowerSigned(tallied, needed);
+    return std::nullopt;
+  }
+
+  static Error VerifyBasic(const ValidatorSet *vals, const Commit *commit, int64_t height, const BlockID &block_id) {
+    if (!vals) return std::string("nil validator set");
+    if (!commit) return std::string("nil commit");
+    if (vals->Size() != commit->signatures.size()) return ErrInvalidCommitSignatures(vals->Size(), commit->signatures.size());
+    if (height != commit->height) return ErrInvalidCommitHeight(height, commit->height);
+    if (!block_id.Equals(commit->block_id))
+      return "invalid commit -- wrong block ID: want " + block_id.String() + ", got " + commit->block_id.String();
+    return std::nullopt;
+  }
+
+  static bool IgnoreAbsent(const CommitSig &c) { return c.block_id_flag == BlockIDFlagAbsent; }
+  static bool CountCommit(const CommitSig &c) { return c.block_id_flag == BlockIDFlagCommit; }
+  static bool IgnoreNotCommit(const CommitSig &c) { return c.block_id_flag != BlockIDFlagCommit; }
+  static bool CountAll(const CommitSig &) { return true; }
+
+  // types/validation.go:27-53
+  Error VerifyCommit(const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id, int64_t height,
+                     const Commit *commit) const {
+    if (Error e = VerifyBasic(vals, commit, height, block_id)) return e;
+    const int64_t needed = vals->TotalVotingPower() * 2 / 3;
+    if (ShouldBatchVerify(*vals, *commit))
+      return VerifyBatch(chain_id, *vals, *commit, needed, IgnoreAbsent, CountCommit, true, true);
+    return VerifySingle(chain_id, *vals, *commit, needed, IgnoreAbsent, CountCommit, true, true);
+  }
+
+  // types/validation.go:61-86
+  Error VerifyCommitLight(const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id,
+                          int64_t height, const Commit *commit) const {
+    if (Error e = VerifyBasic(vals, commit, height, block_id)) return e;
+    const int64_t needed = vals->TotalVotingPower() * 2 / 3;
+    if (ShouldBatchVerify(*vals, *commit))
+      return VerifyBatch(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, true);
+    return VerifySingle(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, true);
+  }
+
+  // types/validation.go:96-132
+  Error VerifyCommitLightTrusting(const std::string &chain_id, const ValidatorSet *vals, const Commit *commit,
+                                  int64_t num, int64_t den) const {
+    if (!vals) return std::string("nil validator set");
+    if (den == 0) return std::string("trustLevel has zero Denominator");
+    if (!commit) return std::string("nil commit");
+    auto [prod, overflow] = SafeMul(vals->TotalVotingPower(), num);
+    if (overflow)
+      return std::string(
+          "int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator");
+    const int64_t needed = prod / den;
+    if (ShouldBatchVerify(*vals, *commit))
+      return VerifyBatch(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, false);
+    return VerifySingle(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, false);
+  }
+};
+
+}  // namespace tmh

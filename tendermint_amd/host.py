@@ -1,0 +1,246 @@
+"""Python view of the C++ host layer (include/tmhost.h): the types the
+reference's commit verification works on, and thin ctypes calls into
+libtmgpu.so's tmv_verify_commit / tmv_vote_sign_bytes / tmv_batch_*.
+
+Mirrors (names and argument meaning):
+  crypto.BatchVerifier / batch.CreateBatchVerifier  -> BatchVerifier / create_batch_verifier
+  types.VerifyCommit / VerifyCommitLight / VerifyCommitLightTrusting
+                                                   -> verify_commit / verify_commit_light /
+                                                      verify_commit_light_trusting
+Errors are returned as strings (None = ok), byte-identical to the Go error
+text; infrastructure failures raise NativeError.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+from . import _native
+from ._native import NativeError, TMV_KIND_ED25519, TMV_KIND_SR25519
+
+KIND_OTHER = 255
+BLOCK_ID_FLAG_ABSENT, BLOCK_ID_FLAG_COMMIT, BLOCK_ID_FLAG_NIL = 1, 2, 3
+MODE_FULL, MODE_LIGHT, MODE_LIGHT_TRUSTING = 0, 1, 2
+ZERO_TIME = (-62135596800, 0)
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class CBlockID(ctypes.Structure):
+    _fields_ = [("hash", _u8p), ("hash_len", ctypes.c_uint32), ("psh_total", ctypes.c_uint32),
+                ("psh_hash", _u8p), ("psh_hash_len", ctypes.c_uint32)]
+
+
+class CValidator(ctypes.Structure):
+    _fields_ = [("address", _u8p), ("address_len", ctypes.c_uint32), ("pub_key", _u8p),
+                ("pub_key_len", ctypes.c_uint32), ("key_kind", ctypes.c_uint8), ("voting_power", ctypes.c_int64),
+                ("proposer_priority", ctypes.c_int64)]
+
+
+class CCommitSig(ctypes.Structure):
+    _fields_ = [("block_id_flag", ctypes.c_uint8), ("validator_address", _u8p),
+                ("validator_address_len", ctypes.c_uint32), ("ts_seconds", ctypes.c_int64),
+                ("ts_nanos", ctypes.c_int32), ("signature", _u8p), ("signature_len", ctypes.c_uint32)]
+
+
+class CCommit(ctypes.Structure):
+    _fields_ = [("height", ctypes.c_int64), ("round", ctypes.c_int32), ("block_id", CBlockID),
+                ("sigs", ctypes.POINTER(CCommitSig)), ("n_sigs", ctypes.c_uint32)]
+
+
+@dataclass
+class BlockID:
+    hash: bytes = b""
+    psh_total: int = 0
+    psh_hash: bytes = b""
+
+    def equals(self, o: "BlockID") -> bool:
+        return (self.hash, self.psh_total, self.psh_hash) == (o.hash, o.psh_total, o.psh_hash)
+
+
+@dataclass
+class Validator:
+    address: bytes
+    pub_key: bytes
+    voting_power: int
+    key_kind: int = TMV_KIND_ED25519
+    proposer_priority: int = 0
+
+
+@dataclass
+class ValidatorSet:
+    validators: List[Validator]
+    proposer_index: int = -1
+
+    def total_voting_power(self) -> int:
+        return sum(v.voting_power for v in self.validators)
+
+
+@dataclass
+class CommitSig:
+    block_id_flag: int = BLOCK_ID_FLAG_ABSENT
+    validator_address: bytes = b""
+    timestamp: Tuple[int, int] = ZERO_TIME
+    signature: bytes = b""
+
+
+@dataclass
+class Commit:
+    height: int
+    round: int
+    block_id: BlockID
+    signatures: List[CommitSig] = field(default_factory=list)
+
+
+class _Keep:
+    """Holds the ctypes buffers alive for the duration of a call."""
+
+    def __init__(self):
+        self.refs = []
+
+    def buf(self, b: bytes):
+        if not b:
+            return None, 0
+        a = (ctypes.c_uint8 * len(b)).from_buffer_copy(b)
+        self.refs.append(a)
+        return ctypes.cast(a, _u8p), len(b)
+
+
+def _c_block_id(k: _Keep, b: BlockID) -> CBlockID:
+    h, hl = k.buf(b.hash)
+    p, pl = k.buf(b.psh_hash)
+    return CBlockID(h, hl, b.psh_total, p, pl)
+
+
+def _setup(L):
+    if getattr(L, "_tmhost_ready", False):
+        return L
+    L.tmv_vote_sign_bytes.restype = ctypes.c_size_t
+    L.tmv_vote_sign_bytes.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.POINTER(CBlockID), ctypes.c_int64, ctypes.c_int32, _u8p, ctypes.c_size_t]
+    L.tmv_verify_commit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(CValidator),
+                                    ctypes.c_uint32, ctypes.c_int32, ctypes.POINTER(CBlockID), ctypes.c_int64,
+                                    ctypes.POINTER(CCommit), ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p,
+                                    ctypes.c_size_t]
+    L.tmv_batch_new.restype = ctypes.c_void_p
+    L.tmv_batch_new.argtypes = [ctypes.c_void_p, ctypes.c_uint8]
+    L.tmv_batch_add.argtypes = [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    L.tmv_batch_len.restype = ctypes.c_size_t
+    L.tmv_batch_len.argtypes = [ctypes.c_void_p]
+    L.tmv_batch_verify.argtypes = [ctypes.c_void_p, _u8p, ctypes.POINTER(ctypes.c_int64), ctypes.c_char_p,
+                                   ctypes.c_size_t]
+    L.tmv_batch_free.argtypes = [ctypes.c_void_p]
+    L._tmhost_ready = True
+    return L
+
+
+def vote_sign_bytes(chain_id: str, vote_type: int, height: int, round_: int, block_id: Optional[BlockID],
+                    timestamp: Tuple[int, int], lib=None) -> bytes:
+    """types.VoteSignBytes through the C++ encoder (tmv_vote_sign_bytes)."""
+    L = _setup(lib or _native.lib())
+    k = _Keep()
+    bid = ctypes.byref(_c_block_id(k, block_id)) if block_id is not None else None
+    out = (ctypes.c_uint8 * 512)()
+    n = L.tmv_vote_sign_bytes(chain_id.encode(), vote_type, height, round_, bid, timestamp[0], timestamp[1],
+                              ctypes.cast(out, _u8p), 512)
+    return bytes(out[:n])
+
+
+def _commit_call(fn, ctx_handle, mode, chain_id, vals: Optional[ValidatorSet], block_id: Optional[BlockID],
+                 height: int, commit: Optional[Commit], trust: Tuple[int, int]) -> Optional[str]:
+    k = _Keep()
+    cvals, nv, prop = None, 0, -1
+    if vals is not None:
+        arr = (CValidator * max(1, len(vals.validators)))()
+        for i, v in enumerate(vals.validators):
+            a, al = k.buf(v.address)
+            p, pl = k.buf(v.pub_key)
+            arr[i] = CValidator(a, al, p, pl, v.key_kind, v.voting_power, v.proposer_priority)
+        k.refs.append(arr)
+        cvals, nv, prop = arr, len(vals.validators), vals.proposer_index
+    ccommit = None
+    if commit is not None:
+        sigs = (CCommitSig * max(1, len(commit.signatures)))()
+        for i, s in enumerate(commit.signatures):
+            a, al = k.buf(s.validator_address)
+            g, gl = k.buf(s.signature)
+            sigs[i] = CCommitSig(s.block_id_flag, a, al, s.timestamp[0], s.timestamp[1], g, gl)
+        k.refs.append(sigs)
+        cc = CCommit(commit.height, commit.round, _c_block_id(k, commit.block_id), sigs, len(commit.signatures))
+        k.refs.append(cc)
+        ccommit = ctypes.byref(cc)
+    bid = ctypes.byref(_c_block_id(k, block_id)) if block_id is not None else None
+    err = ctypes.create_string_buffer(4096)
+    rc = fn(ctx_handle, mode, chain_id.encode(), cvals, nv, prop, bid, height, ccommit, trust[0], trust[1], err,
+            len(err))
+    if rc < 0:
+        raise NativeError(f"commit verification failed ({rc}): {err.value.decode(errors='replace')}")
+    return err.value.decode() if rc == 1 else None
+
+
+def verify_commit(ctx, chain_id: str, vals, block_id, height, commit) -> Optional[str]:
+    L = _setup(_native.lib())
+    return _commit_call(L.tmv_verify_commit, ctx.handle, MODE_FULL, chain_id, vals, block_id, height, commit, (0, 1))
+
+
+def verify_commit_light(ctx, chain_id: str, vals, block_id, height, commit) -> Optional[str]:
+    L = _setup(_native.lib())
+    return _commit_call(L.tmv_verify_commit, ctx.handle, MODE_LIGHT, chain_id, vals, block_id, height, commit, (0, 1))
+
+
+def verify_commit_light_trusting(ctx, chain_id: str, vals, commit, trust_level=(1, 3)) -> Optional[str]:
+    L = _setup(_native.lib())
+    return _commit_call(L.tmv_verify_commit, ctx.handle, MODE_LIGHT_TRUSTING, chain_id, vals, None, 0, commit,
+                        trust_level)
+
+
+class BatchVerifier:
+    """crypto.BatchVerifier over tmv_batch_* (crypto/crypto.go:66-76)."""
+
+    def __init__(self, ctx, key_kind: int):
+        self._L = _setup(_native.lib())
+        self._h = self._L.tmv_batch_new(ctx.handle, key_kind)
+        if not self._h:
+            raise NativeError("no batch verifier for this key type")
+        self.deferred_add_error: Optional[Tuple[int, str]] = None
+
+    def add(self, key_kind: int, pub_key: bytes, msg: bytes, sig: bytes) -> Optional[str]:
+        err = ctypes.create_string_buffer(512)
+        rc = self._L.tmv_batch_add(self._h, key_kind, pub_key, len(pub_key), msg, len(msg), sig, len(sig), err, 512)
+        if rc < 0:
+            raise NativeError("tmv_batch_add failed")
+        return err.value.decode() if rc == 1 else None
+
+    def __len__(self):
+        return self._L.tmv_batch_len(self._h)
+
+    def verify(self) -> Tuple[bool, List[bool]]:
+        n = len(self)
+        out = (ctypes.c_uint8 * max(1, n))()
+        idx = ctypes.c_int64(-1)
+        err = ctypes.create_string_buffer(512)
+        rc = self._L.tmv_batch_verify(self._h, ctypes.cast(out, _u8p), ctypes.byref(idx), err, 512)
+        if rc < 0:
+            raise NativeError(f"tmv_batch_verify failed ({rc}): {err.value.decode(errors='replace')}")
+        self.deferred_add_error = (idx.value, err.value.decode()) if rc == 2 else None
+        return rc == 1, [bool(out[i]) for i in range(n)]
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._L.tmv_batch_free(self._h)
+        except Exception:
+            pass
+
+
+def create_batch_verifier(ctx, key_kind: int) -> Optional[BatchVerifier]:
+    """batch.CreateBatchVerifier: None for key types without batch support."""
+    if key_kind not in (TMV_KIND_ED25519, TMV_KIND_SR25519):
+        return None
+    return BatchVerifier(ctx, key_kind)
+
+
+def supports_batch_verifier(key_kind: int) -> bool:
+    return key_kind in (TMV_KIND_ED25519, TMV_KIND_SR25519)

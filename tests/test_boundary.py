@@ -8,7 +8,7 @@ from tendermint_amd import _native
 
 
 def _declared():
-    src = open(_native.HEADER_PATH).read()
+    src = "".join(open(p).read() for p in _native.HEADER_PATHS)
     return sorted(set(re.findall(r"\b(tmv_[a-z0-9_]+)\s*\(", src)))
 
 
