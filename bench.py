@@ -34,6 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from tendermint_amd import _native as N  # noqa: E402
+from tendermint_amd.shard import all_gather_validity  # noqa: E402
 from tendermint_amd.testing.factory import make_c2_batch, make_commit_batch  # noqa: E402
 
 METRIC = "ed25519 verifies/sec at 1/2/4/8 GPUs + p50 VerifyCommit latency, 150 vals"
@@ -110,10 +111,7 @@ def main():
     d_msg = torch.from_numpy(batch.msg).to(dev)
     d_off = torch.from_numpy(batch.off.view(np.int32)).to(dev)
     d_valid = torch.zeros(n, dtype=torch.uint8, device=dev)
-    nbytes_bitmap = (n + 7) // 8
-    weights = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=dev)
-    pad = nbytes_bitmap * 8 - n
-    gathered = [torch.zeros(nbytes_bitmap, dtype=torch.uint8, device=dev) for _ in range(world)]
+    counts = [n] * world
     stream = torch.cuda.Stream(dev)
     sp = stream.cuda_stream
 
@@ -126,9 +124,7 @@ def main():
             if ev_pair is not None:
                 ev_pair[1].record(stream)
             if world > 1:
-                v = torch.nn.functional.pad(d_valid, (0, pad)).view(-1, 8).to(torch.int32)
-                bitmap = (v * weights).sum(1).to(torch.uint8)
-                dist.all_gather(gathered, bitmap)
+                all_gather_validity(d_valid, counts)
 
     for _ in range(args.warmup):
         step()
