@@ -103,6 +103,19 @@ TMV_HD void fe_carry(fe &h, const fe &f) {
   fe_carry_wide(h, c);
 }
 
+// 19 x as two full-rate shift-adds (v_mul_lo_u32 is quarter rate on CDNA4)
+// (the compiler folds plain shift-adds back into v_mul_lo_u32, hence asm)
+TMV_HD int32_t mul19(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int32_t t, r;
+  asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(t) : "v"(x));
+  asm("v_lshl_add_u32 %0, %1, 4, %2" : "=v"(r) : "v"(x), "v"(t));
+  return r;
+#else
+  return (int32_t)((uint32_t)x * 19u);
+#endif
+}
+
 // h = f * g.  Column k collects f_i g_j with i+j == k, plus 19 f_i g_j for
 // i+j == k+10 (2^255 == 19).  Odd*odd limb products carry an extra factor 2
 // (25.5-bit radix).
@@ -112,7 +125,7 @@ TMV_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   int32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    g19[i] = 19 * g.v[i];
+    g19[i] = mul19(g.v[i]);
     f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
   }
   int64_t c[10];
@@ -135,7 +148,7 @@ TMV_HD void fe_sq(fe &h, const fe &f) {
   TMV_ASSERT_LEVEL(f, 3);
   int32_t f2[10], f19[10];
 #pragma unroll
-  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = 19 * f.v[i]; }
+  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = mul19(f.v[i]); }
   int64_t c[10];
 #pragma unroll
   for (int k = 0; k < 10; k++) c[k] = 0;

@@ -22,7 +22,7 @@ constexpr int qp(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | 
 template <int CTRL>
 TMV_DEV void fe_dpp(fe &h, const fe &f) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = __builtin_amdgcn_mov_dpp(f.v[i], CTRL, 0xF, 0xF, false);
+  for (int i = 0; i < 10; i++) h.v[i] = __builtin_amdgcn_mov_dpp(f.v[i], CTRL, 0xF, 0xF, true);
 }
 
 // h = s * f for a per-lane s in {-1, 0, +1}
@@ -37,7 +37,7 @@ TMV_DEV void fe_signed(fe &h, const fe &f, int s) {
 TMV_DEV void fe_sq_shift(fe &h, const fe &f, int sh) {
   int32_t f2[10], f19[10];
 #pragma unroll
-  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = 19 * f.v[i]; }
+  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = mul19(f.v[i]); }
   int64_t c[10];
 #pragma unroll
   for (int k = 0; k < 10; k++) c[k] = 0;

@@ -115,13 +115,25 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipMalloc(btable)", e); return TMV_ERR_NOMEM; }
   e = hipMemcpy(d.d_btable, table.data(), bytes, hipMemcpyHostToDevice);
   if (e != hipSuccess) { set_error("hipMemcpy(btable)", e); return TMV_ERR_NO_DEVICE; }
-  // quad B table: entry m = (m+1)B as (ymx, ypx, xy2d, 1)
-  std::vector<tmv::fe> bq(32);
-  for (int m = 0; m < 8; m++) {
-    bq[4 * m + 0] = table[m].ymx;
-    bq[4 * m + 1] = table[m].ypx;
-    bq[4 * m + 2] = table[m].xy2d;
-    tmv::fe_one(bq[4 * m + 3]);
+  // quad B table: entry m = (m+1)B, m < kBaseQuadEntries, as (ymx, ypx, xy2d, 1)
+  std::vector<tmv::fe> bq(4 * tmv::kBaseQuadEntries);
+  {
+    tmv::ge_p3 B, P;
+    tmv::ed25519_base_point(B);
+    tmv::ge_cached bc;
+    tmv::ge_p3_to_cached(bc, B);
+    P = B;
+    for (int m = 0; m < tmv::kBaseQuadEntries; m++) {
+      tmv::ge_precomp pc;
+      tmv::ge_p3_to_precomp(pc, P);
+      bq[4 * m + 0] = pc.ymx;
+      bq[4 * m + 1] = pc.ypx;
+      bq[4 * m + 2] = pc.xy2d;
+      tmv::fe_one(bq[4 * m + 3]);
+      tmv::ge_p1p1 t;
+      tmv::ge_add(t, P, bc);
+      tmv::ge_p1p1_to_p3(P, t);
+    }
   }
   e = hipMalloc(&d.d_btab_q, bq.size() * sizeof(tmv::fe));
   if (e != hipSuccess) { set_error("hipMalloc(btab_q)", e); return TMV_ERR_NOMEM; }

@@ -8,6 +8,7 @@ namespace tmv {
 
 constexpr int kVerifyBlock = 256;
 constexpr int kQuadBlock = 64;    // one wave = 16 signatures per block
+constexpr int kBaseQuadEntries = 128;  // (m+1)B, m < 128, CachedQ layout (20 KB)
 
 // Per-signature workspace of the latency path (device memory).
 struct Ed25519Work {

@@ -142,10 +142,26 @@ __device__ __forceinline__ void recode16_store(int8_t *dst, const uint32_t s[8],
   }
 }
 
+// Signed radix-256 recoding (32 digits in [-128, 127], top digit absorbs the
+// carry) for the fixed base B, written to LDS.
+__device__ __forceinline__ void recode256_store(int8_t *dst, const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    int e = (int)((s[i >> 2] >> (8 * (i & 3))) & 255) + carry;
+    if (i < 31) {
+      carry = (e + 128) >> 8;
+      e -= carry * 256;
+    }
+    dst[i] = (int8_t)e;
+  }
+}
+
 constexpr int kQuadSigs = kQuadBlock / 4;
 
 // k_verify_quad: acc = sum over 64 signed radix-16 windows of
-// 16*acc + e_i(k)(-A) + e_i(s)B (Straus, shared doublings), then
+// 16*acc + e_i(k)(-A) [+ d_{i/2}(s)B on even windows, radix-256 digits of s
+// against a 128-entry table of B multiples] (Straus, shared doublings), then
 //   ed25519: [8](acc - R) == O          (ZIP-215 cofactored)
 //   sr25519: acc == R (Ristretto equality)
 // Each signature occupies one quad; writes out[i] (ed25519 1/0; sr25519
@@ -155,7 +171,7 @@ __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned) {
   __shared__ fe tabA[kQuadSigs * 8 * 4];
-  __shared__ fe tabB[8 * 4];
+  __shared__ fe tabB[kBaseQuadEntries * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
   const uint32_t m = entry_count(count_ptr, n);
   if (blockIdx.x * kQuadSigs >= m) return;  // block-uniform
@@ -165,7 +181,7 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   const bool live = raw < m;
   const uint32_t e = live ? raw : m - 1;
   const uint32_t i = idx ? idx[e] : e;
-  for (int t = threadIdx.x; t < 32; t += kQuadBlock) tabB[t] = btab_q[t];
+  for (int t = threadIdx.x; t < kBaseQuadEntries * 4; t += kQuadBlock) tabB[t] = btab_q[t];
 
   uint32_t s_raw[8], s_w[8];
   if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
@@ -185,10 +201,10 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
     const uint4 k0 = kp[0], k1 = kp[1];
     k_w[0] = k0.x; k_w[1] = k0.y; k_w[2] = k0.z; k_w[3] = k0.w;
     k_w[4] = k1.x; k_w[5] = k1.y; k_w[6] = k1.z; k_w[7] = k1.w;
-    uint32_t sc[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) sc[t] = (c & 1) ? s_w[t] : k_w[t];
-    recode16_store(&dig[q][c & 1][0], sc, c < 2);
+    // lane 0: k in signed radix 16 (64 digits); lane 1: s in signed radix 256
+    // (32 digits, |d| <= 128, top digit <= 32 since s < 2^253)
+    if (c == 1) recode256_store(&dig[q][1][0], s_w);
+    else recode16_store(&dig[q][0][0], k_w, c == 0);
   }
   const bool a_ok = w.flags[4 * e] != 0;
   const bool r_ok = w.flags[4 * e + 1] != 0;
@@ -221,7 +237,6 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
       }
     }
     const int da = dig[q][0][wdx];
-    const int db = dig[q][1][wdx];
     fe ent, idq;
     quad::cached_identity(idq);
     const int aa = da < 0 ? -da : da;
@@ -230,12 +245,15 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
     quad::cached_cneg(ent, da < 0);
     quad::add(r, acc, ent);
     quad::p1p1_to_p3(acc, r);
-    const int ab = db < 0 ? -db : db;
-    ent = tabB[(ab ? ab - 1 : 0) * 4 + c];
-    fe_cmov(ent, idq, ab == 0);
-    quad::cached_cneg(ent, db < 0);
-    quad::add(r, acc, ent);
-    quad::p1p1_to_p3(acc, r);
+    if ((wdx & 1) == 0) {  // B digit d_j weighs 256^j = 16^(2j)
+      const int db = dig[q][1][wdx >> 1];
+      const int ab = db < 0 ? -db : db;
+      ent = tabB[(ab ? ab - 1 : 0) * 4 + c];
+      fe_cmov(ent, idq, ab == 0);
+      quad::cached_cneg(ent, db < 0);
+      quad::add(r, acc, ent);
+      quad::p1p1_to_p3(acc, r);
+    }
   }
   int status;
   if (SR) {
