@@ -86,6 +86,23 @@ int tmv_sr25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig
 int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
                            const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out);
 
+/* Batch verification with options.  flags:
+ *   TMV_FLAG_KEY_CACHE  keep expanded public keys on the device (LRU of
+ *   TMV_KEY_CACHE_CAPACITY keys per device, default 4,096 = voi's cache size,
+ *   crypto/ed25519/ed25519.go:31,56).  A cached key is a 64-row comb of -A
+ *   (80 KB), so [k]A needs no doublings; the first batch that sees a key
+ *   pays its table build.  Batches with more distinct keys than the cache
+ *   holds take the uncached path transparently.  Results are identical
+ *   either way.
+ * Replaces the caching verifier behind crypto/ed25519/ed25519.go:173-233
+ * (ed25519) and crypto/sr25519/batch.go:23-47 (sr25519).  status_out as for
+ * tmv_sr25519_verify_batch (ed25519 entries are 1/0). */
+#define TMV_FLAG_KEY_CACHE 1u
+int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const uint8_t *pk, const uint8_t *sig,
+                        const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out);
+/* Cumulative key-cache counters over the context's devices. */
+int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t *used, uint32_t *capacity);
+
 /* Device-resident variants: every pointer is device memory on HIP device
  * `device` (inputs already in HBM), `stream` is a hipStream_t (NULL = the
  * context's own stream for that device).  Asynchronous: the call enqueues the

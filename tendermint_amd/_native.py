@@ -27,12 +27,14 @@ TMV_SR_ADDERR_PUBKEY = -1
 TMV_SR_ADDERR_SIG = -2
 TMV_KIND_ED25519 = 0
 TMV_KIND_SR25519 = 1
+TMV_FLAG_KEY_CACHE = 1
 
 # Every symbol include/tmverify.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
     "tmv_open", "tmv_close", "tmv_num_devices", "tmv_last_error", "tmv_version",
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
+    "tmv_verify_batch_ex", "tmv_key_cache_stats",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_verify_commit",
@@ -77,6 +79,10 @@ def lib() -> ctypes.CDLL:
         L.tmv_ed25519_verify.argtypes = [vp, u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
         L.tmv_sr25519_verify_batch.argtypes = [vp, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
         L.tmv_verify_mixed_batch.argtypes = [vp, u8p, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
+        L.tmv_verify_batch_ex.argtypes = [vp, ctypes.c_uint8, ctypes.c_uint32, u8p, u8p, u8p, u32p, ctypes.c_uint32,
+                                          i8p]
+        L.tmv_key_cache_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.tmv_ed25519_verify_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         L.tmv_verify_mixed_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         _lib = L
@@ -166,6 +172,24 @@ class Context:
                                                           _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
                          "tmv_verify_mixed_batch")
         return rc == TMV_ALL_VALID, out[:n]
+
+    def verify_batch_ex(self, key_kind: int, flags: int, pk, sig, msg, off):
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), np.int8)
+        msg = msg if len(msg) else np.zeros(1, np.uint8)
+        pk = pk if len(pk) else np.zeros(1, np.uint8)
+        sig = sig if len(sig) else np.zeros(1, np.uint8)
+        rc = self._check(self._lib.tmv_verify_batch_ex(self._h, key_kind, flags, _p(pk), _p(sig), _p(msg),
+                                                       _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
+                         "tmv_verify_batch_ex")
+        return rc == TMV_ALL_VALID, out[:n]
+
+    def key_cache_stats(self):
+        h, m = ctypes.c_uint64(), ctypes.c_uint64()
+        u, c = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self._lib.tmv_key_cache_stats(self._h, ctypes.byref(h), ctypes.byref(m), ctypes.byref(u),
+                                                  ctypes.byref(c)), "tmv_key_cache_stats")
+        return {"hits": h.value, "misses": m.value, "used": u.value, "capacity": c.value}
 
     def ed25519_verify_batch_device(self, device: int, d_pk: int, d_sig: int, d_msg: int, d_off: int, n: int,
                                     d_valid: int, stream: int = 0) -> None:

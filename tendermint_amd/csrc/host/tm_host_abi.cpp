@@ -80,13 +80,12 @@ class GpuBatch : public tmh::BatchVerifier {
     if (n == 0) return {false, valid};
     std::vector<uint8_t> out(n);
     int rc;
-    if (kind_ == tmh::KeyType::Ed25519) {
-      rc = tmv_ed25519_verify_batch(ctx_, pk_.data(), sig_.data(), msg_.empty() ? nullptr : msg_.data(),
-                                    off_.data(), n, out.data());
-    } else {
-      rc = tmv_sr25519_verify_batch(ctx_, pk_.data(), sig_.data(), msg_.empty() ? nullptr : msg_.data(),
-                                    off_.data(), n, reinterpret_cast<int8_t *>(out.data()));
-    }
+    // Validator keys repeat across commits: use the device key cache (the
+    // reference's LRU caching verifier, crypto/ed25519/ed25519.go:31).
+    static const uint8_t z = 0;
+    rc = tmv_verify_batch_ex(ctx_, kind_ == tmh::KeyType::Ed25519 ? TMV_KIND_ED25519 : TMV_KIND_SR25519,
+                             TMV_FLAG_KEY_CACHE, pk_.data(), sig_.data(), msg_.empty() ? &z : msg_.data(),
+                             off_.data(), n, reinterpret_cast<int8_t *>(out.data()));
     if (rc < 0) {
       infra_error_ = rc;
       return {false, valid};

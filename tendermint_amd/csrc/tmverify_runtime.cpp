@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <list>
+#include <unordered_map>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -64,6 +66,17 @@ struct Device {
   tmv::strobe_t *d_prefix = nullptr;     // sr25519 transcript prefix (empty context)
   DeviceBuf d_in, d_out, h_in, h_out, d_work, d_work2, d_idx;
   hipEvent_t work_done = nullptr;        // orders workspace reuse across streams
+  tmv::fe *d_bcomb = nullptr;            // 32 x 128 CachedQ: (m+1) 256^j B (key-cached path)
+  // expanded-key cache (device table + host LRU index)
+  tmv::KeyTable kt{nullptr, nullptr};
+  uint32_t kcap = 0;
+  std::unordered_map<std::string, uint32_t> kmap;  // kind byte + 32 key bytes -> slot
+  std::list<uint32_t> klru;                         // front = most recently used
+  std::vector<std::list<uint32_t>::iterator> kpos;
+  std::vector<std::string> kslot_key;
+  std::vector<uint64_t> kslot_epoch;
+  uint64_t kepoch = 0, khits = 0, kmisses = 0;
+  DeviceBuf d_kbuild, h_kbuild;
   std::mutex mu;
 };
 
@@ -147,6 +160,126 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipMemcpy(prefix)", e); return TMV_ERR_NO_DEVICE; }
   e = hipEventCreateWithFlags(&d.work_done, hipEventDisableTiming);
   if (e != hipSuccess) { set_error("hipEventCreate", e); return TMV_ERR_NO_DEVICE; }
+  // base comb for the key-cached path: row j, entry m = (m+1) 256^j B (CachedQ, Z kept)
+  {
+    std::vector<tmv::fe> bc((size_t)32 * tmv::kBaseQuadEntries * 4);
+    tmv::ge_p3 row, P;
+    tmv::ed25519_base_point(row);
+    for (int j = 0; j < 32; j++) {
+      tmv::ge_cached rc;
+      tmv::ge_p3_to_cached(rc, row);
+      P = row;
+      for (int m = 0; m < tmv::kBaseQuadEntries; m++) {
+        tmv::ge_cached c;
+        tmv::ge_p3_to_cached(c, P);
+        tmv::fe *o = &bc[((size_t)j * tmv::kBaseQuadEntries + m) * 4];
+        tmv::fe_carry(o[0], c.YmX);
+        tmv::fe_carry(o[1], c.YpX);
+        o[2] = c.T2d;
+        o[3] = c.Z;
+        tmv::ge_p1p1 t;
+        tmv::ge_add(t, P, rc);
+        tmv::ge_p1p1_to_p3(P, t);
+      }
+      for (int d = 0; d < 8; d++) {  // row *= 256
+        tmv::ge_p1p1 t;
+        tmv::ge_p3_dbl(t, row);
+        tmv::ge_p1p1_to_p3(row, t);
+      }
+    }
+    e = hipMalloc(&d.d_bcomb, bc.size() * sizeof(tmv::fe));
+    if (e != hipSuccess) { set_error("hipMalloc(bcomb)", e); return TMV_ERR_NOMEM; }
+    e = hipMemcpy(d.d_bcomb, bc.data(), bc.size() * sizeof(tmv::fe), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { set_error("hipMemcpy(bcomb)", e); return TMV_ERR_NO_DEVICE; }
+  }
+  const char *kc = getenv("TMV_KEY_CACHE_CAPACITY");
+  d.kcap = kc ? (uint32_t)strtoul(kc, nullptr, 10) : 4096u;  // voi's LRU size (crypto/ed25519/ed25519.go:56)
+  return 0;
+}
+
+// Resolve the key slot of every entry, building the comb tables of missing
+// keys on the device.  Returns 1 if the batch has more distinct keys than the
+// cache holds (caller uses the uncached path), 0 on success, < 0 on error.
+// Caller holds d.mu.  slots_out: n entries (host memory).
+static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint32_t *slots_out, hipStream_t s) {
+  if (d.kcap == 0) return 1;
+  hipError_t e;
+  if (!d.kt.tab) {
+    if ((e = hipMalloc(&d.kt.tab, (size_t)d.kcap * tmv::KeyTable::bytes_per_key())) != hipSuccess) {
+      set_error("hipMalloc(key table)", e);
+      d.kt.tab = nullptr;
+      return 1;  // no room: fall back to the uncached path
+    }
+    if ((e = hipMalloc(&d.kt.ok, d.kcap)) != hipSuccess) { set_error("hipMalloc(key ok)", e); return TMV_ERR_NOMEM; }
+    d.kpos.resize(d.kcap);
+    d.kslot_key.resize(d.kcap);
+    d.kslot_epoch.assign(d.kcap, 0);
+  }
+  const uint64_t epoch = ++d.kepoch;
+  std::vector<uint32_t> miss_idx;
+  std::vector<uint32_t> miss_slot;
+  std::string key(33, '\0');
+  key[0] = sr ? 1 : 0;
+  uint32_t distinct = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    std::memcpy(&key[1], pk + 32ull * i, 32);
+    auto it = d.kmap.find(key);
+    uint32_t slot;
+    if (it != d.kmap.end()) {
+      slot = it->second;
+      if (d.kslot_epoch[slot] != epoch) {
+        d.kslot_epoch[slot] = epoch;
+        distinct++;
+        d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
+        d.khits++;
+      }
+    } else {
+      if (++distinct > d.kcap) return 1;
+      if (d.kmap.size() < d.kcap) {
+        slot = (uint32_t)d.kmap.size();
+        d.klru.push_front(slot);
+      } else {
+        slot = d.klru.back();  // least recently used; never one pinned by this batch
+        if (d.kslot_epoch[slot] == epoch) return 1;
+        d.kmap.erase(d.kslot_key[slot]);
+        d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
+      }
+      d.kpos[slot] = d.klru.begin();
+      d.kslot_key[slot] = key;
+      d.kslot_epoch[slot] = epoch;
+      d.kmap[key] = slot;
+      miss_idx.push_back(i);
+      miss_slot.push_back(slot);
+      d.kmisses++;
+    }
+    slots_out[i] = slot;
+  }
+  const uint32_t m = (uint32_t)miss_idx.size();
+  if (m) {
+    const size_t bytes = 32ull * m + 4ull * m + 64;
+    if ((e = d.h_kbuild.ensure(bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+    if (bytes > d.d_kbuild.cap) {
+      (void)hipEventSynchronize(d.work_done);
+      if ((e = d.d_kbuild.ensure(bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+    }
+    (void)hipStreamWaitEvent(s, d.work_done, 0);
+    uint8_t *h = static_cast<uint8_t *>(d.h_kbuild.ptr);
+    for (uint32_t t = 0; t < m; t++) std::memcpy(h + 32ull * t, pk + 32ull * miss_idx[t], 32);
+    const size_t soff = (32ull * m + 15) & ~size_t(15);
+    std::memcpy(h + soff, miss_slot.data(), 4ull * m);
+    if ((e = hipMemcpyAsync(d.d_kbuild.ptr, h, soff + 4ull * m, hipMemcpyHostToDevice, s)) != hipSuccess) {
+      set_error("hipMemcpyAsync(keys)", e);
+      return TMV_ERR_LAUNCH;
+    }
+    uint8_t *dk = static_cast<uint8_t *>(d.d_kbuild.ptr);
+    if ((e = tmv::launch_key_build(sr, dk, reinterpret_cast<uint32_t *>(dk + soff), m, d.kt, s)) != hipSuccess) {
+      set_error("k_key_build launch", e);
+      return TMV_ERR_LAUNCH;
+    }
+    // the pinned staging is reused by the next build: wait for this copy
+    (void)hipEventRecord(d.work_done, s);
+    (void)hipEventSynchronize(d.work_done);
+  }
   return 0;
 }
 
@@ -190,6 +323,17 @@ static int launch_mixed(Device &d, const uint8_t *kind, const uint8_t *pk, const
   hipError_t e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed,
                                           idx_sr, status, s);
   if (e != hipSuccess) { set_error("mixed launch", e); return TMV_ERR_LAUNCH; }
+  (void)hipEventRecord(d.work_done, s);
+  return 0;
+}
+
+static int launch_cached(Device &d, bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                         const uint32_t *off, const uint32_t *slots, uint32_t n, uint8_t *out, hipStream_t s) {
+  int rc = reserve_work(d, n, false, s);
+  if (rc != 0) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(d.d_work.ptr, n);
+  hipError_t e = tmv::launch_verify_cached(sr, pk, sig, msg, off, slots, n, d.kt, d.d_bcomb, d.d_prefix, w, out, s);
+  if (e != hipSuccess) { set_error("cached verify launch", e); return TMV_ERR_LAUNCH; }
   (void)hipEventRecord(d.work_done, s);
   return 0;
 }
@@ -252,6 +396,11 @@ void tmv_close(tmv_ctx *ctx) {
     d->d_out.release();
     d->d_work.release();
     d->d_work2.release();
+    d->d_kbuild.release();
+    d->h_kbuild.release();
+    if (d->kt.tab) (void)hipFree(d->kt.tab);
+    if (d->kt.ok) (void)hipFree(d->kt.ok);
+    if (d->d_bcomb) (void)hipFree(d->d_bcomb);
     d->d_idx.release();
     if (d->d_prefix) (void)hipFree(d->d_prefix);
     if (d->d_btab_q) (void)hipFree(d->d_btab_q);
@@ -268,7 +417,7 @@ int tmv_num_devices(const tmv_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0
 
 }  // extern "C"
 
-enum class Scheme { Ed25519, Sr25519, Mixed };
+enum class Scheme { Ed25519, Sr25519, Mixed, Ed25519Cached, Sr25519Cached };
 
 // Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
 // Layout: pk | sig | off | msg | kind (16-B aligned pieces).
@@ -277,8 +426,9 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
   const uint32_t n = hi - lo;
   const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
   Layout L(n, mbytes);
+  const bool cached = sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached;
   const size_t kind_at = L.total;
-  const size_t total = L.total + (sch == Scheme::Mixed ? align16(n) : 0);
+  const size_t total = L.total + (sch == Scheme::Mixed ? align16(n) : 0) + (cached ? align16(4ull * n) : 0);
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   if ((e = d.h_in.ensure(total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
@@ -293,6 +443,14 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
   for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
   if (mbytes) std::memcpy(h + L.msg, msg + base, mbytes);
   if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
+  if (cached) {
+    const int kr = resolve_keys(d, sch == Scheme::Sr25519Cached, pk + 32ull * lo, n,
+                                reinterpret_cast<uint32_t *>(h + kind_at), d.stream);
+    if (kr < 0) return kr;
+    if (kr == 1) {  // more distinct keys than the cache holds: uncached path
+      sch = sch == Scheme::Sr25519Cached ? Scheme::Sr25519 : Scheme::Ed25519;
+    }
+  }
   if ((e = hipMemcpyAsync(d.d_in.ptr, h, total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
@@ -307,6 +465,11 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
       break;
     case Scheme::Sr25519:
       rc = launch_sr25519(d, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out), d.stream);
+      break;
+    case Scheme::Ed25519Cached:
+    case Scheme::Sr25519Cached:
+      rc = launch_cached(d, sch == Scheme::Sr25519Cached, dd + L.pk, dd + L.sig, dd + L.msg, doff,
+                         reinterpret_cast<uint32_t *>(dd + kind_at), n, out, d.stream);
       break;
     default:
       rc = launch_mixed(d, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out),
@@ -375,6 +538,31 @@ int tmv_sr25519_verify_batch(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *sig
 int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
                            const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
   return run_batch(ctx, Scheme::Mixed, kind, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out));
+}
+
+int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const uint8_t *pk, const uint8_t *sig,
+                        const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
+  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0;
+  Scheme sch;
+  if (key_kind == TMV_KIND_ED25519) sch = cache ? Scheme::Ed25519Cached : Scheme::Ed25519;
+  else if (key_kind == TMV_KIND_SR25519) sch = cache ? Scheme::Sr25519Cached : Scheme::Sr25519;
+  else { set_error("unsupported key kind"); return TMV_ERR_ARG; }
+  return run_batch(ctx, sch, nullptr, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out));
+}
+
+int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t *used, uint32_t *capacity) {
+  if (!ctx) return TMV_ERR_ARG;
+  uint64_t h = 0, m = 0;
+  uint32_t u = 0, c = 0;
+  for (auto &d : ctx->devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    h += d->khits; m += d->kmisses; u += (uint32_t)d->kmap.size(); c += d->kcap;
+  }
+  if (hits) *hits = h;
+  if (misses) *misses = m;
+  if (used) *used = u;
+  if (capacity) *capacity = c;
+  return 0;
 }
 
 int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kind, const uint8_t *d_pk,

@@ -33,6 +33,21 @@ hipError_t launch_ed25519_verify_quad(const uint8_t *pk, const uint8_t *sig, con
                                       const uint32_t *msg_off, uint32_t n, const fe *btab_q, Ed25519Work w,
                                       uint8_t *valid, hipStream_t stream);
 
+// Device-resident expanded-key table (key-cached path).
+constexpr int kKeyRowsEntries = 64 * 8;  // rows x multiples per key
+struct KeyTable {
+  fe *tab;       // capacity x 64 x 8 x 4 fe  (81,920 B per key)
+  uint8_t *ok;   // capacity bytes: key decoded
+  static size_t bytes_per_key() { return (size_t)kKeyRowsEntries * 4 * sizeof(fe); }
+};
+
+hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
+                            hipStream_t stream);
+hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                const uint32_t *msg_off, const uint32_t *key_slot, uint32_t n, KeyTable kt,
+                                const fe *bcomb, const strobe_t *prefix, Ed25519Work w, uint8_t *out,
+                                hipStream_t stream);
+
 hipError_t launch_sr25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                       const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
                                       Ed25519Work w, int8_t *status, hipStream_t stream);

@@ -284,6 +284,215 @@ __global__ void k_partition(const uint8_t *__restrict__ kind, uint32_t n, uint32
   else out[i] = 0;
 }
 
+// ---------------------------------------------------------------------------
+// Key-cached path (validator keys repeat across commits: the device-resident
+// analogue of the reference's LRU caching verifier,
+// crypto/ed25519/ed25519.go:31,56).  A cached key is stored as a 64-row comb
+// of -A: row i holds (m+1) 16^i (-A), m < 8, in CachedQ layout (80 KB/key),
+// so [k](-A) needs 64 table additions and no doublings.
+
+// One quad per key: decode (every lane redundantly), then 64 rows of
+// multiples with 4 doublings between rows.
+template <bool SR>
+__global__ void __launch_bounds__(kQuadBlock)
+k_key_build(const uint8_t *__restrict__ keys, const uint32_t *__restrict__ slots, uint32_t m, KeyTable kt) {
+  const int c = threadIdx.x & 3;
+  const uint32_t raw = blockIdx.x * kQuadSigs + (threadIdx.x >> 2);
+  const bool live = raw < m;
+  const uint32_t e = live ? raw : m - 1;
+  uint32_t a_w[8];
+  load_words_unaligned(a_w, keys + 32ull * e);
+  ge_p3 A;
+  bool ok = SR ? ristretto_decode(A, a_w) : ge_decode_zip215(A, a_w);
+  if (!ok) ge_p3_identity(A);
+  // -A in P3Q layout on this lane
+  fe P;
+  if (c == 0) fe_neg(P, A.X);
+  else if (c == 1) P = A.Y;
+  else if (c == 2) fe_one(P);
+  else fe_neg(P, A.T);
+  const uint32_t slot = slots[e];
+  fe *row = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
+  fe r, Pm, Q, Q0;
+  for (int i = 0; i < 64; i++) {
+    quad::to_cached(Q0, P);
+    if (live) row[(i * 8 + 0) * 4 + c] = Q0;
+    quad::dbl(r, P);
+    quad::p1p1_to_p3(Pm, r);
+    quad::to_cached(Q, Pm);
+    if (live) row[(i * 8 + 1) * 4 + c] = Q;
+    for (int t = 2; t < 8; t++) {
+      quad::add(r, Pm, Q0);
+      quad::p1p1_to_p3(Pm, r);
+      quad::to_cached(Q, Pm);
+      if (live) row[(i * 8 + t) * 4 + c] = Q;
+    }
+    if (i < 63) {
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        quad::dbl(r, P);
+        quad::p1p1_to_p3(P, r);
+      }
+    }
+  }
+  if (live && c == 0) kt.ok[slot] = ok ? 1 : 0;
+}
+
+// Lanes [0, m) decode R, [m, 2m) compute the challenge (SHA-512 or merlin).
+template <bool SR>
+__global__ void __launch_bounds__(kVerifyBlock)
+k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
+              const uint32_t *__restrict__ msg_off, uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix,
+              int aligned) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const uint32_t task = j / n;
+  const uint32_t i = j - task * n;
+  uint32_t a_w[8], r_w[8];
+  if (aligned) load_words_aligned(r_w, sig + 64ull * i);
+  else load_words_unaligned(r_w, sig + 64ull * i);
+  if (task == 1) {
+    if (aligned) load_words_aligned(a_w, pk + 32ull * i);
+    else load_words_unaligned(a_w, pk + 32ull * i);
+    uint32_t k[8];
+    const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
+    if (SR) {
+      sr25519_challenge(k, *prefix, a_w, r_w, msg + o0, o1 - o0);
+    } else {
+      uint32_t h[16];
+      sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
+      sc_reduce512(k, h);
+    }
+    uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * i);
+    kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
+    kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
+    return;
+  }
+  ge_p3 P;
+  bool ok = SR ? ristretto_decode(P, r_w) : ge_decode_zip215(P, r_w);
+  if (!ok) ge_p3_identity(P);
+  w.flags[4 * i + 1] = ok ? 1 : 0;
+  fe *dst = w.Rc + 4ull * i;
+  if (SR) {
+    dst[0] = P.X; dst[1] = P.Y;
+    fe t; fe_one(t); dst[2] = t;
+    dst[3] = P.T;
+  } else {
+    ge_cached cc;
+    ge_p3_to_cached(cc, P);
+    fe t;
+    fe_carry(t, cc.YmX); dst[0] = t;
+    fe_carry(t, cc.YpX); dst[1] = t;
+    dst[2] = cc.T2d;
+    dst[3] = cc.Z;
+  }
+}
+
+// acc = sum_i e_i(k) 16^i(-A) [key comb] + sum_j d_j(s) 256^j B [base comb];
+// no doublings.  Table entries are prefetched one addition ahead.
+template <bool SR>
+__global__ void __launch_bounds__(kQuadBlock)
+k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_slot, uint32_t n, Ed25519Work w,
+              KeyTable kt, const fe *__restrict__ bcomb, uint8_t *__restrict__ out, int aligned) {
+  __shared__ int8_t dig[kQuadSigs][2][64];
+  if (blockIdx.x * kQuadSigs >= n) return;
+  const int c = threadIdx.x & 3;
+  const int q = threadIdx.x >> 2;
+  const uint32_t raw = blockIdx.x * kQuadSigs + q;
+  const bool live = raw < n;
+  const uint32_t i = live ? raw : n - 1;
+  uint32_t s_raw[8], s_w[8];
+  if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+  else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+  bool s_ok;
+  if (SR) {
+    s_ok = sr25519_decode_s(s_w, s_raw);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
+    s_ok = sc_is_canonical(s_w);
+  }
+  if (!s_ok) s_w[7] &= 0x0fffffffu;
+  {
+    uint32_t k_w[8];
+    const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * i);
+    const uint4 k0 = kp[0], k1 = kp[1];
+    k_w[0] = k0.x; k_w[1] = k0.y; k_w[2] = k0.z; k_w[3] = k0.w;
+    k_w[4] = k1.x; k_w[5] = k1.y; k_w[6] = k1.z; k_w[7] = k1.w;
+    if (c == 1) recode256_store(&dig[q][1][0], s_w);
+    else recode16_store(&dig[q][0][0], k_w, c == 0);
+  }
+  __syncthreads();
+  const uint32_t slot = key_slot[i];
+  const bool a_ok = kt.ok[slot] != 0;
+  const bool r_ok = w.flags[4 * i + 1] != 0;
+  const fe *krow = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
+  fe acc, r, idq;
+  quad::p3_identity(acc);
+  quad::cached_identity(idq);
+  // 64 key-comb additions then 32 base-comb additions, one entry prefetched
+  auto entry_at = [&](int t, int &dsg) -> const fe * {
+    if (t < 64) {
+      dsg = dig[q][0][t];
+      const int a = dsg < 0 ? -dsg : dsg;
+      return krow + ((t * 8) + (a ? a - 1 : 0)) * 4 + c;
+    }
+    dsg = dig[q][1][t - 64];
+    const int a = dsg < 0 ? -dsg : dsg;
+    return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
+  };
+  int dnext;
+  fe nxt = *entry_at(0, dnext);
+  for (int t = 0; t < 96; t++) {
+    const int d = dnext;
+    fe ent = nxt;
+    if (t + 1 < 96) nxt = *entry_at(t + 1, dnext);
+    fe_cmov(ent, idq, d == 0);
+    quad::cached_cneg(ent, d < 0);
+    quad::add(r, acc, ent);
+    quad::p1p1_to_p3(acc, r);
+  }
+  int status;
+  if (SR) {
+    const fe Rq = w.Rc[4ull * i + c];
+    const bool eq = quad::ristretto_equal(acc, Rq);
+    status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
+  } else {
+    fe Rq = w.Rc[4ull * i + c];
+    quad::cached_cneg(Rq, true);
+    quad::add(r, acc, Rq);
+    quad::p1p1_to_p3(acc, r);
+    status = (quad::is_identity_times8(acc) && s_ok && a_ok && r_ok) ? 1 : 0;
+  }
+  if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
+}
+
+hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
+                            hipStream_t stream) {
+  if (m == 0) return hipSuccess;
+  const uint32_t blocks = (m + kQuadSigs - 1) / kQuadSigs;
+  if (sr) hipLaunchKernelGGL(k_key_build<true>, dim3(blocks), dim3(kQuadBlock), 0, stream, keys, slots, m, kt);
+  else hipLaunchKernelGGL(k_key_build<false>, dim3(blocks), dim3(kQuadBlock), 0, stream, keys, slots, m, kt);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                const uint32_t *msg_off, const uint32_t *key_slot, uint32_t n, KeyTable kt,
+                                const fe *bcomb, const strobe_t *prefix, Ed25519Work w, uint8_t *out,
+                                hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  const uint32_t pblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
+  if (sr) hipLaunchKernelGGL(k_prep_cached<true>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
+  else hipLaunchKernelGGL(k_prep_cached<false>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
+  if (sr) hipLaunchKernelGGL(k_verify_comb<true>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned);
+  else hipLaunchKernelGGL(k_verify_comb<false>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned);
+  return hipGetLastError();
+}
+
 static int is_aligned(const void *a, const void *b) {
   return ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
 }

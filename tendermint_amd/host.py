@@ -244,3 +244,35 @@ def create_batch_verifier(ctx, key_kind: int) -> Optional[BatchVerifier]:
 
 def supports_batch_verifier(key_kind: int) -> bool:
     return key_kind in (TMV_KIND_ED25519, TMV_KIND_SR25519)
+
+
+class PreparedCommitCall:
+    """A tmv_verify_commit call with its C structs built once (for timing the
+    L3 path without Python marshalling in the loop)."""
+
+    def __init__(self, ctx, mode, chain_id, vals, block_id, height, commit, trust=(0, 1)):
+        L = _setup(_native.lib())
+        self._L, self._ctx = L, ctx
+        k = _Keep()
+        arr = (CValidator * max(1, len(vals.validators)))()
+        for i, v in enumerate(vals.validators):
+            a, al = k.buf(v.address)
+            p, pl = k.buf(v.pub_key)
+            arr[i] = CValidator(a, al, p, pl, v.key_kind, v.voting_power, v.proposer_priority)
+        sigs = (CCommitSig * max(1, len(commit.signatures)))()
+        for i, s in enumerate(commit.signatures):
+            a, al = k.buf(s.validator_address)
+            g, gl = k.buf(s.signature)
+            sigs[i] = CCommitSig(s.block_id_flag, a, al, s.timestamp[0], s.timestamp[1], g, gl)
+        cc = CCommit(commit.height, commit.round, _c_block_id(k, commit.block_id), sigs, len(commit.signatures))
+        bid = _c_block_id(k, block_id) if block_id is not None else None
+        self._keep = (k, arr, sigs, cc, bid)
+        self._args = (mode, chain_id.encode(), arr, len(vals.validators), vals.proposer_index,
+                      ctypes.byref(bid) if bid is not None else None, height, ctypes.byref(cc), trust[0], trust[1])
+        self._err = ctypes.create_string_buffer(4096)
+
+    def __call__(self) -> Optional[str]:
+        rc = self._L.tmv_verify_commit(self._ctx.handle, *self._args, self._err, len(self._err))
+        if rc < 0:
+            raise NativeError(f"tmv_verify_commit failed ({rc}): {self._err.value.decode(errors='replace')}")
+        return self._err.value.decode() if rc == 1 else None

@@ -243,3 +243,25 @@ def make_mixed_batch(n: int, seed: int = 0xC5, sr_frac: float = 0.5):
             entries.append(sr.entry(isr)); labels.append("sr:" + sr.kinds[isr]); isr += 1
         kinds.append(k)
     return np.array(kinds, np.uint8), Batch.from_entries(entries, labels)
+
+
+def make_c1_commit(n_vals: int = 150, chain_id: str = "test_chain_id", height: int = 3, seed: int = 1):
+    """Config 1: n validators (GenPrivKeyFromSecret("key: %x")),
+    power 5n each (types/validator_set_test.go:1544 convention), height 3,
+    round 0, random BlockID, all flags Commit, timestamps
+    2020-01-01T00:00:00Z + i ms.  Returns (ValidatorSet, BlockID, Commit) of
+    tendermint_amd.host."""
+    from .. import host as H
+    rng = random.Random(seed)
+    bid = random_block_id(rng)
+    signers = sorted((Ed25519Signer(key_seed(i)) for i in range(n_vals)),
+                     key=lambda s: hashlib.sha256(s.public_key).digest()[:20])
+    vals = H.ValidatorSet([H.Validator(hashlib.sha256(s.public_key).digest()[:20], s.public_key, 5 * n_vals)
+                           for s in signers], proposer_index=0)
+    hbid = H.BlockID(bid.hash, bid.part_set_header.total, bid.part_set_header.hash)
+    sigs = []
+    for i, s in enumerate(signers):
+        ts = (1577836800, i * 1_000_000)
+        msg = commit_vote_message(chain_id, height, 0, bid, ts[0], ts[1])
+        sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
+    return vals, hbid, H.Commit(height, 0, hbid, sigs)

@@ -1,0 +1,79 @@
+"""Key-cached path (TMV_FLAG_KEY_CACHE: device-resident 64-row combs of the
+validator keys, k_key_build + k_prep_cached + k_verify_comb) must give the
+same vectors as the oracle, across cache hits, misses and LRU eviction."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import Batch, make_c2_batch, make_sr25519_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _repeat_keys(b: Batch, n_keys: int) -> Batch:
+    """Same signatures, but only n_keys distinct public keys (wrong key for most
+    entries -> mostly invalid, which exercises the vector)."""
+    ents = [b.entry(i) for i in range(b.n)]
+    ents = [(ents[i % n_keys][0], m, s) if i % 3 else (pk, m, s) for i, (pk, m, s) in enumerate(ents)]
+    return Batch.from_entries(ents)
+
+
+def test_ed25519_cached_matches_oracle(ctx):
+    b = make_c2_batch(2000, seed=31, edge_scale=4.0)
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    for _ in range(3):  # miss, then hits
+        ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+        assert np.array_equal(st.astype(np.uint8), ref)
+    s = ctx.key_cache_stats()
+    assert s["hits"] > 0 and s["misses"] > 0
+
+
+def test_ed25519_cached_repeated_keys(ctx):
+    b = _repeat_keys(make_c2_batch(1500, seed=32), 40)
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st.astype(np.uint8), ref)
+
+
+def test_sr25519_cached_matches_oracle(ctx):
+    b = make_sr25519_batch(1200, seed=33, bad_frac=0.05)
+    ref = C.sr25519_status_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    for _ in range(2):
+        ok, st = ctx.verify_batch_ex(N.TMV_KIND_SR25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+        assert np.array_equal(st, ref)
+
+
+def test_eviction_small_capacity():
+    """Capacity 64 with 3 rounds over 200 keys (evictions) and one batch with
+    more distinct keys than the capacity (uncached fallback)."""
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, '.'); sys.path.insert(0, 'oracle')
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import make_c2_batch, Batch
+ctx = N.Context(1)
+b = make_c2_batch(200, seed=34, edge_scale=10.0)
+_, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=4)
+for lo in (0, 50, 100, 150, 0, 60):
+    idx = list(range(lo, min(lo + 50, b.n)))
+    sub = Batch.from_entries([b.entry(i) for i in idx])
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, sub.pk, sub.sig, sub.msg, sub.off)
+    assert np.array_equal(st.astype(np.uint8), ref[idx]), lo
+ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+assert np.array_equal(st.astype(np.uint8), ref)
+s = ctx.key_cache_stats()
+assert s["used"] <= 64 and s["capacity"] == 64, s
+print("ok", s)
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TMV_KEY_CACHE_CAPACITY="64")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ok" in out.stdout
