@@ -102,6 +102,29 @@ int tmv_verify_commit(tmv_ctx *ctx, int mode, const char *chain_id, const tmv_va
                       int32_t proposer_index, const tmv_block_id *block_id, int64_t height, const tmv_commit *commit,
                       int64_t trust_num, int64_t trust_den, char *err, size_t err_cap);
 
+/* Many commit checks in one device batch (cross-commit batching: blocksync
+ * look-ahead, light-client sequential headers).  Each job is
+ * one tmv_verify_commit call; results[j] = 0 ok / 1 error (text at
+ * errs + j*err_stride), identical to calling tmv_verify_commit per job.
+ * Jobs that pass the same tmv_commit pointer share signature entries (a
+ * commit that blocksync checks light and then full is verified once).
+ * Returns the number of failed jobs, or < 0 on an infrastructure error. */
+typedef struct {
+  int mode;
+  const char *chain_id;
+  const tmv_validator *vals;
+  uint32_t n_vals;
+  int32_t proposer_index;
+  const tmv_block_id *block_id;
+  int64_t height;
+  const tmv_commit *commit;
+  int64_t trust_num;
+  int64_t trust_den;
+} tmv_commit_job;
+
+int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                       size_t err_stride);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,7 +37,7 @@ EXPORTS = [
     "tmv_verify_batch_ex", "tmv_key_cache_stats",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
-    "tmv_vote_sign_bytes", "tmv_verify_commit",
+    "tmv_vote_sign_bytes", "tmv_verify_commit", "tmv_verify_commits",
 ]
 
 

@@ -20,56 +20,15 @@ void put_err(char *err, size_t cap, const std::string &s) {
   err[n] = 0;
 }
 
-const uint8_t kL[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7,
-                        0xa2, 0xde, 0xf9, 0xde, 0x14, 0,    0,    0,    0,    0,    0,
-                        0,    0,    0,    0,    0,    0,    0,    0,    0,    0x10};
-
-bool scalar_canonical(const uint8_t s[32]) {
-  for (int i = 31; i >= 0; i--) {
-    if (s[i] < kL[i]) return true;
-    if (s[i] > kL[i]) return false;
-  }
-  return false;
-}
-
 // Packed entries + GPU verify.
 class GpuBatch : public tmh::BatchVerifier {
  public:
   GpuBatch(tmv_ctx *ctx, tmh::KeyType kind) : ctx_(ctx), kind_(kind) { off_.push_back(0); }
 
   tmh::Error Add(const tmh::PubKey &key, const tmh::Bytes &msg, const tmh::Bytes &sig) override {
-    if (kind_ == tmh::KeyType::Ed25519) {
-      // crypto/ed25519/ed25519.go:209-224
-      if (key.type != tmh::KeyType::Ed25519) return std::string("pubkey is not Ed25519");
-      if (key.bytes.size() != 32)
-        return "pubkey size is incorrect; expected: 32, got " + std::to_string(key.bytes.size());
-      if (sig.size() != 64) return std::string("invalid signature");
-      push(key.bytes.data(), msg, sig.data(), "");
-      return std::nullopt;
-    }
-    // crypto/sr25519/batch.go:23-28: type check is synchronous ...
-    if (key.type != tmh::KeyType::Sr25519) return std::string("sr25519: pubkey is not sr25519");
-    // ... decoding failures are resolved on the device (status -1 / -2 with
-    // the public key taking precedence, like the reference's Add order).
-    if (key.bytes.size() != 32) {
-      return "sr25519: invalid public key: sr25519: bad PublicKey size: " + std::to_string(key.bytes.size());
-    }
-    std::string sig_err;
-    uint8_t s64[64] = {0};
-    if (sig.size() != 64) {
-      sig_err = "sr25519: unable to decode signature: sr25519: bad Signature size: " + std::to_string(sig.size());
-    } else {
-      std::memcpy(s64, sig.data(), 64);
-      uint8_t s[32];
-      std::memcpy(s, s64 + 32, 32);
-      if (!(s[31] & 0x80)) {
-        sig_err = "sr25519: unable to decode signature: sr25519: signature is not marked as a schnorrkel signature";
-      } else {
-        s[31] &= 0x7f;
-        if (!scalar_canonical(s)) sig_err = "sr25519: unable to decode signature: sr25519: non-canonical scalar";
-      }
-    }
-    push(key.bytes.data(), msg, s64, sig_err);
+    tmh::AddCheck ac = tmh::CheckAdd(kind_, key, sig);
+    if (ac.sync) return ac.sync;
+    push(key.bytes.data(), msg, ac.sig64.data(), ac.deferred_sig);
     return std::nullopt;
   }
 
@@ -97,8 +56,7 @@ class GpuBatch : public tmh::BatchVerifier {
       all = all && valid[i];
       if (!deferred_ && st < 0) {
         if (st == TMV_SR_ADDERR_PUBKEY)
-          deferred_ = std::make_pair((size_t)i, std::string("sr25519: invalid public key: sr25519: failed to "
-                                                            "decompress public key"));
+          deferred_ = std::make_pair((size_t)i, tmh::DeferredPubKeyError());
         else
           deferred_ = std::make_pair((size_t)i, sig_err_[i].empty()
                                                     ? std::string("sr25519: unable to decode signature")
@@ -208,6 +166,161 @@ size_t tmv_vote_sign_bytes(const char *chain_id, int32_t vote_type, int64_t heig
   return sb.size();
 }
 
+}  // extern "C"
+
+namespace {
+
+// Signature backend over the device: entries split by key kind, each kind one
+// tmv_verify_batch_ex call with the key cache (validator keys repeat);
+// identical (commit, index, key) entries — blocksync verifies each commit
+// twice, light then full — are verified once.
+struct GpuBackend {
+  tmv_ctx *ctx;
+  int infra = 0;
+  std::vector<int8_t> operator()(const std::vector<tmh::SigEntry> &es) {
+    std::vector<int8_t> st(es.size(), 0);
+    for (int kind = 0; kind < 2; kind++) {
+      const tmh::KeyType kt = kind == 0 ? tmh::KeyType::Ed25519 : tmh::KeyType::Sr25519;
+      std::vector<uint32_t> idx;
+      std::vector<uint8_t> pk, sig, msg;
+      std::vector<uint32_t> off{0};
+      for (size_t i = 0; i < es.size(); i++) {
+        const tmh::SigEntry &e = es[i];
+        if (e.kind != kt) continue;
+        if (e.pk->size() != 32 || e.sig.size() != 64) continue;  // VerifySignature: false
+        idx.push_back((uint32_t)i);
+        pk.insert(pk.end(), e.pk->begin(), e.pk->end());
+        sig.insert(sig.end(), e.sig.begin(), e.sig.end());
+        msg.insert(msg.end(), e.msg.begin(), e.msg.end());
+        off.push_back((uint32_t)msg.size());
+      }
+      if (idx.empty()) continue;
+      std::vector<int8_t> out(idx.size());
+      static const uint8_t z = 0;
+      const int rc = tmv_verify_batch_ex(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE,
+                                         pk.data(), sig.data(), msg.empty() ? &z : msg.data(), off.data(),
+                                         (uint32_t)idx.size(), out.data());
+      if (rc < 0) { infra = rc; continue; }
+      for (size_t t = 0; t < idx.size(); t++) st[idx[t]] = out[t];
+    }
+    return st;
+  }
+};
+
+struct OwnedCommitArgs {
+  std::unique_ptr<tmh::ValidatorSet> vals;
+  tmh::Commit *commit = nullptr;
+  tmh::BlockID block_id;
+};
+
+std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index) {
+  if (!vals) return nullptr;
+  auto vs = std::make_unique<tmh::ValidatorSet>();
+  vs->validators.resize(n_vals);
+  for (uint32_t i = 0; i < n_vals; i++) {
+    tmh::Validator &v = vs->validators[i];
+    v.address = bytes_of(vals[i].address, vals[i].address_len);
+    v.pub_key = tmh::PubKey{to_kind(vals[i].key_kind), bytes_of(vals[i].pub_key, vals[i].pub_key_len)};
+    v.voting_power = vals[i].voting_power;
+    v.proposer_priority = vals[i].proposer_priority;
+  }
+  vs->proposer = proposer_index;
+  return vs;
+}
+
+std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit) {
+  if (!commit) return nullptr;
+  auto cm = std::make_unique<tmh::Commit>();
+  cm->height = commit->height;
+  cm->round = commit->round;
+  cm->block_id = block_id_of(commit->block_id);
+  cm->signatures.resize(commit->n_sigs);
+  for (uint32_t i = 0; i < commit->n_sigs; i++) {
+    const tmv_commit_sig &s = commit->sigs[i];
+    tmh::CommitSig &c = cm->signatures[i];
+    c.block_id_flag = (tmh::BlockIDFlag)s.block_id_flag;
+    c.validator_address = bytes_of(s.validator_address, s.validator_address_len);
+    c.timestamp = tmh::Timestamp{s.ts_seconds, s.ts_nanos};
+    c.signature = bytes_of(s.signature, s.signature_len);
+  }
+  return cm;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                       size_t err_stride) {
+  if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
+  // Convert once per distinct validator set / commit pointer (a commit
+  // checked twice, as blocksync does, shares its entries).
+  std::unordered_map<const void *, std::unique_ptr<tmh::ValidatorSet>> vmap;
+  std::unordered_map<const void *, std::unique_ptr<tmh::Commit>> cmap;
+  std::vector<tmh::CommitPlan> plans(n_jobs);
+  for (uint32_t j = 0; j < n_jobs; j++) {
+    const tmv_commit_job &jb = jobs[j];
+    tmh::ValidatorSet *vs = nullptr;
+    if (jb.vals) {
+      auto &slot = vmap[jb.vals];
+      if (!slot) slot = vals_of(jb.vals, jb.n_vals, jb.proposer_index);
+      vs = slot.get();
+    }
+    tmh::Commit *cm = nullptr;
+    if (jb.commit) {
+      auto &slot = cmap[jb.commit];
+      if (!slot) slot = commit_of(jb.commit);
+      cm = slot.get();
+    }
+    const tmh::BlockID bid = jb.block_id ? block_id_of(*jb.block_id) : tmh::BlockID{};
+    if (jb.mode < 0 || jb.mode > 2) return TMV_ERR_ARG;
+    plans[j] = tmh::CommitVerifier::Plan((tmh::CommitVerifier::Mode)jb.mode, jb.chain_id ? jb.chain_id : "", vs, bid,
+                                         jb.height, cm, jb.trust_num, jb.trust_den);
+  }
+  // dedupe identical entries across plans (same commit object, index, key)
+  std::vector<tmh::SigEntry> uniq;
+  std::vector<std::vector<uint32_t>> where(n_jobs);
+  std::unordered_map<std::string, uint32_t> seen;
+  for (uint32_t j = 0; j < n_jobs; j++) {
+    const tmh::CommitPlan &pl = plans[j];
+    if (pl.early) continue;
+    where[j].resize(pl.entries.size());
+    for (size_t e = 0; e < pl.entries.size(); e++) {
+      std::string key(reinterpret_cast<const char *>(&pl.commit), sizeof(void *));
+      const int si = pl.sig_idx[e];
+      const void *pkp = pl.entries[e].pk;
+      key.append(reinterpret_cast<const char *>(&si), sizeof si);
+      key.append(reinterpret_cast<const char *>(&pkp), sizeof pkp);
+      key.push_back(pl.batch ? 'b' : 's');
+      auto it = seen.find(key);
+      if (it != seen.end() && uniq[it->second].msg == pl.entries[e].msg) {
+        where[j][e] = it->second;
+      } else {
+        where[j][e] = (uint32_t)uniq.size();
+        seen[key] = (uint32_t)uniq.size();
+        uniq.push_back(pl.entries[e]);
+      }
+    }
+  }
+  GpuBackend be{ctx};
+  std::vector<int8_t> st = uniq.empty() ? std::vector<int8_t>() : be(uniq);
+  if (be.infra < 0) {
+    if (errs && err_stride) put_err(errs, err_stride, tmv_last_error());
+    return be.infra;
+  }
+  int bad = 0;
+  std::vector<int8_t> buf;
+  for (uint32_t j = 0; j < n_jobs; j++) {
+    buf.resize(where[j].size());
+    for (size_t e = 0; e < where[j].size(); e++) buf[e] = st[where[j][e]];
+    tmh::Error e = tmh::CommitVerifier::Finish(plans[j], buf.data());
+    if (results) results[j] = e ? 1 : 0;
+    if (errs && err_stride) put_err(errs + (size_t)j * err_stride, err_stride, e ? *e : std::string());
+    bad += e ? 1 : 0;
+  }
+  return bad;
+}
+
 int tmv_verify_commit(tmv_ctx *ctx, int mode, const char *chain_id, const tmv_validator *vals, uint32_t n_vals,
                       int32_t proposer_index, const tmv_block_id *block_id, int64_t height, const tmv_commit *commit,
                       int64_t trust_num, int64_t trust_den, char *err, size_t err_cap) {
@@ -215,83 +328,11 @@ int tmv_verify_commit(tmv_ctx *ctx, int mode, const char *chain_id, const tmv_va
     put_err(err, err_cap, "null context");
     return TMV_ERR_ARG;
   }
-  std::unique_ptr<tmh::ValidatorSet> vs;
-  if (vals) {
-    vs = std::make_unique<tmh::ValidatorSet>();
-    vs->validators.resize(n_vals);
-    for (uint32_t i = 0; i < n_vals; i++) {
-      tmh::Validator &v = vs->validators[i];
-      v.address = bytes_of(vals[i].address, vals[i].address_len);
-      v.pub_key = tmh::PubKey{to_kind(vals[i].key_kind), bytes_of(vals[i].pub_key, vals[i].pub_key_len)};
-      v.voting_power = vals[i].voting_power;
-      v.proposer_priority = vals[i].proposer_priority;
-    }
-    vs->proposer = proposer_index;
-  }
-  std::unique_ptr<tmh::Commit> cm;
-  if (commit) {
-    cm = std::make_unique<tmh::Commit>();
-    cm->height = commit->height;
-    cm->round = commit->round;
-    cm->block_id = block_id_of(commit->block_id);
-    cm->signatures.resize(commit->n_sigs);
-    for (uint32_t i = 0; i < commit->n_sigs; i++) {
-      const tmv_commit_sig &s = commit->sigs[i];
-      tmh::CommitSig &c = cm->signatures[i];
-      c.block_id_flag = (tmh::BlockIDFlag)s.block_id_flag;
-      c.validator_address = bytes_of(s.validator_address, s.validator_address_len);
-      c.timestamp = tmh::Timestamp{s.ts_seconds, s.ts_nanos};
-      c.signature = bytes_of(s.signature, s.signature_len);
-    }
-  }
-  int infra = 0;
-  tmh::CommitVerifier cv;
-  std::vector<GpuBatch *> made;
-  cv.make_batch = [&](tmh::KeyType k) -> std::unique_ptr<tmh::BatchVerifier> {
-    auto b = std::make_unique<GpuBatch>(ctx, k);
-    made.push_back(b.get());
-    return b;
-  };
-  cv.verify_single = [&](const tmh::PubKey &pk, const tmh::Bytes &msg, const tmh::Bytes &sig) -> bool {
-    // PubKey.VerifySignature (crypto/ed25519/ed25519.go:173-180; crypto/sr25519/pubkey.go:49-62)
-    if (pk.type == tmh::KeyType::Ed25519) {
-      if (pk.bytes.size() != 32) return false;
-      int r = tmv_ed25519_verify(ctx, pk.bytes.data(), msg.data(), msg.size(), sig.data(), sig.size());
-      if (r < 0) { infra = r; return false; }
-      return r == 1;
-    }
-    if (pk.type == tmh::KeyType::Sr25519) {
-      if (pk.bytes.size() != 32 || sig.size() != 64) return false;
-      uint32_t off[2] = {0, (uint32_t)msg.size()};
-      int8_t st = 0;
-      static const uint8_t z = 0;
-      int r = tmv_sr25519_verify_batch(ctx, pk.bytes.data(), sig.data(), msg.empty() ? &z : msg.data(), off, 1, &st);
-      if (r < 0) { infra = r; return false; }
-      return st == 1;
-    }
-    return false;  // key types without a GPU verifier are out of scope
-  };
-  tmh::BlockID bid = block_id ? block_id_of(*block_id) : tmh::BlockID{};
-  const std::string cid = chain_id ? chain_id : "";
-  tmh::Error e;
-  switch (mode) {
-    case TMV_COMMIT_FULL: e = cv.VerifyCommit(cid, vs.get(), bid, height, cm.get()); break;
-    case TMV_COMMIT_LIGHT: e = cv.VerifyCommitLight(cid, vs.get(), bid, height, cm.get()); break;
-    case TMV_COMMIT_LIGHT_TRUSTING: e = cv.VerifyCommitLightTrusting(cid, vs.get(), cm.get(), trust_num, trust_den); break;
-    default: put_err(err, err_cap, "unknown mode"); return TMV_ERR_ARG;
-  }
-  for (GpuBatch *b : made)
-    if (b->infra_error() < 0) infra = b->infra_error();
-  if (infra < 0) {
-    put_err(err, err_cap, tmv_last_error());
-    return infra;
-  }
-  if (e) {
-    put_err(err, err_cap, *e);
-    return 1;
-  }
-  put_err(err, err_cap, "");
-  return 0;
+  tmv_commit_job jb{mode, chain_id, vals, n_vals, proposer_index, block_id, height, commit, trust_num, trust_den};
+  int32_t res = 0;
+  const int rc = tmv_verify_commits(ctx, &jb, 1, &res, err, err_cap);
+  if (rc < 0) return rc;
+  return res;
 }
 
 }  // extern "C"

@@ -307,31 +307,119 @@ inline std::pair<int64_t, bool> SafeMul(int64_t a, int64_t b) {
   return {a * b, false};
 }
 
+// ---------------------------------------------------------------- Add-time checks
+// crypto/ed25519/ed25519.go:209-224 and crypto/sr25519/batch.go:23-37.
+// `sync` is an error the reference's Add returns that needs no curve work;
+// sr25519 decoding failures are found on the device: `deferred_sig` is the
+// text to report if the device flags the signature encoding (status -2).
+struct AddCheck {
+  Error sync;
+  std::string deferred_sig;
+  Bytes sig64;  // the 64 bytes handed to the device (zeros when the length is wrong)
+};
+
+inline bool ScalarCanonical(const uint8_t s[32]) {
+  static const uint8_t L[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7,
+                                0xa2, 0xde, 0xf9, 0xde, 0x14, 0,    0,    0,    0,    0,    0,
+                                0,    0,    0,    0,    0,    0,    0,    0,    0,    0x10};
+  for (int i = 31; i >= 0; i--) {
+    if (s[i] < L[i]) return true;
+    if (s[i] > L[i]) return false;
+  }
+  return false;
+}
+
+inline AddCheck CheckAdd(KeyType batch_kind, const PubKey &key, const Bytes &sig) {
+  AddCheck r;
+  if (batch_kind == KeyType::Ed25519) {
+    if (key.type != KeyType::Ed25519) { r.sync = std::string("pubkey is not Ed25519"); return r; }
+    if (key.bytes.size() != 32) {
+      r.sync = "pubkey size is incorrect; expected: 32, got " + std::to_string(key.bytes.size());
+      return r;
+    }
+    if (sig.size() != 64) { r.sync = std::string("invalid signature"); return r; }
+    r.sig64 = sig;
+    return r;
+  }
+  if (key.type != KeyType::Sr25519) { r.sync = std::string("sr25519: pubkey is not sr25519"); return r; }
+  if (key.bytes.size() != 32) {
+    r.sync = "sr25519: invalid public key: sr25519: bad PublicKey size: " + std::to_string(key.bytes.size());
+    return r;
+  }
+  r.sig64.assign(64, 0);  // a zero signature has no schnorrkel marker: the device reports -2
+  if (sig.size() != 64) {
+    r.deferred_sig = "sr25519: unable to decode signature: sr25519: bad Signature size: " + std::to_string(sig.size());
+    return r;
+  }
+  r.sig64 = sig;
+  uint8_t sc[32];
+  std::memcpy(sc, sig.data() + 32, 32);
+  if (!(sc[31] & 0x80)) {
+    r.deferred_sig = "sr25519: unable to decode signature: sr25519: signature is not marked as a schnorrkel signature";
+  } else {
+    sc[31] &= 0x7f;
+    if (!ScalarCanonical(sc)) r.deferred_sig = "sr25519: unable to decode signature: sr25519: non-canonical scalar";
+  }
+  return r;
+}
+
+inline std::string DeferredPubKeyError() {
+  return "sr25519: invalid public key: sr25519: failed to decompress public key";
+}
+
 // ---------------------------------------------------------------- commit verification
 constexpr int kBatchVerifyThreshold = 2;  // types/validation.go:12
 
-struct CommitVerifier {
-  BatchVerifierFactory make_batch;  // batch.CreateBatchVerifier
-  SingleVerifier verify_single;     // PubKey.VerifySignature
+// One signature to verify: status 1 valid, 0 invalid, -1 / -2 device-found
+// sr25519 Add errors (public key / signature encoding).
+struct SigEntry {
+  KeyType kind;
+  const Bytes *pk;
+  Bytes msg;
+  Bytes sig;
+};
+using SigBackend = std::function<std::vector<int8_t>(const std::vector<SigEntry> &)>;
 
-  bool ShouldBatchVerify(const ValidatorSet &vals, const Commit &commit) const {
+// A commit check up to the point where signature results are needed.
+// Plan (loop of verifyCommitBatch / verifyCommitSingle) -> the backend
+// verifies the entries of many plans in one device batch -> Finish.
+struct CommitPlan {
+  Error early;                       // decided before any signature result
+  bool batch = false;                // verifyCommitBatch (true) or verifyCommitSingle
+  bool defer_add = false;            // sr25519 batch: device statuses -1/-2 are Add errors
+  int64_t tallied = 0, needed = 0;
+  std::vector<SigEntry> entries;     // in Add order
+  std::vector<int> sig_idx;          // commit.Signatures index of each entry
+  std::vector<std::string> deferred_sig;
+  std::vector<uint8_t> crosses;      // single: this entry crosses the threshold (early ok)
+  const Commit *commit = nullptr;
+};
+
+struct CommitVerifier {
+  SigBackend backend;
+
+  static bool ShouldBatchVerify(const ValidatorSet &vals, const Commit &commit) {
     const Validator *p = vals.GetProposer();
     return commit.signatures.size() >= (size_t)kBatchVerifyThreshold && p && SupportsBatchVerifier(p->pub_key);
   }
 
   using SigPred = bool (*)(const CommitSig &);
 
-  Error VerifyBatch(const std::string &chain_id, const ValidatorSet &vals, const Commit &commit, int64_t needed,
-                    SigPred ignore, SigPred count, bool count_all, bool by_index) const {
-    const Validator *proposer = vals.GetProposer();
-    std::unique_ptr<BatchVerifier> bv =
-        (proposer && SupportsBatchVerifier(proposer->pub_key)) ? make_batch(proposer->pub_key.type) : nullptr;
-    if (!bv || commit.signatures.size() < (size_t)kBatchVerifyThreshold)
-      return std::string("unsupported signature algorithm or insufficient signatures for batch verification");
-    int64_t tallied = 0;
+  // The loop of types/validation.go:179-227 (batch) / :284-327 (single).
+  static void PlanLoop(CommitPlan &pl, const std::string &chain_id, const ValidatorSet &vals, const Commit &commit,
+                       SigPred ignore, SigPred count, bool count_all, bool by_index) {
+    KeyType bkind = KeyType::Other;
+    if (pl.batch) {
+      const Validator *proposer = vals.GetProposer();
+      if (!proposer || !SupportsBatchVerifier(proposer->pub_key) ||
+          commit.signatures.size() < (size_t)kBatchVerifyThreshold) {
+        pl.early = std::string("unsupported signature algorithm or insufficient signatures for batch verification");
+        return;
+      }
+      bkind = proposer->pub_key.type;
+      pl.defer_add = bkind == KeyType::Sr25519;
+    }
     std::unordered_map<int32_t, int> seen;
-    std::vector<int> batch_idx;
-    batch_idx.reserve(commit.signatures.size());
     for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
       const CommitSig &cs = commit.signatures[idx];
       if (ignore(cs)) continue;
@@ -342,69 +430,66 @@ struct CommitVerifier {
         auto [vi, v] = vals.GetByAddress(cs.validator_address);
         if (!v) continue;
         auto it = seen.find(vi);
-        if (it != seen.end())
-          return "double vote from " + v->String() + " (" + std::to_string(it->second) + " and " +
-                 std::to_string(idx) + ")";
+        if (it != seen.end()) {
+          pl.early = "double vote from " + v->String() + " (" + std::to_string(it->second) + " and " +
+                     std::to_string(idx) + ")";
+          return;
+        }
         seen[vi] = (int)idx;
         val = v;
       }
-      Bytes sb = commit.VoteSignBytes(chain_id, (int32_t)idx);
-      if (Error e = bv->Add(val->pub_key, sb, cs.signature)) return e;
-      batch_idx.push_back((int)idx);
-      if (count(cs)) tallied += val->voting_power;
-      if (!count_all && tallied > needed) break;
-    }
-    // A device-detected Add error (sr25519) must win over the power check, as
-    // the reference's Add would have returned it inside the loop above; for
-    // ed25519 the reference order (power check, then Verify) is kept.
-    std::pair<bool, std::vector<bool>> res;
-    if (bv->MayDeferAddErrors()) {
-      res = bv->Verify();
-      if (auto de = bv->DeferredAddError()) return de->second;
-      if (tallied <= needed) return ErrNotEnoughVotingPowerSigned(tallied, needed);
-    } else {
-      if (tallied <= needed) return ErrNotEnoughVotingPowerSigned(tallied, needed);
-      res = bv->Verify();
-    }
-    const bool ok = res.first;
-    const std::vector<bool> &valid = res.second;
-    if (ok) return std::nullopt;
-    for (size_t i = 0; i < valid.size(); i++) {
-      if (!valid[i]) {
-        const int idx = batch_idx[i];
-        return "wrong signature (#" + std::to_string(idx) + "): " + HexUpper(commit.signatures[(size_t)idx].String());
+      SigEntry e{val->pub_key.type, &val->pub_key.bytes, commit.VoteSignBytes(chain_id, (int32_t)idx), {}};
+      if (pl.batch) {
+        AddCheck ac = CheckAdd(bkind, val->pub_key, cs.signature);
+        if (ac.sync) {  // bv.Add error, returned verbatim (:211-213)
+          pl.early = ac.sync;
+          return;
+        }
+        e.sig = std::move(ac.sig64);
+        pl.deferred_sig.push_back(std::move(ac.deferred_sig));
+      } else {
+        e.sig = cs.signature;
       }
+      pl.entries.push_back(std::move(e));
+      pl.sig_idx.push_back((int)idx);
+      if (count(cs)) pl.tallied += val->voting_power;
+      const bool cross = !count_all && pl.tallied > pl.needed;
+      pl.crosses.push_back(cross ? 1 : 0);
+      if (cross) break;
     }
-    return std::string("BUG: batch verification failed with no invalid signatures");
   }
 
-  Error VerifySingle(const std::string &chain_id, const ValidatorSet &vals, const Commit &commit, int64_t needed,
-                     SigPred ignore, SigPred count, bool count_all, bool by_index) const {
-    int64_t tallied = 0;
-    std::unordered_map<int32_t, int> seen;
-    for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
-      const CommitSig &cs = commit.signatures[idx];
-      if (ignore(cs)) continue;
-      const Validator *val;
-      if (by_index) {
-        val = &vals.validators[idx];
-      } else {
-        auto [vi, v] = vals.GetByAddress(cs.validator_address);
-        if (!v) continue;
-        auto it = seen.find(vi);
-        if (it != seen.end())
-          return "double vote from " + v->String() + " (" + std::to_string(it->second) + " and " +
-                 std::to_string(idx) + ")";
-        seen[vi] = (int)idx;
-        val = v;
+  // Signature results -> the reference's return value.
+  static Error Finish(const CommitPlan &pl, const int8_t *st) {
+    if (pl.early) return pl.early;
+    const Commit &commit = *pl.commit;
+    if (pl.batch) {
+      // a device-found Add error wins, as the reference's Add returns it in the loop
+      if (pl.defer_add) {
+        for (size_t i = 0; i < pl.entries.size(); i++) {
+          if (st[i] == -1) return DeferredPubKeyError();
+          if (st[i] == -2)
+            return pl.deferred_sig[i].empty() ? std::string("sr25519: unable to decode signature") : pl.deferred_sig[i];
+        }
       }
-      Bytes sb = commit.VoteSignBytes(chain_id, (int32_t)idx);
-      if (!verify_single(val->pub_key, sb, cs.signature))
-        return "wrong signature (#" + std::to_string(idx) + "): " + HexUpper(cs.signature);
-      if (count(cs)) tallied += val->voting_power;
-      if (!count_all && tallied > needed) return std::nullopt;
+      if (pl.tallied <= pl.needed) return ErrNotEnoughVotingPowerSigned(pl.tallied, pl.needed);
+      for (size_t i = 0; i < pl.entries.size(); i++) {
+        if (st[i] != 1) {
+          const int idx = pl.sig_idx[i];
+          return "wrong signature (#" + std::to_string(idx) + "): " + HexUpper(commit.signatures[(size_t)idx].String());
+        }
+      }
+      if (pl.entries.empty()) return std::string("BUG: batch verification failed with no invalid signatures");
+      return std::nullopt;
     }
-    if (tallied <= needed) return ErrNotEnoughVotingPowerSigned(tallied, needed);
+    for (size_t i = 0; i < pl.entries.size(); i++) {
+      if (st[i] != 1) {
+        const int idx = pl.sig_idx[i];
+        return "wrong signature (#" + std::to_string(idx) + "): " + HexUpper(commit.signatures[(size_t)idx].signature);
+      }
+      if (pl.crosses[i]) return std::nullopt;
+    }
+    if (pl.tallied <= pl.needed) return ErrNotEnoughVotingPowerSigned(pl.tallied, pl.needed);
     return std::nullopt;
   }
 
@@ -423,40 +508,71 @@ struct CommitVerifier {
   static bool IgnoreNotCommit(const CommitSig &c) { return c.block_id_flag != BlockIDFlagCommit; }
   static bool CountAll(const CommitSig &) { return true; }
 
-  // types/validation.go:27-53
+  enum Mode { kFull = 0, kLight = 1, kLightTrusting = 2 };
+
+  // types/validation.go:27-53 (kFull), :61-86 (kLight), :96-132 (kLightTrusting)
+  static CommitPlan Plan(Mode mode, const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id,
+                         int64_t height, const Commit *commit, int64_t num, int64_t den) {
+    CommitPlan pl;
+    pl.commit = commit;
+    if (mode == kLightTrusting) {
+      if (!vals) { pl.early = std::string("nil validator set"); return pl; }
+      if (den == 0) { pl.early = std::string("trustLevel has zero Denominator"); return pl; }
+      if (!commit) { pl.early = std::string("nil commit"); return pl; }
+      auto [prod, overflow] = SafeMul(vals->TotalVotingPower(), num);
+      if (overflow) {
+        pl.early = std::string(
+            "int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator");
+        return pl;
+      }
+      pl.needed = prod / den;
+      pl.batch = ShouldBatchVerify(*vals, *commit);
+      PlanLoop(pl, chain_id, *vals, *commit, IgnoreNotCommit, CountAll, false, false);
+      return pl;
+    }
+    if ((pl.early = VerifyBasic(vals, commit, height, block_id))) return pl;
+    pl.needed = vals->TotalVotingPower() * 2 / 3;
+    pl.batch = ShouldBatchVerify(*vals, *commit);
+    if (mode == kFull) PlanLoop(pl, chain_id, *vals, *commit, IgnoreAbsent, CountCommit, true, true);
+    else PlanLoop(pl, chain_id, *vals, *commit, IgnoreNotCommit, CountAll, false, true);
+    return pl;
+  }
+
+  // Many commits, one backend call (cross-commit batching: blocksync
+  // look-ahead, light-client sequential headers).  Identical results to
+  // calling the single-commit functions one by one.
+  std::vector<Error> VerifyMany(std::vector<CommitPlan> &plans) const {
+    std::vector<SigEntry> all;
+    std::vector<size_t> start(plans.size());
+    for (size_t p = 0; p < plans.size(); p++) {
+      start[p] = all.size();
+      if (plans[p].early) continue;
+      for (auto &e : plans[p].entries) all.push_back(e);
+    }
+    std::vector<int8_t> st = all.empty() ? std::vector<int8_t>() : backend(all);
+    std::vector<Error> out(plans.size());
+    for (size_t p = 0; p < plans.size(); p++) out[p] = Finish(plans[p], st.data() + start[p]);
+    return out;
+  }
+
+  Error Run(Mode mode, const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id, int64_t height,
+            const Commit *commit, int64_t num = 0, int64_t den = 1) const {
+    std::vector<CommitPlan> plans;
+    plans.push_back(Plan(mode, chain_id, vals, block_id, height, commit, num, den));
+    return VerifyMany(plans)[0];
+  }
+
   Error VerifyCommit(const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id, int64_t height,
                      const Commit *commit) const {
-    if (Error e = VerifyBasic(vals, commit, height, block_id)) return e;
-    const int64_t needed = vals->TotalVotingPower() * 2 / 3;
-    if (ShouldBatchVerify(*vals, *commit))
-      return VerifyBatch(chain_id, *vals, *commit, needed, IgnoreAbsent, CountCommit, true, true);
-    return VerifySingle(chain_id, *vals, *commit, needed, IgnoreAbsent, CountCommit, true, true);
+    return Run(kFull, chain_id, vals, block_id, height, commit);
   }
-
-  // types/validation.go:61-86
   Error VerifyCommitLight(const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id,
                           int64_t height, const Commit *commit) const {
-    if (Error e = VerifyBasic(vals, commit, height, block_id)) return e;
-    const int64_t needed = vals->TotalVotingPower() * 2 / 3;
-    if (ShouldBatchVerify(*vals, *commit))
-      return VerifyBatch(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, true);
-    return VerifySingle(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, true);
+    return Run(kLight, chain_id, vals, block_id, height, commit);
   }
-
-  // types/validation.go:96-132
   Error VerifyCommitLightTrusting(const std::string &chain_id, const ValidatorSet *vals, const Commit *commit,
                                   int64_t num, int64_t den) const {
-    if (!vals) return std::string("nil validator set");
-    if (den == 0) return std::string("trustLevel has zero Denominator");
-    if (!commit) return std::string("nil commit");
-    auto [prod, overflow] = SafeMul(vals->TotalVotingPower(), num);
-    if (overflow)
-      return std::string(
-          "int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator");
-    const int64_t needed = prod / den;
-    if (ShouldBatchVerify(*vals, *commit))
-      return VerifyBatch(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, false);
-    return VerifySingle(chain_id, *vals, *commit, needed, IgnoreNotCommit, CountAll, false, false);
+    return Run(kLightTrusting, chain_id, vals, BlockID{}, 0, commit, num, den);
   }
 };
 

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cstdint>
 #include <list>
 #include <unordered_map>
 #include <cstdlib>
@@ -35,6 +37,23 @@ void set_error(const std::string &s) { g_last_error = s; }
 
 inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// Large staging copies into pinned memory use several host threads (one
+// thread moves ~10 GB/s; a 1M-signature batch is ~220 MB).
+void par_memcpy(void *dst, const void *src, size_t n) {
+  const size_t kChunk = size_t(4) << 20;
+  if (n < 2 * kChunk) { std::memcpy(dst, src, n); return; }
+  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const unsigned nt = (unsigned)std::min<size_t>(hw, n / kChunk);
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (unsigned t = 1; t < nt; t++) {
+    const size_t lo = t * per, len = std::min(n, lo + per) - lo;
+    th.emplace_back([=] { std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len); });
+  }
+  std::memcpy(dst, src, std::min(n, per));
+  for (auto &x : th) x.join();
+}
+
 struct DeviceBuf {
   void *ptr = nullptr;
   size_t cap = 0;
@@ -58,6 +77,62 @@ struct DeviceBuf {
   }
 };
 
+// Open-addressing (linear probing, tombstones) index of cached keys.  Keys
+// are public keys, i.e. uniformly random bytes, so 8 of them are the hash.
+struct KeyIndex {
+  struct Ent { std::array<uint8_t, 33> key; uint32_t slot; uint8_t state; };  // 0 empty, 1 full, 2 deleted
+  std::vector<Ent> t;
+  size_t live = 0, used = 0;
+  static uint64_t hash(const uint8_t *k33) {
+    uint64_t h;
+    std::memcpy(&h, k33 + 1, 8);
+    return (h ^ (h >> 29) ^ ((uint64_t)k33[0] << 63)) * 0x9E3779B97F4A7C15ull;
+  }
+  void init(size_t cap) {
+    size_t sz = 16;
+    while (sz < 4 * cap) sz <<= 1;
+    t.assign(sz, Ent{{}, 0, 0});
+    live = used = 0;
+  }
+  // returns slot or UINT32_MAX
+  uint32_t find(const uint8_t *k33) const {
+    const size_t mask = t.size() - 1;
+    for (size_t i = hash(k33) & mask;; i = (i + 1) & mask) {
+      const Ent &e = t[i];
+      if (e.state == 0) return UINT32_MAX;
+      if (e.state == 1 && std::memcmp(e.key.data(), k33, 33) == 0) return e.slot;
+    }
+  }
+  void insert(const uint8_t *k33, uint32_t slot) {
+    if (2 * (used + 1) > t.size()) rehash();
+    const size_t mask = t.size() - 1;
+    size_t i = hash(k33) & mask;
+    while (t[i].state == 1) i = (i + 1) & mask;
+    if (t[i].state == 0) used++;
+    std::memcpy(t[i].key.data(), k33, 33);
+    t[i].slot = slot;
+    t[i].state = 1;
+    live++;
+  }
+  void erase(const uint8_t *k33) {
+    const size_t mask = t.size() - 1;
+    for (size_t i = hash(k33) & mask;; i = (i + 1) & mask) {
+      Ent &e = t[i];
+      if (e.state == 0) return;
+      if (e.state == 1 && std::memcmp(e.key.data(), k33, 33) == 0) { e.state = 2; live--; return; }
+    }
+  }
+  void rehash() {
+    std::vector<Ent> old;
+    old.swap(t);
+    t.assign(old.size(), Ent{{}, 0, 0});
+    live = used = 0;
+    for (const Ent &e : old)
+      if (e.state == 1) insert(e.key.data(), e.slot);
+  }
+  size_t size() const { return live; }
+};
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
@@ -70,10 +145,10 @@ struct Device {
   // expanded-key cache (device table + host LRU index)
   tmv::KeyTable kt{nullptr, nullptr};
   uint32_t kcap = 0;
-  std::unordered_map<std::string, uint32_t> kmap;  // kind byte + 32 key bytes -> slot
+  KeyIndex kindex;                                  // (kind, key bytes) -> slot
   std::list<uint32_t> klru;                         // front = most recently used
   std::vector<std::list<uint32_t>::iterator> kpos;
-  std::vector<std::string> kslot_key;
+  std::vector<std::array<uint8_t, 33>> kslot_key;
   std::vector<uint64_t> kslot_epoch;
   uint64_t kepoch = 0, khits = 0, kmisses = 0;
   DeviceBuf d_kbuild, h_kbuild;
@@ -215,18 +290,24 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     d.kslot_key.resize(d.kcap);
     d.kslot_epoch.assign(d.kcap, 0);
   }
+  if (d.kindex.t.empty()) d.kindex.init(d.kcap);
   const uint64_t epoch = ++d.kepoch;
   std::vector<uint32_t> miss_idx;
   std::vector<uint32_t> miss_slot;
-  std::string key(33, '\0');
+  uint8_t key[33];
   key[0] = sr ? 1 : 0;
   uint32_t distinct = 0;
+  uint32_t last_slot = UINT32_MAX;
+  const uint8_t *last_pk = nullptr;
   for (uint32_t i = 0; i < n; i++) {
-    std::memcpy(&key[1], pk + 32ull * i, 32);
-    auto it = d.kmap.find(key);
-    uint32_t slot;
-    if (it != d.kmap.end()) {
-      slot = it->second;
+    const uint8_t *p = pk + 32ull * i;
+    if (last_pk && std::memcmp(p, last_pk, 32) == 0) {  // runs of one key
+      slots_out[i] = last_slot;
+      continue;
+    }
+    std::memcpy(key + 1, p, 32);
+    uint32_t slot = d.kindex.find(key);
+    if (slot != UINT32_MAX) {
       if (d.kslot_epoch[slot] != epoch) {
         d.kslot_epoch[slot] = epoch;
         distinct++;
@@ -235,24 +316,26 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
       }
     } else {
       if (++distinct > d.kcap) return 1;
-      if (d.kmap.size() < d.kcap) {
-        slot = (uint32_t)d.kmap.size();
+      if (d.kindex.size() < d.kcap && d.klru.size() < d.kcap) {
+        slot = (uint32_t)d.klru.size();
         d.klru.push_front(slot);
       } else {
         slot = d.klru.back();  // least recently used; never one pinned by this batch
         if (d.kslot_epoch[slot] == epoch) return 1;
-        d.kmap.erase(d.kslot_key[slot]);
+        d.kindex.erase(d.kslot_key[slot].data());
         d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
       }
       d.kpos[slot] = d.klru.begin();
-      d.kslot_key[slot] = key;
+      std::memcpy(d.kslot_key[slot].data(), key, 33);
       d.kslot_epoch[slot] = epoch;
-      d.kmap[key] = slot;
+      d.kindex.insert(key, slot);
       miss_idx.push_back(i);
       miss_slot.push_back(slot);
       d.kmisses++;
     }
     slots_out[i] = slot;
+    last_slot = slot;
+    last_pk = p;
   }
   const uint32_t m = (uint32_t)miss_idx.size();
   if (m) {
@@ -436,12 +519,12 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
   if ((e = d.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   uint8_t *h = static_cast<uint8_t *>(d.h_in.ptr);
-  std::memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
-  std::memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
+  par_memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
+  par_memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
   uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
   const uint32_t base = msg_off[lo];
   for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
-  if (mbytes) std::memcpy(h + L.msg, msg + base, mbytes);
+  if (mbytes) par_memcpy(h + L.msg, msg + base, mbytes);
   if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
   if (cached) {
     const int kr = resolve_keys(d, sch == Scheme::Sr25519Cached, pk + 32ull * lo, n,
@@ -556,7 +639,7 @@ int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t
   uint32_t u = 0, c = 0;
   for (auto &d : ctx->devs) {
     std::lock_guard<std::mutex> lk(d->mu);
-    h += d->khits; m += d->kmisses; u += (uint32_t)d->kmap.size(); c += d->kcap;
+    h += d->khits; m += d->kmisses; u += (uint32_t)d->kindex.size(); c += d->kcap;
   }
   if (hits) *hits = h;
   if (misses) *misses = m;

@@ -276,3 +276,108 @@ class PreparedCommitCall:
         if rc < 0:
             raise NativeError(f"tmv_verify_commit failed ({rc}): {self._err.value.decode(errors='replace')}")
         return self._err.value.decode() if rc == 1 else None
+
+
+class CCommitJob(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("chain_id", ctypes.c_char_p), ("vals", ctypes.POINTER(CValidator)),
+                ("n_vals", ctypes.c_uint32), ("proposer_index", ctypes.c_int32),
+                ("block_id", ctypes.POINTER(CBlockID)), ("height", ctypes.c_int64),
+                ("commit", ctypes.POINTER(CCommit)), ("trust_num", ctypes.c_int64), ("trust_den", ctypes.c_int64)]
+
+
+@dataclass
+class CommitJob:
+    """One commit check: mode MODE_FULL / MODE_LIGHT / MODE_LIGHT_TRUSTING."""
+    mode: int
+    chain_id: str
+    vals: Optional[ValidatorSet]
+    block_id: Optional[BlockID]
+    height: int
+    commit: Optional[Commit]
+    trust: Tuple[int, int] = (1, 3)
+
+
+class PreparedJobs:
+    """C structs for a list of CommitJob, built once.  Jobs that share a
+    Commit object (by identity) share one tmv_commit, so the engine verifies
+    their common signatures once (blocksync checks each commit twice)."""
+
+    def __init__(self, jobs: List[CommitJob]):
+        k = _Keep()
+        vcache, ccache = {}, {}
+        arr = (CCommitJob * max(1, len(jobs)))()
+        for j, jb in enumerate(jobs):
+            cv, nv, prop = None, 0, -1
+            if jb.vals is not None:
+                key = id(jb.vals)
+                if key not in vcache:
+                    va = (CValidator * max(1, len(jb.vals.validators)))()
+                    for i, v in enumerate(jb.vals.validators):
+                        a, al = k.buf(v.address)
+                        p, pl = k.buf(v.pub_key)
+                        va[i] = CValidator(a, al, p, pl, v.key_kind, v.voting_power, v.proposer_priority)
+                    k.refs.append(va)
+                    vcache[key] = va
+                cv, nv, prop = vcache[key], len(jb.vals.validators), jb.vals.proposer_index
+            cc = None
+            if jb.commit is not None:
+                key = id(jb.commit)
+                if key not in ccache:
+                    sigs = (CCommitSig * max(1, len(jb.commit.signatures)))()
+                    for i, s in enumerate(jb.commit.signatures):
+                        a, al = k.buf(s.validator_address)
+                        g, gl = k.buf(s.signature)
+                        sigs[i] = CCommitSig(s.block_id_flag, a, al, s.timestamp[0], s.timestamp[1], g, gl)
+                    c = CCommit(jb.commit.height, jb.commit.round, _c_block_id(k, jb.commit.block_id), sigs,
+                                len(jb.commit.signatures))
+                    k.refs += [sigs, c]
+                    ccache[key] = c
+                cc = ctypes.pointer(ccache[key])
+            bid = None
+            if jb.block_id is not None:
+                b = _c_block_id(k, jb.block_id)
+                k.refs.append(b)
+                bid = ctypes.pointer(b)
+            cid = jb.chain_id.encode()
+            k.refs.append(cid)
+            arr[j] = CCommitJob(jb.mode, cid, cv, nv, prop, bid, jb.height, cc, jb.trust[0], jb.trust[1])
+        self.keep = (k, vcache, ccache)
+        self.arr = arr
+        self.n = len(jobs)
+        self.stride = 512
+        self.errs = ctypes.create_string_buffer(self.stride * max(1, self.n))
+        self.results = (ctypes.c_int32 * max(1, self.n))()
+
+    def decode(self) -> List[Optional[str]]:
+        out = []
+        for j in range(self.n):
+            if self.results[j]:
+                raw = self.errs.raw[j * self.stride:(j + 1) * self.stride]
+                out.append(raw.split(b"\0", 1)[0].decode())
+            else:
+                out.append(None)
+        return out
+
+
+def _setup_many(L):
+    if not getattr(L, "_tmhost_many", False):
+        L.tmv_verify_commits.argtypes = [ctypes.c_void_p, ctypes.POINTER(CCommitJob), ctypes.c_uint32,
+                                         ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_size_t]
+        L._tmhost_many = True
+    return L
+
+
+def run_prepared_jobs(ctx, pj: PreparedJobs) -> int:
+    L = _setup_many(_setup(_native.lib()))
+    rc = L.tmv_verify_commits(ctx.handle, pj.arr, pj.n, pj.results, pj.errs, pj.stride)
+    if rc < 0:
+        raise NativeError(f"tmv_verify_commits failed ({rc}): {_native.last_error()}")
+    return rc
+
+
+def verify_commits(ctx, jobs: List[CommitJob]) -> List[Optional[str]]:
+    """Cross-commit batching: every job's result equals verify_commit* of that
+    job alone; all signatures go to the GPU in one batch."""
+    pj = PreparedJobs(jobs)
+    run_prepared_jobs(ctx, pj)
+    return pj.decode()

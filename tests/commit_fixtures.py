@@ -100,7 +100,7 @@ class FakeBackend:
         return self._call(H.MODE_LIGHT_TRUSTING, chain_id, vals, None, 0, commit, trust)
 
     def batches_made(self):
-        return ctypes.c_int.in_dll(self.L, "commitcheck_batches_made").value
+        return ctypes.c_int.in_dll(self.L, "commitcheck_backend_calls").value
 
 
 class GpuBackend:
@@ -115,3 +115,58 @@ class GpuBackend:
 
     def verify_commit_light_trusting(self, chain_id, vals, commit, trust=(1, 3)):
         return H.verify_commit_light_trusting(self.ctx, chain_id, vals, commit, trust)
+
+
+def fake_verify_commits(backend: "FakeBackend", jobs):
+    L = backend.L
+    if not getattr(L, "_many", False):
+        L.commitcheck_verify_commits.argtypes = [ctypes.POINTER(H.CCommitJob), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_size_t]
+        L._many = True
+    pj = H.PreparedJobs(jobs)
+    L.commitcheck_verify_commits(pj.arr, pj.n, pj.results, pj.errs, pj.stride)
+    return pj.decode()
+
+
+def random_jobs(scheme: str, n_jobs: int, seed: int):
+    """Random commit checks covering every branch: sizes 1..9, absent / nil /
+    commit flags, corrupted signatures, wrong block IDs / heights, all three
+    modes, shared commits (checked twice, like blocksync)."""
+    import random
+    rng = random.Random(seed)
+    jobs = []
+    pool = {}
+    for j in range(n_jobs):
+        nv = rng.randint(1, 9)
+        if nv not in pool:
+            pool[nv] = rand_val_set(scheme, nv, rng.randint(1, 50), tag=f"r{nv}")
+        vals, signers = pool[nv]
+        vals = H.ValidatorSet([H.Validator(v.address, v.pub_key, rng.randint(1, 30), v.key_kind)
+                               for v in vals.validators], 0)
+        height = rng.randint(1, 5)
+        bid = random_block_id(rng.randint(0, 3))
+        sigs = []
+        for i, s in enumerate(signers):
+            r = rng.random()
+            if r < 0.15:
+                sigs.append(H.CommitSig())
+                continue
+            flag = H.BLOCK_ID_FLAG_NIL if r < 0.3 else H.BLOCK_ID_FLAG_COMMIT
+            chain = "chain" if rng.random() > 0.1 else "other"
+            sigs.append(sign_commit_sig(s, chain, height, 0, bid, flag, (1577836800 + i, rng.randrange(10**9))))
+        commit = H.Commit(height, 0, bid, sigs)
+        mode = rng.choice([H.MODE_FULL, H.MODE_LIGHT, H.MODE_LIGHT_TRUSTING])
+        want_bid = bid if rng.random() > 0.1 else random_block_id(9)
+        want_h = height if rng.random() > 0.1 else height + 1
+        jobs.append(H.CommitJob(mode, "chain", vals, want_bid, want_h, commit, (rng.randint(1, 2), 3)))
+        if rng.random() < 0.3:  # same commit checked again (blocksync: light then full)
+            jobs.append(H.CommitJob(H.MODE_FULL, "chain", vals, want_bid, want_h, commit))
+    return jobs
+
+
+def single_result(backend, jb):
+    if jb.mode == H.MODE_FULL:
+        return backend.verify_commit(jb.chain_id, jb.vals, jb.block_id, jb.height, jb.commit)
+    if jb.mode == H.MODE_LIGHT:
+        return backend.verify_commit_light(jb.chain_id, jb.vals, jb.block_id, jb.height, jb.commit)
+    return backend.verify_commit_light_trusting(jb.chain_id, jb.vals, jb.commit, jb.trust)

@@ -169,3 +169,23 @@ def test_wrong_block_id_text(backend):
             other.psh_hash[:6].hex().upper() + ", got " + bid.hash.hex().upper() + ":" + str(bid.psh_total) + ":" +
             bid.psh_hash[:6].hex().upper())
     assert err == want
+
+
+def test_verify_many_equals_single_fake(fake):
+    """Cross-commit batching (CommitVerifier::VerifyMany / tmv_verify_commits)
+    returns exactly the per-commit results, on 300 random commit checks."""
+    jobs = F.random_jobs("fake", 300, seed=5)
+    many = F.fake_verify_commits(fake, jobs)
+    single = [F.single_result(fake, jb) for jb in jobs]
+    assert many == single
+    assert sum(r is None for r in many) > 20 and sum(r is not None for r in many) > 20
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scheme", ["ed25519", "sr25519"])
+def test_verify_many_equals_single_gpu(ctx, scheme):
+    jobs = F.random_jobs(scheme, 80, seed=6)
+    g = F.GpuBackend(ctx, scheme)
+    many = H.verify_commits(ctx, jobs)
+    single = [F.single_result(g, jb) for jb in jobs]
+    assert many == single
