@@ -265,3 +265,85 @@ def make_c1_commit(n_vals: int = 150, chain_id: str = "test_chain_id", height: i
         msg = commit_vote_message(chain_id, height, 0, bid, ts[0], ts[1])
         sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
     return vals, hbid, H.Commit(height, 0, hbid, sigs)
+
+
+def _valset_hash(vals) -> bytes:
+    """Stand-in for ValidatorSet.Hash (merkle, out of scope): SHA-256 over the keys and powers."""
+    h = hashlib.sha256()
+    for v in vals.validators:
+        h.update(v.pub_key + v.voting_power.to_bytes(8, "little"))
+    return h.digest()
+
+
+def make_light_chain(n_headers: int, n_vals: int = 100, chain_id: str = "test", rotate: int = 1, seed: int = 7):
+    """Config 3 shape (light/helpers_test.go:165-216 genLightBlocksWithKeys):
+    n_vals validators of power 2, `rotate` keys replaced per height, round 1,
+    every validator signs.  Returns (trusted SignedHeader at height 1,
+    [LightBlock] for heights 2..n_headers+1)."""
+    from .. import host as H
+    from ..chains import LightBlock, SignedHeader
+    rng = random.Random(seed)
+    next_key = [n_vals]
+    signers = [Ed25519Signer(key_seed(i, "lkey")) for i in range(n_vals)]
+
+    def valset(sgs):
+        vs = sorted(sgs, key=lambda s: hashlib.sha256(s.public_key).digest()[:20])
+        return vs, H.ValidatorSet([H.Validator(hashlib.sha256(s.public_key).digest()[:20], s.public_key, 2)
+                                   for s in vs], proposer_index=0)
+
+    def header(height, sgs, next_sgs, t):
+        vs, vals = valset(sgs)
+        _, nvals = valset(next_sgs)
+        bid = random_block_id(rng)
+        hbid = H.BlockID(bid.hash, bid.part_set_header.total, bid.part_set_header.hash)
+        sigs = []
+        for i, s in enumerate(vs):
+            ts = (t[0], t[1] + i)
+            msg = commit_vote_message(chain_id, height, 1, bid, ts[0], ts[1])
+            sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
+        commit = H.Commit(height, 1, hbid, sigs)
+        return SignedHeader(chain_id, height, t, _valset_hash(vals), _valset_hash(nvals), commit), vals
+
+    cur = signers
+    t0 = 1577836800
+    nxt = list(cur)
+    for _ in range(rotate):
+        nxt = nxt[1:] + [Ed25519Signer(key_seed(next_key[0], "lkey"))]
+        next_key[0] += 1
+    trusted, _ = header(1, cur, nxt, (t0, 0))
+    blocks = []
+    for h in range(2, n_headers + 2):
+        cur = nxt
+        nxt = list(cur)
+        for _ in range(rotate):
+            nxt = nxt[1:] + [Ed25519Signer(key_seed(next_key[0], "lkey"))]
+            next_key[0] += 1
+        hd, vals = header(h, cur, nxt, (t0 + h, 0))
+        blocks.append(LightBlock(hd, vals))
+    return trusted, blocks
+
+
+def make_block_chain(n_blocks: int, n_vals: int = 175, chain_id: str = "test_chain_id", seed: int = 11):
+    """Config 4 shape: a chain of n_blocks with a static n_vals-validator set;
+    block h carries LastCommit = commit for h-1.  Returns (ValidatorSet, [Block])."""
+    from .. import host as H
+    from ..chains import Block
+    rng = random.Random(seed)
+    signers = sorted((Ed25519Signer(key_seed(i, "bkey")) for i in range(n_vals)),
+                     key=lambda s: hashlib.sha256(s.public_key).digest()[:20])
+    vals = H.ValidatorSet([H.Validator(hashlib.sha256(s.public_key).digest()[:20], s.public_key, 10)
+                           for s in signers], proposer_index=0)
+    blocks = []
+    prev_commit = None
+    for h in range(1, n_blocks + 1):
+        bid = random_block_id(rng)
+        hbid = H.BlockID(bid.hash, bid.part_set_header.total, bid.part_set_header.hash)
+        sigs = []
+        for i, s in enumerate(signers):
+            ts = (1577836800 + h, i * 1000)
+            msg = commit_vote_message(chain_id, h, 0, bid, ts[0], ts[1])
+            sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
+        commit = H.Commit(h, 0, hbid, sigs)
+        blocks.append(Block(h, hbid, prev_commit, commit))
+        prev_commit = commit
+    return vals, blocks

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Secondary measurements for BASELINE configs 1, 3, 4, 5 (one JSON line
+each; the headline line is bench.py's C2).  Single GPU.
+
+  C1  types.VerifyCommit, 150 validators: p50/p99 latency, cold + warm key cache
+  C3  light sequential: H headers x 100 validators (VerifyCommitLight, 67
+      signatures read per header), window-batched
+  C4  blocksync replay: B blocks x 175 validators (light + full check per
+      block = 292 reference verifications, 175 unique)
+  C5  mixed ed25519 + sr25519 batch (kernel path, inputs resident)
+"""
+import argparse, json, os, statistics, sys, time
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np
+import torch
+from tendermint_amd import _native as N, host as H, chains
+from tendermint_amd.testing import factory as Fa
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--headers", type=int, default=2000)
+ap.add_argument("--blocks", type=int, default=1000)
+ap.add_argument("--c5", type=int, default=1_000_000)
+ap.add_argument("--only", default="1,3,4,5")
+a = ap.parse_args()
+only = set(a.only.split(","))
+ctx = N.Context(1)
+
+if "1" in only:
+    vals, bid, commit = Fa.make_c1_commit(150)
+    call = H.PreparedCommitCall(ctx, H.MODE_FULL, "test_chain_id", vals, bid, 3, commit)
+    t = time.perf_counter(); assert call() is None; cold = (time.perf_counter() - t) * 1e3
+    lat = []
+    for _ in range(500):
+        t = time.perf_counter(); assert call() is None; lat.append((time.perf_counter() - t) * 1e3)
+    lat.sort()
+    print(json.dumps({"config": "C1 VerifyCommit 150 vals", "cold_ms": round(cold, 3),
+                      "p50_ms": round(lat[250], 4), "p99_ms": round(lat[494], 4)}), flush=True)
+
+if "3" in only:
+    trusted, blocks = Fa.make_light_chain(a.headers, 100)
+    chains.verify_sequential(ctx, trusted, blocks[:50])  # warm
+    t = time.perf_counter()
+    n, err = chains.verify_sequential(ctx, trusted, blocks, window=1000)
+    dt = time.perf_counter() - t
+    assert err is None, err
+    print(json.dumps({"config": f"C3 light sequential {a.headers} headers x 100 vals", "seconds": round(dt, 4),
+                      "headers_per_s": round(n / dt, 1), "verifies_per_s_ref_count": round(67 * n / dt)}),
+          flush=True)
+
+if "4" in only:
+    vals, blocks = Fa.make_block_chain(a.blocks, 175)
+    chains.blocksync_replay(ctx, "test_chain_id", vals, blocks[:20])  # warm (key table)
+    t = time.perf_counter()
+    applied, err = chains.blocksync_replay(ctx, "test_chain_id", vals, blocks, window=600)
+    dt = time.perf_counter() - t
+    assert err is None, err
+    print(json.dumps({"config": f"C4 blocksync {a.blocks} blocks x 175 vals", "seconds": round(dt, 4),
+                      "blocks_per_s": round(applied / dt, 1),
+                      "verifies_per_s_ref_count": round(292 * applied / dt),
+                      "unique_verifies_per_s": round(175 * applied / dt)}), flush=True)
+
+if "5" in only:
+    kind, base = Fa.make_mixed_batch(20_000)
+    reps = (a.c5 + base.n - 1) // base.n
+    b = base.tile(a.c5)
+    kind = np.tile(kind, reps)[:a.c5]
+    dev = torch.device("cuda:0")
+    t = lambda x: torch.from_numpy(x).to(dev)
+    dk, dp, ds, dm = t(kind), t(b.pk), t(b.sig), t(b.msg)
+    do = t(b.off.view(np.int32))
+    dst = torch.zeros(a.c5, dtype=torch.int8, device=dev)
+    st = torch.cuda.Stream()
+    for _ in range(2):
+        ctx.verify_mixed_batch_device(0, dk.data_ptr(), dp.data_ptr(), ds.data_ptr(), dm.data_ptr(), do.data_ptr(),
+                                      a.c5, dst.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(3):
+        ctx.verify_mixed_batch_device(0, dk.data_ptr(), dp.data_ptr(), ds.data_ptr(), dm.data_ptr(), do.data_ptr(),
+                                      a.c5, dst.data_ptr(), st.cuda_stream)
+    e1.record(st); torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 3
+    print(json.dumps({"config": f"C5 mixed ed25519+sr25519 {a.c5} sigs, 1 GPU, kernel path",
+                      "ms": round(ms, 3), "verifies_per_s": round(a.c5 / ms * 1e3),
+                      "valid": int((dst == 1).sum().item())}), flush=True)
