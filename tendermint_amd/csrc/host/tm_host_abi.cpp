@@ -2,8 +2,16 @@
 // backed by the GPU entry points of include/tmverify.h, canonical vote
 // sign-bytes, and the commit verifiers of tm_types.h instantiated with them.
 // Only the public tmv_* C-ABI is used to reach the device (layering).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
 #include <cstring>
 #include <memory>
+#include <thread>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -170,40 +178,96 @@ size_t tmv_vote_sign_bytes(const char *chain_id, int32_t vote_type, int64_t heig
 
 namespace {
 
+// Run fn(i) for i in [0, n) on up to 16 host threads (serial when small).
+template <class F>
+void parallel_for(size_t n, size_t min_per_thread, F fn) {
+  const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t nt = std::min(hw, n / std::max<size_t>(1, min_per_thread));
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto worker = [&] {
+    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; t++) th.emplace_back(worker);
+  worker();
+  for (auto &t : th) t.join();
+}
+
 // Signature backend over the device: entries split by key kind, each kind one
-// tmv_verify_batch_ex call with the key cache (validator keys repeat);
-// identical (commit, index, key) entries — blocksync verifies each commit
-// twice, light then full — are verified once.
+// tmv_verify_batch_ex call with the key cache (validator keys repeat).  The
+// packed arrays are filled in parallel from precomputed offsets.
 struct GpuBackend {
   tmv_ctx *ctx;
   int infra = 0;
-  std::vector<int8_t> operator()(const std::vector<tmh::SigEntry> &es) {
+  std::vector<int8_t> operator()(const std::vector<const tmh::SigEntry *> &es) {
     std::vector<int8_t> st(es.size(), 0);
     for (int kind = 0; kind < 2; kind++) {
       const tmh::KeyType kt = kind == 0 ? tmh::KeyType::Ed25519 : tmh::KeyType::Sr25519;
       std::vector<uint32_t> idx;
-      std::vector<uint8_t> pk, sig, msg;
       std::vector<uint32_t> off{0};
       for (size_t i = 0; i < es.size(); i++) {
-        const tmh::SigEntry &e = es[i];
+        const tmh::SigEntry &e = *es[i];
         if (e.kind != kt) continue;
         if (e.pk->size() != 32 || e.sig.size() != 64) continue;  // VerifySignature: false
         idx.push_back((uint32_t)i);
-        pk.insert(pk.end(), e.pk->begin(), e.pk->end());
-        sig.insert(sig.end(), e.sig.begin(), e.sig.end());
-        msg.insert(msg.end(), e.msg.begin(), e.msg.end());
-        off.push_back((uint32_t)msg.size());
+        off.push_back(off.back() + (uint32_t)e.msg.size());
       }
       if (idx.empty()) continue;
-      std::vector<int8_t> out(idx.size());
-      static const uint8_t z = 0;
+      const size_t m = idx.size();
+      std::vector<uint8_t> pk(32 * m), sig(64 * m), msg(std::max<uint32_t>(1, off.back()));
+      parallel_for((m + 255) / 256, 4, [&](size_t c) {
+        for (size_t t = c * 256; t < std::min(m, c * 256 + 256); t++) {
+          const tmh::SigEntry &e = *es[idx[t]];
+          std::memcpy(&pk[32 * t], e.pk->data(), 32);
+          std::memcpy(&sig[64 * t], e.sig.data(), 64);
+          if (!e.msg.empty()) std::memcpy(&msg[off[t]], e.msg.data(), e.msg.size());
+        }
+      });
+      std::vector<int8_t> out(m);
       const int rc = tmv_verify_batch_ex(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE,
-                                         pk.data(), sig.data(), msg.empty() ? &z : msg.data(), off.data(),
-                                         (uint32_t)idx.size(), out.data());
+                                         pk.data(), sig.data(), msg.data(), off.data(), (uint32_t)m, out.data());
       if (rc < 0) { infra = rc; continue; }
-      for (size_t t = 0; t < idx.size(); t++) st[idx[t]] = out[t];
+      for (size_t t = 0; t < m; t++) st[idx[t]] = out[t];
     }
     return st;
+  }
+};
+
+// Phase timing of tmv_verify_commits, printed to stderr when the
+// environment variable TMV_HOST_TIMING is set (profiling aid).
+struct PhaseTimer {
+  bool on = std::getenv("TMV_HOST_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[tmv_verify_commits] %-8s %9.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+
+// Identity of a signature entry for cross-job dedup: same commit object,
+// same signature index, same public key object, same verifier kind.
+struct EntryKey {
+  const void *commit;
+  const void *pk;
+  int32_t sig_idx;
+  bool batch;
+  bool operator==(const EntryKey &o) const {
+    return commit == o.commit && pk == o.pk && sig_idx == o.sig_idx && batch == o.batch;
+  }
+};
+struct EntryKeyHash {
+  size_t operator()(const EntryKey &k) const {
+    uint64_t h = (uint64_t)(uintptr_t)k.commit * 0x9e3779b97f4a7c15ull;
+    h ^= (uint64_t)(uintptr_t)k.pk + 0x632be59bd9b4e019ull + (h << 6) + (h >> 2);
+    h ^= (uint64_t)(uint32_t)k.sig_idx * 2 + (k.batch ? 1 : 0) + (h << 6) + (h >> 2);
+    return (size_t)h;
   }
 };
 
@@ -253,57 +317,72 @@ extern "C" {
 int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                        size_t err_stride) {
   if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
+  for (uint32_t j = 0; j < n_jobs; j++)
+    if (jobs[j].mode < 0 || jobs[j].mode > 2) return TMV_ERR_ARG;
+  PhaseTimer tm;
   // Convert once per distinct validator set / commit pointer (a commit
-  // checked twice, as blocksync does, shares its entries).
-  std::unordered_map<const void *, std::unique_ptr<tmh::ValidatorSet>> vmap;
-  std::unordered_map<const void *, std::unique_ptr<tmh::Commit>> cmap;
-  std::vector<tmh::CommitPlan> plans(n_jobs);
+  // checked twice, as blocksync does, shares its entries), in parallel.
+  std::unordered_map<const void *, size_t> vidx, cidx;
+  std::vector<const tmv_commit_job *> vsrc, csrc;
+  std::vector<size_t> jv(n_jobs, SIZE_MAX), jc(n_jobs, SIZE_MAX);
   for (uint32_t j = 0; j < n_jobs; j++) {
-    const tmv_commit_job &jb = jobs[j];
-    tmh::ValidatorSet *vs = nullptr;
-    if (jb.vals) {
-      auto &slot = vmap[jb.vals];
-      if (!slot) slot = vals_of(jb.vals, jb.n_vals, jb.proposer_index);
-      vs = slot.get();
+    if (jobs[j].vals) {
+      auto [it, fresh] = vidx.emplace(jobs[j].vals, vsrc.size());
+      if (fresh) vsrc.push_back(&jobs[j]);
+      jv[j] = it->second;
     }
-    tmh::Commit *cm = nullptr;
-    if (jb.commit) {
-      auto &slot = cmap[jb.commit];
-      if (!slot) slot = commit_of(jb.commit);
-      cm = slot.get();
+    if (jobs[j].commit) {
+      auto [it, fresh] = cidx.emplace(jobs[j].commit, csrc.size());
+      if (fresh) csrc.push_back(&jobs[j]);
+      jc[j] = it->second;
     }
-    const tmh::BlockID bid = jb.block_id ? block_id_of(*jb.block_id) : tmh::BlockID{};
-    if (jb.mode < 0 || jb.mode > 2) return TMV_ERR_ARG;
-    plans[j] = tmh::CommitVerifier::Plan((tmh::CommitVerifier::Mode)jb.mode, jb.chain_id ? jb.chain_id : "", vs, bid,
-                                         jb.height, cm, jb.trust_num, jb.trust_den);
   }
+  std::vector<std::unique_ptr<tmh::ValidatorSet>> vsets(vsrc.size());
+  std::vector<std::unique_ptr<tmh::Commit>> commits(csrc.size());
+  parallel_for(vsrc.size() + csrc.size(), 4, [&](size_t i) {
+    if (i < vsrc.size())
+      vsets[i] = vals_of(vsrc[i]->vals, vsrc[i]->n_vals, vsrc[i]->proposer_index);
+    else
+      commits[i - vsrc.size()] = commit_of(csrc[i - vsrc.size()]->commit);
+  });
+  tm.mark("convert");
+  std::vector<tmh::CommitPlan> plans(n_jobs);
+  parallel_for(n_jobs, 4, [&](size_t j) {
+    const tmv_commit_job &jb = jobs[j];
+    const tmh::BlockID bid = jb.block_id ? block_id_of(*jb.block_id) : tmh::BlockID{};
+    plans[j] = tmh::CommitVerifier::Plan((tmh::CommitVerifier::Mode)jb.mode, jb.chain_id ? jb.chain_id : "",
+                                         jv[j] == SIZE_MAX ? nullptr : vsets[jv[j]].get(), bid, jb.height,
+                                         jc[j] == SIZE_MAX ? nullptr : commits[jc[j]].get(), jb.trust_num,
+                                         jb.trust_den);
+  });
+  tm.mark("plan");
   // dedupe identical entries across plans (same commit object, index, key)
-  std::vector<tmh::SigEntry> uniq;
+  std::vector<const tmh::SigEntry *> uniq;
   std::vector<std::vector<uint32_t>> where(n_jobs);
-  std::unordered_map<std::string, uint32_t> seen;
+  std::unordered_map<EntryKey, uint32_t, EntryKeyHash> seen;
+  const bool dedup = n_jobs > 1;
   for (uint32_t j = 0; j < n_jobs; j++) {
     const tmh::CommitPlan &pl = plans[j];
     if (pl.early) continue;
     where[j].resize(pl.entries.size());
     for (size_t e = 0; e < pl.entries.size(); e++) {
-      std::string key(reinterpret_cast<const char *>(&pl.commit), sizeof(void *));
-      const int si = pl.sig_idx[e];
-      const void *pkp = pl.entries[e].pk;
-      key.append(reinterpret_cast<const char *>(&si), sizeof si);
-      key.append(reinterpret_cast<const char *>(&pkp), sizeof pkp);
-      key.push_back(pl.batch ? 'b' : 's');
-      auto it = seen.find(key);
-      if (it != seen.end() && uniq[it->second].msg == pl.entries[e].msg) {
-        where[j][e] = it->second;
-      } else {
-        where[j][e] = (uint32_t)uniq.size();
-        seen[key] = (uint32_t)uniq.size();
-        uniq.push_back(pl.entries[e]);
+      if (dedup) {
+        const EntryKey key{pl.commit, pl.entries[e].pk, pl.sig_idx[e], pl.batch};
+        auto [it, fresh] = seen.emplace(key, (uint32_t)uniq.size());
+        if (!fresh && uniq[it->second]->msg == pl.entries[e].msg) {
+          where[j][e] = it->second;
+          continue;
+        }
+        it->second = (uint32_t)uniq.size();
       }
+      where[j][e] = (uint32_t)uniq.size();
+      uniq.push_back(&pl.entries[e]);
     }
   }
+  tm.mark("dedup");
   GpuBackend be{ctx};
   std::vector<int8_t> st = uniq.empty() ? std::vector<int8_t>() : be(uniq);
+  tm.mark("verify");
   if (be.infra < 0) {
     if (errs && err_stride) put_err(errs, err_stride, tmv_last_error());
     return be.infra;
@@ -318,6 +397,7 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
     if (errs && err_stride) put_err(errs + (size_t)j * err_stride, err_stride, e ? *e : std::string());
     bad += e ? 1 : 0;
   }
+  tm.mark("finish");
   return bad;
 }
 

@@ -173,62 +173,79 @@ struct CommitSig {
 constexpr int32_t kPrevoteType = 1;
 constexpr int32_t kPrecommitType = 2;
 
-inline void PutUvarint(Bytes &out, uint64_t x) {
-  while (x >= 0x80) {
-    out.push_back((uint8_t)(x | 0x80));
-    x >>= 7;
-  }
-  out.push_back((uint8_t)x);
+inline size_t UvarintLen(uint64_t x) {
+  size_t n = 1;
+  while (x >= 0x80) { x >>= 7; n++; }
+  return n;
 }
-inline void PutFixed64(Bytes &out, int64_t v) {
-  for (int i = 0; i < 8; i++) out.push_back((uint8_t)((uint64_t)v >> (8 * i)));
+inline uint8_t *PutUvarintP(uint8_t *p, uint64_t x) {
+  while (x >= 0x80) { *p++ = (uint8_t)(x | 0x80); x >>= 7; }
+  *p++ = (uint8_t)x;
+  return p;
+}
+inline uint8_t *PutFixed64P(uint8_t *p, int64_t v) {
+  for (int i = 0; i < 8; i++) *p++ = (uint8_t)((uint64_t)v >> (8 * i));
+  return p;
+}
+inline uint8_t *PutBytesField(uint8_t *p, uint8_t tag, const Bytes &b) {
+  *p++ = tag;
+  p = PutUvarintP(p, b.size());
+  if (!b.empty()) std::memcpy(p, b.data(), b.size());
+  return p + b.size();
 }
 
-// types.VoteSignBytes: MarshalDelimited(CanonicalizeVote(chainID, vote)).
-// block_id == nullptr or a nil BlockID omits field 4 (types/canonical.go:18-32).
+// types.VoteSignBytes: MarshalDelimited(CanonicalizeVote(chainID, vote)),
+// field by field as gogoproto emits CanonicalVote (proto3: zero fields
+// omitted; the timestamp is always present).  block_id == nullptr or a nil
+// BlockID omits field 4 (types/canonical.go:18-32).  Sizes are computed first
+// and the message is written in one pass into one buffer.
 inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t height, int32_t round,
                            const BlockID *block_id, const Timestamp &ts) {
-  Bytes body;
-  body.reserve(128);
-  if (type != 0) { body.push_back(0x08); PutUvarint(body, (uint64_t)(uint32_t)type); }
-  if (height != 0) { body.push_back(0x11); PutFixed64(body, height); }
-  if (round != 0) { body.push_back(0x19); PutFixed64(body, (int64_t)round); }
-  if (block_id && !block_id->IsNil()) {
-    Bytes psh;
-    if (block_id->part_set_header.total != 0) { psh.push_back(0x08); PutUvarint(psh, block_id->part_set_header.total); }
-    if (!block_id->part_set_header.hash.empty()) {
-      psh.push_back(0x12);
-      PutUvarint(psh, block_id->part_set_header.hash.size());
-      psh.insert(psh.end(), block_id->part_set_header.hash.begin(), block_id->part_set_header.hash.end());
-    }
-    Bytes cb;
-    if (!block_id->hash.empty()) {
-      cb.push_back(0x0a);
-      PutUvarint(cb, block_id->hash.size());
-      cb.insert(cb.end(), block_id->hash.begin(), block_id->hash.end());
-    }
-    cb.push_back(0x12);
-    PutUvarint(cb, psh.size());
-    cb.insert(cb.end(), psh.begin(), psh.end());
-    body.push_back(0x22);
-    PutUvarint(body, cb.size());
-    body.insert(body.end(), cb.begin(), cb.end());
+  const bool has_bid = block_id && !block_id->IsNil();
+  size_t psh_len = 0, cb_len = 0;
+  if (has_bid) {
+    const PartSetHeader &ph = block_id->part_set_header;
+    if (ph.total != 0) psh_len += 1 + UvarintLen(ph.total);
+    if (!ph.hash.empty()) psh_len += 1 + UvarintLen(ph.hash.size()) + ph.hash.size();
+    if (!block_id->hash.empty()) cb_len += 1 + UvarintLen(block_id->hash.size()) + block_id->hash.size();
+    cb_len += 1 + UvarintLen(psh_len) + psh_len;
   }
-  Bytes t;
-  if (ts.seconds != 0) { t.push_back(0x08); PutUvarint(t, (uint64_t)ts.seconds); }
-  if (ts.nanos != 0) { t.push_back(0x10); PutUvarint(t, (uint64_t)(int64_t)ts.nanos); }
-  body.push_back(0x2a);
-  PutUvarint(body, t.size());
-  body.insert(body.end(), t.begin(), t.end());
+  size_t t_len = 0;
+  if (ts.seconds != 0) t_len += 1 + UvarintLen((uint64_t)ts.seconds);
+  if (ts.nanos != 0) t_len += 1 + UvarintLen((uint64_t)(int64_t)ts.nanos);
+  size_t body = 0;
+  if (type != 0) body += 1 + UvarintLen((uint64_t)(uint32_t)type);
+  if (height != 0) body += 9;
+  if (round != 0) body += 9;
+  if (has_bid) body += 1 + UvarintLen(cb_len) + cb_len;
+  body += 1 + UvarintLen(t_len) + t_len;
+  if (!chain_id.empty()) body += 1 + UvarintLen(chain_id.size()) + chain_id.size();
+
+  Bytes out(UvarintLen(body) + body);
+  uint8_t *p = PutUvarintP(out.data(), body);
+  if (type != 0) { *p++ = 0x08; p = PutUvarintP(p, (uint64_t)(uint32_t)type); }
+  if (height != 0) { *p++ = 0x11; p = PutFixed64P(p, height); }
+  if (round != 0) { *p++ = 0x19; p = PutFixed64P(p, (int64_t)round); }
+  if (has_bid) {
+    const PartSetHeader &ph = block_id->part_set_header;
+    *p++ = 0x22;
+    p = PutUvarintP(p, cb_len);
+    if (!block_id->hash.empty()) p = PutBytesField(p, 0x0a, block_id->hash);
+    *p++ = 0x12;
+    p = PutUvarintP(p, psh_len);
+    if (ph.total != 0) { *p++ = 0x08; p = PutUvarintP(p, ph.total); }
+    if (!ph.hash.empty()) p = PutBytesField(p, 0x12, ph.hash);
+  }
+  *p++ = 0x2a;
+  p = PutUvarintP(p, t_len);
+  if (ts.seconds != 0) { *p++ = 0x08; p = PutUvarintP(p, (uint64_t)ts.seconds); }
+  if (ts.nanos != 0) { *p++ = 0x10; p = PutUvarintP(p, (uint64_t)(int64_t)ts.nanos); }
   if (!chain_id.empty()) {
-    body.push_back(0x32);
-    PutUvarint(body, chain_id.size());
-    body.insert(body.end(), chain_id.begin(), chain_id.end());
+    *p++ = 0x32;
+    p = PutUvarintP(p, chain_id.size());
+    std::memcpy(p, chain_id.data(), chain_id.size());
+    p += chain_id.size();
   }
-  Bytes out;
-  out.reserve(body.size() + 2);
-  PutUvarint(out, body.size());
-  out.insert(out.end(), body.begin(), body.end());
   return out;
 }
 
@@ -240,8 +257,9 @@ struct Commit {
   // types/block.go:836-862: only the timestamp and the flag differ per index
   Bytes VoteSignBytes(const std::string &chain_id, int32_t idx) const {
     const CommitSig &cs = signatures[(size_t)idx];
-    const BlockID bid = cs.BlockIDFor(block_id);
-    return tmh::VoteSignBytes(chain_id, kPrecommitType, height, round, &bid, cs.timestamp);
+    // BlockIDFor: the commit's BlockID for a Commit flag, else the nil BlockID
+    return tmh::VoteSignBytes(chain_id, kPrecommitType, height, round,
+                              cs.block_id_flag == BlockIDFlagCommit ? &block_id : nullptr, cs.timestamp);
   }
 };
 

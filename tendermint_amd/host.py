@@ -113,6 +113,81 @@ def _c_block_id(k: _Keep, b: BlockID) -> CBlockID:
     return CBlockID(h, hl, b.psh_total, p, pl)
 
 
+def _np_dtype(struct) -> "np.dtype":
+    """numpy view of a ctypes Structure (pointers as uint64), same offsets."""
+    import numpy as np
+    conv = {ctypes.c_uint8: np.uint8, ctypes.c_uint32: np.uint32, ctypes.c_int32: np.int32,
+            ctypes.c_int64: np.int64, ctypes.c_int: np.int32}
+    names, formats, offsets = [], [], []
+    for name, ty in struct._fields_:
+        names.append(name)
+        formats.append(conv.get(ty, np.uint64))
+        offsets.append(getattr(struct, name).offset)
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": ctypes.sizeof(struct)})
+
+
+_DT = {}
+
+
+def _dt(key, struct):
+    d = _DT.get(key)
+    if d is None:
+        d = _DT[key] = _np_dtype(struct)
+    return d
+
+
+def _blob_ptrs(k: _Keep, items: List[bytes]):
+    """Concatenate byte strings into one kept buffer; per-item (pointer, len),
+    pointer NULL for an empty item (as _Keep.buf)."""
+    import numpy as np
+    blob = b"".join(items)
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+    if not blob:
+        return np.zeros(len(items), np.uint64), lens
+    buf = np.frombuffer(blob, dtype=np.uint8)
+    k.refs.append(blob)
+    offs = np.zeros(len(items), np.uint64)
+    np.cumsum(lens[:-1], out=offs[1:])
+    ptrs = np.where(lens > 0, offs + np.uint64(buf.ctypes.data), np.uint64(0))
+    return ptrs, lens
+
+
+def _c_validators(k: _Keep, vals: ValidatorSet):
+    """tmv_validator[] for a validator set, built column-wise."""
+    import numpy as np
+    dt = _dt("v", CValidator)
+    vs = vals.validators
+    a = np.zeros(max(1, len(vs)), dtype=dt)
+    if vs:
+        a["address"][:len(vs)], a["address_len"][:len(vs)] = _blob_ptrs(k, [v.address for v in vs])
+        a["pub_key"][:len(vs)], a["pub_key_len"][:len(vs)] = _blob_ptrs(k, [v.pub_key for v in vs])
+        a["key_kind"][:len(vs)] = [v.key_kind for v in vs]
+        a["voting_power"][:len(vs)] = [v.voting_power for v in vs]
+        a["proposer_priority"][:len(vs)] = [v.proposer_priority for v in vs]
+    k.refs.append(a)
+    return ctypes.cast(a.ctypes.data, ctypes.POINTER(CValidator))
+
+
+def _c_commit(k: _Keep, commit: Commit) -> CCommit:
+    """tmv_commit for a Commit; its tmv_commit_sig[] built column-wise."""
+    import numpy as np
+    dt = _dt("s", CCommitSig)
+    ss = commit.signatures
+    n = len(ss)
+    a = np.zeros(max(1, n), dtype=dt)
+    if n:
+        a["block_id_flag"][:n] = [s.block_id_flag for s in ss]
+        a["validator_address"][:n], a["validator_address_len"][:n] = _blob_ptrs(k, [s.validator_address for s in ss])
+        a["ts_seconds"][:n] = [s.timestamp[0] for s in ss]
+        a["ts_nanos"][:n] = [s.timestamp[1] for s in ss]
+        a["signature"][:n], a["signature_len"][:n] = _blob_ptrs(k, [s.signature for s in ss])
+    k.refs.append(a)
+    c = CCommit(commit.height, commit.round, _c_block_id(k, commit.block_id),
+                ctypes.cast(a.ctypes.data, ctypes.POINTER(CCommitSig)), n)
+    k.refs.append(c)
+    return c
+
+
 def _setup(L):
     if getattr(L, "_tmhost_ready", False):
         return L
@@ -153,24 +228,8 @@ def _commit_call(fn, ctx_handle, mode, chain_id, vals: Optional[ValidatorSet], b
     k = _Keep()
     cvals, nv, prop = None, 0, -1
     if vals is not None:
-        arr = (CValidator * max(1, len(vals.validators)))()
-        for i, v in enumerate(vals.validators):
-            a, al = k.buf(v.address)
-            p, pl = k.buf(v.pub_key)
-            arr[i] = CValidator(a, al, p, pl, v.key_kind, v.voting_power, v.proposer_priority)
-        k.refs.append(arr)
-        cvals, nv, prop = arr, len(vals.validators), vals.proposer_index
-    ccommit = None
-    if commit is not None:
-        sigs = (CCommitSig * max(1, len(commit.signatures)))()
-        for i, s in enumerate(commit.signatures):
-            a, al = k.buf(s.validator_address)
-            g, gl = k.buf(s.signature)
-            sigs[i] = CCommitSig(s.block_id_flag, a, al, s.timestamp[0], s.timestamp[1], g, gl)
-        k.refs.append(sigs)
-        cc = CCommit(commit.height, commit.round, _c_block_id(k, commit.block_id), sigs, len(commit.signatures))
-        k.refs.append(cc)
-        ccommit = ctypes.byref(cc)
+        cvals, nv, prop = _c_validators(k, vals), len(vals.validators), vals.proposer_index
+    ccommit = ctypes.byref(_c_commit(k, commit)) if commit is not None else None
     bid = ctypes.byref(_c_block_id(k, block_id)) if block_id is not None else None
     err = ctypes.create_string_buffer(4096)
     rc = fn(ctx_handle, mode, chain_id.encode(), cvals, nv, prop, bid, height, ccommit, trust[0], trust[1], err,
@@ -254,19 +313,10 @@ class PreparedCommitCall:
         L = _setup(_native.lib())
         self._L, self._ctx = L, ctx
         k = _Keep()
-        arr = (CValidator * max(1, len(vals.validators)))()
-        for i, v in enumerate(vals.validators):
-            a, al = k.buf(v.address)
-            p, pl = k.buf(v.pub_key)
-            arr[i] = CValidator(a, al, p, pl, v.key_kind, v.voting_power, v.proposer_priority)
-        sigs = (CCommitSig * max(1, len(commit.signatures)))()
-        for i, s in enumerate(commit.signatures):
-            a, al = k.buf(s.validator_address)
-            g, gl = k.buf(s.signature)
-            sigs[i] = CCommitSig(s.block_id_flag, a, al, s.timestamp[0], s.timestamp[1], g, gl)
-        cc = CCommit(commit.height, commit.round, _c_block_id(k, commit.block_id), sigs, len(commit.signatures))
+        arr = _c_validators(k, vals)
+        cc = _c_commit(k, commit)
         bid = _c_block_id(k, block_id) if block_id is not None else None
-        self._keep = (k, arr, sigs, cc, bid)
+        self._keep = (k, arr, cc, bid)
         self._args = (mode, chain_id.encode(), arr, len(vals.validators), vals.proposer_index,
                       ctypes.byref(bid) if bid is not None else None, height, ctypes.byref(cc), trust[0], trust[1])
         self._err = ctypes.create_string_buffer(4096)
@@ -311,27 +361,13 @@ class PreparedJobs:
             if jb.vals is not None:
                 key = id(jb.vals)
                 if key not in vcache:
-                    va = (CValidator * max(1, len(jb.vals.validators)))()
-                    for i, v in enumerate(jb.vals.validators):
-                        a, al = k.buf(v.address)
-                        p, pl = k.buf(v.pub_key)
-                        va[i] = CValidator(a, al, p, pl, v.key_kind, v.voting_power, v.proposer_priority)
-                    k.refs.append(va)
-                    vcache[key] = va
+                    vcache[key] = _c_validators(k, jb.vals)
                 cv, nv, prop = vcache[key], len(jb.vals.validators), jb.vals.proposer_index
             cc = None
             if jb.commit is not None:
                 key = id(jb.commit)
                 if key not in ccache:
-                    sigs = (CCommitSig * max(1, len(jb.commit.signatures)))()
-                    for i, s in enumerate(jb.commit.signatures):
-                        a, al = k.buf(s.validator_address)
-                        g, gl = k.buf(s.signature)
-                        sigs[i] = CCommitSig(s.block_id_flag, a, al, s.timestamp[0], s.timestamp[1], g, gl)
-                    c = CCommit(jb.commit.height, jb.commit.round, _c_block_id(k, jb.commit.block_id), sigs,
-                                len(jb.commit.signatures))
-                    k.refs += [sigs, c]
-                    ccache[key] = c
+                    ccache[key] = _c_commit(k, jb.commit)
                 cc = ctypes.pointer(ccache[key])
             bid = None
             if jb.block_id is not None:

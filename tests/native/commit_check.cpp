@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/tmhost.h"
+#include "../../include/tmverify.h"
 #include "../../tendermint_amd/csrc/host/tm_types.h"
 #include "../../tendermint_amd/csrc/sha512_dev.h"
 
@@ -37,91 +38,52 @@ int8_t fake_status(const SigEntry &e) {
   return fake_sig(*e.pk, e.msg) == e.sig ? 1 : 0;
 }
 
-Bytes b(const uint8_t *p, size_t n) { return p && n ? Bytes(p, p + n) : Bytes(); }
-KeyType kind(uint8_t k) { return k == 0 ? KeyType::Ed25519 : k == 1 ? KeyType::Sr25519 : KeyType::Other; }
-
-std::unique_ptr<ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n, int32_t prop) {
-  if (!vals) return nullptr;
-  auto vs = std::make_unique<ValidatorSet>();
-  for (uint32_t i = 0; i < n; i++)
-    vs->validators.push_back(Validator{b(vals[i].address, vals[i].address_len),
-                                       PubKey{kind(vals[i].key_kind), b(vals[i].pub_key, vals[i].pub_key_len)},
-                                       vals[i].voting_power, vals[i].proposer_priority});
-  vs->proposer = prop;
-  return vs;
-}
-
-BlockID bid_of(const tmv_block_id &x) {
-  BlockID r;
-  r.hash = b(x.hash, x.hash_len);
-  r.part_set_header.total = x.psh_total;
-  r.part_set_header.hash = b(x.psh_hash, x.psh_hash_len);
-  return r;
-}
-
-std::unique_ptr<Commit> commit_of(const tmv_commit *commit) {
-  if (!commit) return nullptr;
-  auto cm = std::make_unique<Commit>();
-  cm->height = commit->height;
-  cm->round = commit->round;
-  cm->block_id = bid_of(commit->block_id);
-  for (uint32_t i = 0; i < commit->n_sigs; i++) {
-    const tmv_commit_sig &s = commit->sigs[i];
-    cm->signatures.push_back(CommitSig{(BlockIDFlag)s.block_id_flag, b(s.validator_address, s.validator_address_len),
-                                       Timestamp{s.ts_seconds, s.ts_nanos}, b(s.signature, s.signature_len)});
-  }
-  return cm;
-}
-
 }  // namespace
+
+// The host layer under test is the product's own tm_host_abi.cpp, linked
+// into this library; only the device entry points it calls
+// (include/tmverify.h) are replaced by the test double below.
+struct tmv_ctx {
+  int unused;
+};
 
 extern "C" {
 int commitcheck_backend_calls = 0;
 int commitcheck_entries_verified = 0;
+int g_skip_hash = 0;  // timing of the host layer alone (tools only)
+
+const char *tmv_last_error(void) { return "fake device error"; }
+
+int tmv_verify_batch_ex(tmv_ctx *, uint8_t key_kind, uint32_t, const uint8_t *pk, const uint8_t *sig,
+                        const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
+  commitcheck_backend_calls++;
+  commitcheck_entries_verified += (int)n;
+  const Bytes dummy_pk;
+  bool all = n > 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const Bytes key(pk + 32 * i, pk + 32 * i + 32);
+    SigEntry e{key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, &key,
+               Bytes(msg + msg_off[i], msg + msg_off[i + 1]), Bytes(sig + 64 * i, sig + 64 * i + 64)};
+    status_out[i] = g_skip_hash ? 1 : fake_status(e);
+    all = all && status_out[i] == 1;
+  }
+  return all ? TMV_ALL_VALID : TMV_NOT_ALL;
+}
+
+static tmv_ctx g_ctx;
 
 // Same contract as tmv_verify_commits (include/tmhost.h), fake signatures.
 int commitcheck_verify_commits(const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                                size_t err_stride) {
-  std::vector<std::unique_ptr<ValidatorSet>> vs;
-  std::vector<std::unique_ptr<Commit>> cs;
-  std::vector<CommitPlan> plans;
-  for (uint32_t j = 0; j < n_jobs; j++) {
-    const tmv_commit_job &jb = jobs[j];
-    vs.push_back(vals_of(jb.vals, jb.n_vals, jb.proposer_index));
-    cs.push_back(commit_of(jb.commit));
-    const BlockID bid = jb.block_id ? bid_of(*jb.block_id) : BlockID{};
-    plans.push_back(CommitVerifier::Plan((CommitVerifier::Mode)jb.mode, jb.chain_id ? jb.chain_id : "", vs.back().get(),
-                                         bid, jb.height, cs.back().get(), jb.trust_num, jb.trust_den));
-  }
-  CommitVerifier cv;
-  cv.backend = [](const std::vector<SigEntry> &es) {
-    commitcheck_backend_calls++;
-    commitcheck_entries_verified += (int)es.size();
-    std::vector<int8_t> st(es.size());
-    for (size_t i = 0; i < es.size(); i++) st[i] = fake_status(es[i]);
-    return st;
-  };
-  std::vector<Error> out = cv.VerifyMany(plans);
-  int bad = 0;
-  for (uint32_t j = 0; j < n_jobs; j++) {
-    if (results) results[j] = out[j] ? 1 : 0;
-    const std::string s = out[j] ? *out[j] : std::string();
-    char *dst = errs + (size_t)j * err_stride;
-    std::strncpy(dst, s.c_str(), err_stride - 1);
-    dst[err_stride - 1] = 0;
-    bad += out[j] ? 1 : 0;
-  }
-  return bad;
+  return tmv_verify_commits(&g_ctx, jobs, n_jobs, results, errs, err_stride);
 }
 
 int commitcheck_verify_commit(int mode, const char *chain_id, const tmv_validator *vals, uint32_t n_vals,
                               int32_t proposer_index, const tmv_block_id *block_id, int64_t height,
                               const tmv_commit *commit, int64_t trust_num, int64_t trust_den, char *err,
                               size_t err_cap) {
-  tmv_commit_job jb{mode, chain_id, vals, n_vals, proposer_index, block_id, height, commit, trust_num, trust_den};
-  int32_t r = 0;
-  commitcheck_verify_commits(&jb, 1, &r, err, err_cap);
-  return r;
+  return tmv_verify_commit(&g_ctx, mode, chain_id, vals, n_vals, proposer_index, block_id, height, commit, trust_num,
+                           trust_den, err, err_cap);
 }
 
 size_t commitcheck_canonical_time(int64_t secs, int32_t nanos, char *out, size_t cap) {
