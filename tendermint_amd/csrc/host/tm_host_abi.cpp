@@ -181,7 +181,11 @@ namespace {
 // Run fn(i) for i in [0, n) on up to 16 host threads (serial when small).
 template <class F>
 void parallel_for(size_t n, size_t min_per_thread, F fn) {
-  const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  static const size_t hw = [] {
+    const char *e = std::getenv("TMV_HOST_THREADS");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? (size_t)v : (size_t)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  }();
   const size_t nt = std::min(hw, n / std::max<size_t>(1, min_per_thread));
   if (nt <= 1) {
     for (size_t i = 0; i < n; i++) fn(i);

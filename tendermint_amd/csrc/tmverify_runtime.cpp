@@ -133,14 +133,25 @@ struct KeyIndex {
   size_t size() const { return live; }
 };
 
+// Scratch of one launch stream: prep outputs (Ed25519Work), mixed-batch
+// partition, and the event that orders reuse of these buffers.
+struct Workspace {
+  DeviceBuf work, work2, idx;
+  hipEvent_t done = nullptr;
+};
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
   tmv::ge_precomp *d_btable = nullptr;   // 32x8 comb (single-lane kernel)
   tmv::fe *d_btab_q = nullptr;           // 8 x CachedQ multiples of B (quad kernel)
   tmv::strobe_t *d_prefix = nullptr;     // sr25519 transcript prefix (empty context)
-  DeviceBuf d_in, d_out, h_in, h_out, d_work, d_work2, d_idx;
-  hipEvent_t work_done = nullptr;        // orders workspace reuse across streams
+  DeviceBuf d_in, d_out, h_in, h_out;
+  // one workspace per launch stream, so device-resident batches issued on
+  // different caller streams run concurrently (the context's own stream is
+  // one of them)
+  std::unordered_map<hipStream_t, std::unique_ptr<Workspace>> ws;
+  hipEvent_t work_done = nullptr;        // orders key-build staging reuse
   tmv::fe *d_bcomb = nullptr;            // 32 x 128 CachedQ: (m+1) 256^j B (key-cached path)
   // expanded-key cache (device table + host LRU index)
   tmv::KeyTable kt{nullptr, nullptr};
@@ -366,58 +377,68 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   return 0;
 }
 
-// Make the workspace(s) big enough for n entries and order this launch after
-// the previous user of the workspace.  Caller holds d.mu.
-static int reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s) {
+// The workspace of stream s, big enough for n entries, with this launch
+// ordered after the previous user of that workspace.  Caller holds d.mu.
+static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s, int *rc) {
+  auto &slot = d.ws[s];
+  if (!slot) {
+    slot = std::make_unique<Workspace>();
+    hipError_t e = hipEventCreateWithFlags(&slot->done, hipEventDisableTiming);
+    if (e != hipSuccess) { set_error("hipEventCreate", e); *rc = TMV_ERR_NO_DEVICE; d.ws.erase(s); return nullptr; }
+  }
+  Workspace &w = *slot;
   const size_t need = tmv::Ed25519Work::bytes(n);
   const size_t idx_need = 2ull * 4 * n + 64;
-  if (need > d.d_work.cap || (mixed && (need > d.d_work2.cap || idx_need > d.d_idx.cap))) {
-    (void)hipEventSynchronize(d.work_done);  // old buffers may still be in use
+  if (need > w.work.cap || (mixed && (need > w.work2.cap || idx_need > w.idx.cap))) {
+    (void)hipEventSynchronize(w.done);  // old buffers may still be in use
     hipError_t e;
-    if ((e = d.d_work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); return TMV_ERR_NOMEM; }
+    if ((e = w.work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
     if (mixed) {
-      if ((e = d.d_work2.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work2)", e); return TMV_ERR_NOMEM; }
-      if ((e = d.d_idx.ensure(idx_need, false)) != hipSuccess) { set_error("hipMalloc(idx)", e); return TMV_ERR_NOMEM; }
+      if ((e = w.work2.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work2)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
+      if ((e = w.idx.ensure(idx_need, false)) != hipSuccess) { set_error("hipMalloc(idx)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
     }
   }
-  (void)hipStreamWaitEvent(s, d.work_done, 0);
-  return 0;
+  *rc = 0;
+  return &w;
 }
 
 static int launch_sr25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
                           uint32_t n, int8_t *status, hipStream_t s) {
-  int rc = reserve_work(d, n, false, s);
-  if (rc != 0) return rc;
-  tmv::Ed25519Work w = tmv::Ed25519Work::carve(d.d_work.ptr, n);
+  int rc;
+  Workspace *ws = reserve_work(d, n, false, s, &rc);
+  if (!ws) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
   hipError_t e = tmv::launch_sr25519_verify_quad(pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w, status, s);
   if (e != hipSuccess) { set_error("sr25519 launch", e); return TMV_ERR_LAUNCH; }
-  (void)hipEventRecord(d.work_done, s);
+  (void)hipEventRecord(ws->done, s);
   return 0;
 }
 
 static int launch_mixed(Device &d, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                         const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
-  int rc = reserve_work(d, n, true, s);
-  if (rc != 0) return rc;
-  tmv::Ed25519Work w1 = tmv::Ed25519Work::carve(d.d_work.ptr, n);
-  tmv::Ed25519Work w2 = tmv::Ed25519Work::carve(d.d_work2.ptr, n);
-  uint32_t *ib = static_cast<uint32_t *>(d.d_idx.ptr);
+  int rc;
+  Workspace *ws = reserve_work(d, n, true, s, &rc);
+  if (!ws) return rc;
+  tmv::Ed25519Work w1 = tmv::Ed25519Work::carve(ws->work.ptr, n);
+  tmv::Ed25519Work w2 = tmv::Ed25519Work::carve(ws->work2.ptr, n);
+  uint32_t *ib = static_cast<uint32_t *>(ws->idx.ptr);
   uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n;
   hipError_t e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed,
                                           idx_sr, status, s);
   if (e != hipSuccess) { set_error("mixed launch", e); return TMV_ERR_LAUNCH; }
-  (void)hipEventRecord(d.work_done, s);
+  (void)hipEventRecord(ws->done, s);
   return 0;
 }
 
 static int launch_cached(Device &d, bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                          const uint32_t *off, const uint32_t *slots, uint32_t n, uint8_t *out, hipStream_t s) {
-  int rc = reserve_work(d, n, false, s);
-  if (rc != 0) return rc;
-  tmv::Ed25519Work w = tmv::Ed25519Work::carve(d.d_work.ptr, n);
+  int rc;
+  Workspace *ws = reserve_work(d, n, false, s, &rc);
+  if (!ws) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
   hipError_t e = tmv::launch_verify_cached(sr, pk, sig, msg, off, slots, n, d.kt, d.d_bcomb, d.d_prefix, w, out, s);
   if (e != hipSuccess) { set_error("cached verify launch", e); return TMV_ERR_LAUNCH; }
-  (void)hipEventRecord(d.work_done, s);
+  (void)hipEventRecord(ws->done, s);
   return 0;
 }
 
@@ -433,12 +454,13 @@ static int launch_ed25519(Device &d, const uint8_t *pk, const uint8_t *sig, cons
     if (e != hipSuccess) { set_error("k_ed25519_verify launch", e); return TMV_ERR_LAUNCH; }
     return 0;
   }
-  int rc = reserve_work(d, n, false, s);
-  if (rc != 0) return rc;
-  tmv::Ed25519Work w = tmv::Ed25519Work::carve(d.d_work.ptr, n);
+  int rc;
+  Workspace *ws = reserve_work(d, n, false, s, &rc);
+  if (!ws) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
   e = tmv::launch_ed25519_verify_quad(pk, sig, msg, off, n, d.d_btab_q, w, valid, s);
   if (e != hipSuccess) { set_error("k_ed25519_verify_quad launch", e); return TMV_ERR_LAUNCH; }
-  (void)hipEventRecord(d.work_done, s);
+  (void)hipEventRecord(ws->done, s);
   return 0;
 }
 
@@ -477,14 +499,19 @@ void tmv_close(tmv_ctx *ctx) {
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     d->d_in.release();
     d->d_out.release();
-    d->d_work.release();
-    d->d_work2.release();
+    for (auto &kv : d->ws) {
+      if (kv.second->done) (void)hipEventSynchronize(kv.second->done);
+      kv.second->work.release();
+      kv.second->work2.release();
+      kv.second->idx.release();
+      if (kv.second->done) (void)hipEventDestroy(kv.second->done);
+    }
+    d->ws.clear();
     d->d_kbuild.release();
     d->h_kbuild.release();
     if (d->kt.tab) (void)hipFree(d->kt.tab);
     if (d->kt.ok) (void)hipFree(d->kt.ok);
     if (d->d_bcomb) (void)hipFree(d->d_bcomb);
-    d->d_idx.release();
     if (d->d_prefix) (void)hipFree(d->d_prefix);
     if (d->d_btab_q) (void)hipFree(d->d_btab_q);
     if (d->work_done) (void)hipEventDestroy(d->work_done);

@@ -16,7 +16,7 @@ run() {
   return 0
 }
 run list rocprofv3 -L
-run trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py --no-cpu-baseline --steps 20
+run trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py
 run fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
 run write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
 run valu rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES --output-format csv -d $OUT/valu -o valu -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
