@@ -100,6 +100,36 @@ int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk,
 #define TMV_FLAG_KEY_CACHE 1u
 int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out);
+/* Batch equation (random linear combination), the
+ * check voi's BatchVerifier.Verify runs (crypto/ed25519/ed25519.go:231-233,
+ * crypto/sr25519/batch.go:44-47): entries are split into groups of
+ * 2^group_log2 consecutive signatures of one kind; each group is checked with
+ * one multi-scalar multiplication under fresh 128-bit random weights
+ * (ed25519: cofactored [8](...) == O, ZIP-215; sr25519: Ristretto identity)
+ * and the entries of a failing group are verified one by one, so the
+ * validity vector is the same as per-entry verification (false accept
+ * probability <= 2^-128 per group, as the reference's).
+ *   TMV_FLAG_BATCH_EQUATION  use it for this call
+ *   TMV_FLAG_PER_ENTRY       never use it for this call
+ * Neither flag: batch equation when n >= $TMV_MSM_MIN (unset = never).
+ * TMV_FLAG_BATCH_EQUATION overrides TMV_FLAG_KEY_CACHE. */
+#define TMV_FLAG_BATCH_EQUATION 2u
+#define TMV_FLAG_PER_ENTRY 4u
+/* group_log2: 0 = default (6) or 5..10; window_bits: 0 = chosen from the group
+ * size, or 4..9; seed32: NULL = a fresh getrandom() key per call (production),
+ * else a fixed ChaCha20 key (tests: reproducible weights).
+ * opt_flags: TMV_BATCHOPT_STATS = count group verdicts (host-buffer calls;
+ * costs one small device read per call). */
+#define TMV_BATCHOPT_STATS 1u
+int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bits, const uint8_t *seed32,
+                          uint32_t opt_flags);
+/* Groups checked / failed since the context was opened (TMV_BATCHOPT_STATS). */
+int tmv_batch_stats(tmv_ctx *ctx, uint64_t *groups, uint64_t *groups_failed);
+/* Mixed batch with flags (see tmv_verify_mixed_batch). */
+int tmv_verify_mixed_batch_ex(tmv_ctx *ctx, uint32_t flags, const uint8_t *kind, const uint8_t *pk,
+                              const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off, uint32_t n,
+                              int8_t *status_out);
+
 /* Cumulative key-cache counters over the context's devices. */
 int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t *used, uint32_t *capacity);
 
@@ -115,6 +145,13 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
 int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kind, const uint8_t *d_pk,
                                   const uint8_t *d_sig, const uint8_t *d_msg, const uint32_t *d_msg_off,
                                   uint32_t n, int8_t *d_status, void *stream);
+/* Device-resident batch with flags; key_kind TMV_KIND_ED25519, TMV_KIND_SR25519
+ * or TMV_KIND_MIXED (then d_kind gives each entry's kind).  d_status as for
+ * tmv_sr25519_verify_batch (ed25519 entries 1/0). */
+#define TMV_KIND_MIXED 2
+int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint32_t flags, const uint8_t *d_kind,
+                               const uint8_t *d_pk, const uint8_t *d_sig, const uint8_t *d_msg,
+                               const uint32_t *d_msg_off, uint32_t n, int8_t *d_status, void *stream);
 
 #ifdef __cplusplus
 }

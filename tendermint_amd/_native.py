@@ -28,13 +28,18 @@ TMV_SR_ADDERR_SIG = -2
 TMV_KIND_ED25519 = 0
 TMV_KIND_SR25519 = 1
 TMV_FLAG_KEY_CACHE = 1
+TMV_FLAG_BATCH_EQUATION = 2
+TMV_FLAG_PER_ENTRY = 4
+TMV_BATCHOPT_STATS = 1
+TMV_KIND_MIXED = 2
 
 # Every symbol include/tmverify.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
     "tmv_open", "tmv_close", "tmv_num_devices", "tmv_last_error", "tmv_version",
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
-    "tmv_verify_batch_ex", "tmv_key_cache_stats",
+    "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
+    "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_verify_commit", "tmv_verify_commits",
@@ -83,6 +88,11 @@ def lib() -> ctypes.CDLL:
                                           i8p]
         L.tmv_key_cache_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        L.tmv_set_batch_options.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint32]
+        L.tmv_batch_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.tmv_verify_mixed_batch_ex.argtypes = [vp, ctypes.c_uint32, u8p, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
+        L.tmv_verify_batch_device_ex.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32, vp, vp, vp, vp,
+                                                 vp, ctypes.c_uint32, vp, vp]
         L.tmv_ed25519_verify_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         L.tmv_verify_mixed_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         _lib = L
@@ -183,6 +193,44 @@ class Context:
                                                        _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
                          "tmv_verify_batch_ex")
         return rc == TMV_ALL_VALID, out[:n]
+
+    def verify_mixed_batch_ex(self, flags: int, kind, pk, sig, msg, off):
+        n = len(off) - 1
+        out = np.zeros(max(n, 1), np.int8)
+        msg = msg if len(msg) else np.zeros(1, np.uint8)
+        kind = kind if len(kind) else np.zeros(1, np.uint8)
+        pk = pk if len(pk) else np.zeros(1, np.uint8)
+        sig = sig if len(sig) else np.zeros(1, np.uint8)
+        rc = self._check(self._lib.tmv_verify_mixed_batch_ex(self._h, flags, _p(kind), _p(pk), _p(sig), _p(msg),
+                                                             _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
+                         "tmv_verify_mixed_batch_ex")
+        return rc == TMV_ALL_VALID, out[:n]
+
+    def set_batch_options(self, group_log2: int = 0, window_bits: int = 0, seed: bytes | None = None,
+                          stats: bool = False) -> None:
+        """Batch-equation options (tmv_set_batch_options): group size 2^group_log2,
+        window bits, a fixed ChaCha20 key (tests only; None = fresh randomness
+        per call) and group-verdict counting."""
+        sp = None
+        if seed is not None:
+            if len(seed) != 32:
+                raise ValueError("seed must be 32 bytes")
+            self._seed_buf = np.frombuffer(seed, np.uint8).copy()
+            sp = _p(self._seed_buf)
+        self._check(self._lib.tmv_set_batch_options(self._h, group_log2, window_bits, sp,
+                                                    TMV_BATCHOPT_STATS if stats else 0),
+                    "tmv_set_batch_options")
+
+    def batch_stats(self):
+        g, f = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._lib.tmv_batch_stats(self._h, ctypes.byref(g), ctypes.byref(f)), "tmv_batch_stats")
+        return {"groups": g.value, "failed": f.value}
+
+    def verify_batch_device_ex(self, device: int, key_kind: int, flags: int, d_kind: int, d_pk: int, d_sig: int,
+                               d_msg: int, d_off: int, n: int, d_status: int, stream: int = 0) -> None:
+        self._check(self._lib.tmv_verify_batch_device_ex(self._h, device, key_kind, flags, d_kind or None, d_pk,
+                                                         d_sig, d_msg, d_off, n, d_status, stream or None),
+                    "tmv_verify_batch_device_ex")
 
     def key_cache_stats(self):
         h, m = ctypes.c_uint64(), ctypes.c_uint64()

@@ -293,6 +293,7 @@ std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n
     v.proposer_priority = vals[i].proposer_priority;
   }
   vs->proposer = proposer_index;
+  vs->UpdateTotalVotingPower();
   return vs;
 }
 

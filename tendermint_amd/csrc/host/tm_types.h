@@ -277,13 +277,20 @@ struct Validator {
 struct ValidatorSet {
   std::vector<Validator> validators;
   int proposer = -1;  // index of the current proposer, -1 = derive from priorities
-  mutable int64_t total_voting_power = 0;
+  int64_t total_voting_power = 0;  // 0 = not precomputed (see UpdateTotalVotingPower)
 
   size_t Size() const { return validators.size(); }
+  // Read-only: plans of one batch run on several threads over a shared set,
+  // so the getter never writes; converters call UpdateTotalVotingPower once.
   int64_t TotalVotingPower() const {
-    if (total_voting_power == 0)
-      for (const auto &v : validators) total_voting_power += v.voting_power;
-    return total_voting_power;
+    if (total_voting_power != 0) return total_voting_power;
+    int64_t t = 0;
+    for (const auto &v : validators) t += v.voting_power;
+    return t;
+  }
+  void UpdateTotalVotingPower() {
+    total_voting_power = 0;
+    total_voting_power = TotalVotingPower();
   }
   // types/validator_set.go:267-274 (linear scan, like the reference)
   std::pair<int32_t, const Validator *> GetByAddress(const Bytes &addr) const {

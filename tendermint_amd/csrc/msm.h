@@ -1,0 +1,196 @@
+// Random-linear-combination batch check: the
+// device analogue of curve25519-voi's BatchVerifier.Verify behind
+// crypto/ed25519/ed25519.go:231-233 and crypto/sr25519/batch.go:44-47.
+//
+// For a group g of entries (m consecutive signatures of one key kind) with
+// random 128-bit z_i (device ChaCha20, key drawn from getrandom per call):
+//   T_g = [sum z_i s_i mod l] B + sum [z_i] (-R_i) + sum [z_i k_i mod l] (-A_i)
+// ed25519 (ZIP-215, cofactored): group passes iff [8] T_g == O
+// sr25519 (Ristretto):           group passes iff T_g is the Ristretto identity
+// Entries that failed decoding / the S check are left out of the sums (their
+// status is already known).  A passing group makes every remaining entry
+// valid (false accept probability <= 2^-128 per group, as voi's); a failing
+// group's entries are verified one by one (row H: k_verify_quad with the
+// group verdicts), so the validity vector is exact.
+//
+// Pippenger over the 2m+1 points of a group with signed c-bit digits:
+//   k_msm_sort   one workgroup per group: scalars, digits, LDS counting sort
+//                of (window, |digit|) bucket entries into the group's region
+//   k_msm_accum  one lane per kChunk consecutive sorted entries: runs of one
+//                bucket are summed (mixed additions, Niels points); runs that
+//                cross a chunk edge leave partial sums
+//   k_msm_group  one workgroup per group: bucket values (merging partials),
+//                per-window running sums split over lanes, then the Horner
+//                combination over windows in quad-lane arithmetic and the
+//                group verdict
+#pragma once
+#include <stdint.h>
+#include "curve25519.h"
+
+namespace tmv {
+
+constexpr int kMsmChunk = 8;                 // sorted entries per accumulation lane
+constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
+constexpr int kMsmSortBlock = 256;
+constexpr int kMsmGroupBlock = 256;
+
+// Affine Niels point padded to one 128-byte line.
+struct alignas(16) niels_pt {
+  fe ypx, ymx, xy2d;
+  int32_t pad[2];
+};
+
+struct MsmParams {
+  uint32_t m_log2;   // group size = 1 << m_log2 (>= 5, so a 16-signature quad block never spans groups)
+  uint32_t c;        // window bits
+  uint32_t W;        // windows for a scalar < 2^253: ceil(254 / c)
+  uint32_t WR;       // windows for z < 2^128: ceil(129 / c)
+  uint32_t H;        // buckets per window = 2^(c-1)
+  uint32_t cap;      // sorted-entry slots per group (multiple of kMsmChunk)
+  uint32_t groups;   // groups allocated = ceil(n / m)
+  uint32_t P;        // lanes per window in k_msm_group (power of two <= H)
+
+  TMV_HD uint32_t m() const { return 1u << m_log2; }
+  TMV_HD uint32_t buckets_per_group() const { return W * H; }
+  TMV_HD uint32_t chunks_per_group() const { return cap / kMsmChunk; }
+
+  static MsmParams make(uint32_t n, uint32_t m_log2, uint32_t c) {
+    MsmParams p;
+    p.m_log2 = m_log2;
+    p.c = c;
+    p.W = (254 + c - 1) / c;
+    p.WR = (129 + c - 1) / c;
+    p.H = 1u << (c - 1);
+    const uint32_t m = 1u << m_log2;
+    const uint32_t slots = (2 * m + 1) * p.W;
+    p.cap = (slots + kMsmChunk - 1) / kMsmChunk * kMsmChunk;
+    p.groups = (n + m - 1) >> m_log2;
+    uint32_t P = 1;
+    while (2 * P <= p.H && 2 * P * p.W <= (uint32_t)kMsmGroupBlock) P *= 2;
+    p.P = P;
+    return p;
+  }
+};
+
+// Device workspace of the batch check (all per launch stream).
+struct MsmWork {
+  niels_pt *pts;       // 2n+1: [2e] = -R_e, [2e+1] = -A_e, [2n] = B
+  uint32_t *ent_pt;    // groups x cap: point index << 1 | negate
+  uint32_t *ent_bk;    // groups x cap: global bucket id, kMsmEmpty for padding
+  uint32_t *bk_start;  // groups x W x H: first sorted slot of the bucket
+  uint32_t *bk_cnt;    // groups x W x H
+  ge_p3 *bk_sum;       // groups x W x H: sums of buckets that fit in one chunk
+  ge_p3 *part_first;   // chunks: run that began in an earlier chunk and ends here
+  ge_p3 *part_last;    // chunks: run that continues into the next chunk
+  uint8_t *group_ok;   // groups
+  uint32_t n_pts;      // index of B (= 2n)
+
+  static size_t bytes(uint32_t n, const MsmParams &p) {
+    const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
+    const size_t chunks = ent / kMsmChunk;
+    return (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
+           2 * chunks * sizeof(ge_p3) + G + 16 * 10;
+  }
+  static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
+    auto up = [](size_t x) { return (x + 15) & ~size_t(15); };
+    uint8_t *b = static_cast<uint8_t *>(base);
+    const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
+    const size_t chunks = ent / kMsmChunk;
+    MsmWork w;
+    size_t o = 0;
+    w.pts = reinterpret_cast<niels_pt *>(b + o); o = up(o + (2ull * n + 1) * sizeof(niels_pt));
+    w.ent_pt = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * ent);
+    w.ent_bk = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * ent);
+    w.bk_start = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * bk);
+    w.bk_cnt = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * bk);
+    w.bk_sum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + bk * sizeof(ge_p3));
+    w.part_first = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
+    w.part_last = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
+    w.group_ok = b + o;
+    w.n_pts = 2 * n;
+    return w;
+  }
+};
+
+// Per-call randomness: ChaCha20 key (from getrandom, or a caller seed in
+// tests) and a nonce that separates the launches of one call.
+struct MsmSeed {
+  uint32_t key[8];
+  uint32_t nonce[3];
+};
+
+// ---------------------------------------------------------------- ChaCha20
+// RFC 8439 block function; z_e = first 16 bytes of block (key, counter = e,
+// nonce).  Row I: the reference draws z from rand.Reader
+// (crypto/ed25519/ed25519.go:232).
+TMV_HD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+#define TMV_QR(a, b, c, d)              \
+  a += b; d ^= a; d = rotl32(d, 16);    \
+  c += d; b ^= c; b = rotl32(b, 12);    \
+  a += b; d ^= a; d = rotl32(d, 8);     \
+  c += d; b ^= c; b = rotl32(b, 7);
+
+TMV_HD void chacha20_block(uint32_t out[16], const uint32_t key[8], uint32_t counter, const uint32_t nonce[3]) {
+  uint32_t x[16];
+  x[0] = 0x61707865u; x[1] = 0x3320646eu; x[2] = 0x79622d32u; x[3] = 0x6b206574u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[4 + i] = key[i];
+  x[12] = counter;
+  x[13] = nonce[0]; x[14] = nonce[1]; x[15] = nonce[2];
+  uint32_t s[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = x[i];
+#pragma unroll 1
+  for (int r = 0; r < 10; r++) {
+    TMV_QR(s[0], s[4], s[8], s[12]);
+    TMV_QR(s[1], s[5], s[9], s[13]);
+    TMV_QR(s[2], s[6], s[10], s[14]);
+    TMV_QR(s[3], s[7], s[11], s[15]);
+    TMV_QR(s[0], s[5], s[10], s[15]);
+    TMV_QR(s[1], s[6], s[11], s[12]);
+    TMV_QR(s[2], s[7], s[8], s[13]);
+    TMV_QR(s[3], s[4], s[9], s[14]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) out[i] = s[i] + x[i];
+}
+#undef TMV_QR
+
+// ---------------------------------------------------------------- scalars
+// r = (a * b) mod l, a: na words (na <= 8), b: 8 words.
+TMV_HD void sc_mul_mod(uint32_t r[8], const uint32_t *a, int na, const uint32_t b[8]) {
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = 0;
+  for (int i = 0; i < na; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = (uint64_t)a[i] * b[j] + x[i + j] + carry;
+      x[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    x[i + 8] = (uint32_t)carry;
+  }
+  sc_reduce512(r, x);
+}
+
+// Signed digit of window w (c bits) of a scalar of nw words, given the carry
+// of window w-1; top window keeps a digit in [0, 2^(c-1)] (no carry out).
+TMV_HD int sc_window_digit(const uint32_t *s, int nw, uint32_t w, uint32_t c, bool top, int &carry) {
+  const uint32_t bit = w * c;
+  const uint32_t wi = bit >> 5, sh = bit & 31;
+  uint64_t x = wi < (uint32_t)nw ? s[wi] : 0;
+  if (wi + 1 < (uint32_t)nw) x |= (uint64_t)s[wi + 1] << 32;
+  int d = (int)((x >> sh) & ((1u << c) - 1)) + carry;
+  if (!top && d >= (1 << (c - 1))) {
+    d -= 1 << c;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return d;
+}
+
+}  // namespace tmv

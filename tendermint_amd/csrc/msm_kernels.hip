@@ -1,0 +1,444 @@
+// Batch-equation kernels (msm.h): the random-linear-combination check that
+// curve25519-voi's BatchVerifier.Verify performs behind
+// crypto/ed25519/ed25519.go:231-233 and crypto/sr25519/batch.go:44-47, laid
+// out for CDNA4: groups of m signatures, Pippenger buckets found by an LDS
+// counting sort, bucket sums by independent lanes over fixed-size chunks of
+// the sorted entries (no atomics on points), and a per-group Horner
+// combination in quad-lane arithmetic (quad.h).  All integer VALU work.
+#include <hip/hip_runtime.h>
+#include "ed25519_core.h"
+#include "kernel_util.h"
+#include "quad.h"
+#include "verify_kernels.h"
+
+namespace tmv {
+
+namespace {
+
+// word i of an nw-word scalar held in registers (static indexing: no scratch)
+template <int NW>
+__device__ __forceinline__ uint32_t word_at(const uint32_t *s, uint32_t i) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) x = (i == (uint32_t)k) ? s[k] : x;
+  return x;
+}
+
+// Signed c-bit digit of window w given the previous window's carry; the top
+// window keeps [0, 2^(c-1)] (callers size the window count so it fits).
+template <int NW>
+__device__ __forceinline__ int window_digit(const uint32_t *s, uint32_t w, uint32_t c, bool top, int &carry) {
+  const uint32_t bit = w * c;
+  const uint32_t wi = bit >> 5, sh = bit & 31;
+  const uint64_t x = (uint64_t)word_at<NW>(s, wi) | ((uint64_t)word_at<NW>(s, wi + 1) << 32);
+  int d = (int)((x >> sh) & ((1u << c) - 1)) + carry;
+  if (!top && d >= (1 << (c - 1))) {
+    d -= 1 << c;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return d;
+}
+
+// For every nonzero digit of a scalar: f(bucket within group, negative).
+template <int NW, typename F>
+__device__ __forceinline__ void for_each_digit(const uint32_t *s, uint32_t windows, const MsmParams &p, F f) {
+  int carry = 0;
+  for (uint32_t w = 0; w < windows; w++) {
+    const int d = window_digit<NW>(s, w, p.c, w + 1 == windows, carry);
+    if (d != 0) f(w * p.H + (uint32_t)((d < 0 ? -d : d) - 1), d < 0);
+  }
+}
+
+__device__ __forceinline__ void p3_add(ge_p3 &a, const ge_p3 &b) {
+  ge_cached c;
+  ge_p3_to_cached(c, b);
+  ge_p1p1 r;
+  ge_add(r, a, c);
+  ge_p1p1_to_p3(a, r);
+}
+
+__device__ __forceinline__ void p3_dbl(ge_p3 &a) {
+  ge_p1p1 r;
+  ge_p3_dbl(r, a);
+  ge_p1p1_to_p3(a, r);
+}
+
+// Bucket b's sum; false if the bucket is empty.  A bucket that fits in one
+// chunk was stored whole by k_msm_accum; a longer one is the run that left
+// its first chunk, the middle chunks and the run that ended in its last.
+__device__ bool bucket_value(const MsmWork &mw, uint32_t b, ge_p3 &out) {
+  const uint32_t cnt = mw.bk_cnt[b];
+  if (cnt == 0) return false;
+  const uint32_t bs = mw.bk_start[b];
+  const uint32_t t0 = bs / kMsmChunk, t1 = (bs + cnt - 1) / kMsmChunk;
+  if (t0 == t1) {
+    out = mw.bk_sum[b];
+    return true;
+  }
+  out = mw.part_last[t0];
+  for (uint32_t t = t0 + 1; t < t1; t++) p3_add(out, mw.part_last[t]);
+  p3_add(out, mw.part_first[t1]);
+  return true;
+}
+
+}  // namespace
+
+// One workgroup per group of m entries: z_e, z_e k_e mod l, sum z_e s_e mod l
+// (the B scalar), then a counting sort of the (window, |digit|) bucket entries
+// of the 2m+1 points into the group's slots of ent_pt/ent_bk.
+template <bool SR>
+__global__ void __launch_bounds__(kMsmSortBlock)
+k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
+           Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned) {
+  extern __shared__ uint32_t smem[];
+  const uint32_t cnt = entry_count(count_ptr, n);
+  const uint32_t g = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t e0 = g << p.m_log2;
+  if (g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
+    niels_pt bp;
+    bp.ymx = btab_q[0];
+    bp.ypx = btab_q[1];
+    bp.xy2d = btab_q[2];
+    bp.pad[0] = bp.pad[1] = 0;
+    mw.pts[mw.n_pts] = bp;
+  }
+  if (e0 >= cnt) return;  // block-uniform
+  const uint32_t mlive = min(p.m(), cnt - e0);
+  const uint32_t WH = p.W * p.H;
+  uint32_t *hist = smem;                       // WH counters, then cursors
+  uint32_t *red = smem + WH;                   // kMsmSortBlock x 9 words
+  uint32_t *scan = red + kMsmSortBlock * 9;    // kMsmSortBlock + 1
+
+  constexpr int R = 4;  // entries per thread: m <= 4 * kMsmSortBlock
+  uint32_t z[R][4], wv[R][8];
+  bool live[R];
+  uint32_t acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; t++) acc[t] = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    live[r] = false;
+#pragma unroll
+    for (int t = 0; t < 4; t++) z[r][t] = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) wv[r][t] = 0;
+    const uint32_t j = tid + r * kMsmSortBlock;
+    if (j >= mlive) continue;
+    const uint32_t e = e0 + j;
+    const uint32_t i = idx ? idx[e] : e;
+    uint32_t s_raw[8], s[8];
+    if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+    else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+    bool s_ok;
+    if (SR) {
+      s_ok = sr25519_decode_s(s, s_raw);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; t++) s[t] = s_raw[t];
+      s_ok = sc_is_canonical(s);
+    }
+    if (!(s_ok && w.flags[4 * e] && w.flags[4 * e + 1])) continue;  // left out of the sums
+    live[r] = true;
+    uint32_t blk[16];
+    chacha20_block(blk, seed.key, e, seed.nonce);
+#pragma unroll
+    for (int t = 0; t < 4; t++) z[r][t] = blk[t];
+    uint32_t k[8];
+    const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * e);
+    const uint4 k0 = kp[0], k1 = kp[1];
+    k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w;
+    k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
+    sc_mul_mod(wv[r], z[r], 4, k);
+    uint32_t u[8];
+    sc_mul_mod(u, z[r], 4, s);
+    uint64_t c = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      c += (uint64_t)acc[t] + u[t];
+      acc[t] = (uint32_t)c;
+      c >>= 32;
+    }
+    acc[8] += (uint32_t)c;
+  }
+  // B scalar = (sum of z_e s_e) mod l: block tree sum (< m l < 2^264), then Barrett
+#pragma unroll
+  for (int t = 0; t < 9; t++) red[tid * 9 + t] = acc[t];
+  __syncthreads();
+  for (uint32_t stride = kMsmSortBlock / 2; stride > 0; stride >>= 1) {
+    if (tid < stride) {
+      uint64_t c = 0;
+      for (int t = 0; t < 9; t++) {
+        c += (uint64_t)red[tid * 9 + t] + red[(tid + stride) * 9 + t];
+        red[tid * 9 + t] = (uint32_t)c;
+        c >>= 32;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    uint32_t x[16], b[8];
+    for (int t = 0; t < 16; t++) x[t] = t < 9 ? red[t] : 0;
+    sc_reduce512(b, x);
+    for (int t = 0; t < 8; t++) red[t] = b[t];
+  }
+  for (uint32_t t = tid; t < WH; t += kMsmSortBlock) hist[t] = 0;
+  __syncthreads();
+  uint32_t bsc[8];
+#pragma unroll
+  for (int t = 0; t < 8; t++) bsc[t] = red[t];
+
+  // pass 1: bucket sizes
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (!live[r]) continue;
+    for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
+    for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
+  }
+  if (tid == 0) for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
+  __syncthreads();
+
+  // exclusive scan: contiguous segments per thread, thread 0 scans the totals
+  const uint32_t seg = (WH + kMsmSortBlock - 1) / kMsmSortBlock;
+  const uint32_t lo = min(WH, tid * seg), hi = min(WH, lo + seg);
+  uint32_t local = 0;
+  for (uint32_t t = lo; t < hi; t++) local += hist[t];
+  scan[tid] = local;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int t = 0; t < kMsmSortBlock; t++) {
+      const uint32_t v = scan[t];
+      scan[t] = run;
+      run += v;
+    }
+    scan[kMsmSortBlock] = run;
+  }
+  __syncthreads();
+  const uint32_t gbase = g * p.cap;
+  const uint32_t bbase = g * WH;
+  {
+    uint32_t off = scan[tid];
+    for (uint32_t t = lo; t < hi; t++) {
+      const uint32_t c = hist[t];
+      mw.bk_start[bbase + t] = gbase + off;
+      mw.bk_cnt[bbase + t] = c;
+      hist[t] = off;  // cursor
+      off += c;
+    }
+  }
+  __syncthreads();
+
+  // pass 2: scatter (point index << 1 | negate); stored points are -R, -A, +B
+  uint32_t *ent_pt = mw.ent_pt + gbase;
+  uint32_t *ent_bk = mw.ent_bk + gbase;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (!live[r]) continue;
+    const uint32_t e = e0 + tid + r * kMsmSortBlock;
+    for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool neg) {
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      ent_pt[pos] = ((2 * e) << 1) | (neg ? 1u : 0u);
+      ent_bk[pos] = bbase + bk;
+    });
+    for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool neg) {
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      ent_pt[pos] = ((2 * e + 1) << 1) | (neg ? 1u : 0u);
+      ent_bk[pos] = bbase + bk;
+    });
+  }
+  if (tid == 0) {
+    for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool neg) {
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      ent_pt[pos] = (mw.n_pts << 1) | (neg ? 1u : 0u);
+      ent_bk[pos] = bbase + bk;
+    });
+  }
+  for (uint32_t t = scan[kMsmSortBlock] + tid; t < p.cap; t += kMsmSortBlock) ent_bk[t] = kMsmEmpty;
+}
+
+// One lane per chunk of kMsmChunk sorted entries: sums each run of equal
+// bucket ids with mixed additions.  A run that is the whole bucket goes to
+// bk_sum; a run cut by the chunk's end goes to part_last, one cut by its
+// start to part_first (k_msm_group joins them).
+__global__ void __launch_bounds__(256)
+k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t cpg = p.chunks_per_group();
+  const uint32_t g = t / cpg;
+  if (g >= p.groups) return;
+  if ((g << p.m_log2) >= entry_count(count_ptr, n)) return;
+  const uint32_t base = t * kMsmChunk;
+  uint32_t bk[kMsmChunk], pt[kMsmChunk];
+  {
+    const uint4 *b4 = reinterpret_cast<const uint4 *>(mw.ent_bk + base);
+    const uint4 *p4 = reinterpret_cast<const uint4 *>(mw.ent_pt + base);
+#pragma unroll
+    for (int q = 0; q < kMsmChunk / 4; q++) {
+      const uint4 x = b4[q], y = p4[q];
+      bk[4 * q] = x.x; bk[4 * q + 1] = x.y; bk[4 * q + 2] = x.z; bk[4 * q + 3] = x.w;
+      pt[4 * q] = y.x; pt[4 * q + 1] = y.y; pt[4 * q + 2] = y.z; pt[4 * q + 3] = y.w;
+    }
+  }
+  if (bk[0] == kMsmEmpty) return;
+  auto flush = [&](uint32_t b, uint32_t rs, uint32_t re, const ge_p3 &acc) {
+    const uint32_t bs = mw.bk_start[b], be = bs + mw.bk_cnt[b];
+    if (rs == bs && re == be) mw.bk_sum[b] = acc;
+    else if (re == base + kMsmChunk && re < be) mw.part_last[t] = acc;
+    else mw.part_first[t] = acc;
+  };
+  ge_p3 acc;
+  ge_p3_identity(acc);
+  uint32_t cur = bk[0], rs = base;
+  uint32_t j = 0;
+  bool more = true;
+#pragma unroll
+  for (int q = 0; q < kMsmChunk; q++) {
+    more = more && bk[q] != kMsmEmpty;  // padding only follows the last bucket
+    if (!more) continue;
+    if (bk[q] != cur) {
+      flush(cur, rs, base + q, acc);
+      ge_p3_identity(acc);
+      cur = bk[q];
+      rs = base + q;
+    }
+    const niels_pt P = mw.pts[pt[q] >> 1];
+    ge_precomp np;
+    const bool neg = pt[q] & 1;
+    np.ypx = neg ? P.ymx : P.ypx;
+    np.ymx = neg ? P.ypx : P.ymx;
+    fe_neg(np.xy2d, P.xy2d);
+    fe_cmov(np.xy2d, P.xy2d, !neg);
+    ge_p1p1 r;
+    ge_madd(r, acc, np);
+    ge_p1p1_to_p3(acc, r);
+    j = q + 1;
+  }
+  flush(cur, rs, base + j, acc);
+}
+
+// One workgroup per group: window sums S_w = sum_j (j+1) bucket_j, split
+// over P lanes per window (lane part q sums buckets [q s, (q+1) s) with the
+// running-sum trick; S_w = sum_q T_q + s * sum_q q U_q), then
+// T_g = sum_w 2^(c w) S_w by Horner on one quad, and the group verdict.
+template <bool SR>
+__global__ void __launch_bounds__(kMsmGroupBlock)
+k_msm_group(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  __shared__ ge_p3 Ts[kMsmGroupBlock];
+  __shared__ ge_p3 Us[kMsmGroupBlock];
+  __shared__ ge_p3 Ss[64];
+  const uint32_t g = blockIdx.x;
+  if ((g << p.m_log2) >= entry_count(count_ptr, n)) return;  // block-uniform
+  const uint32_t tid = threadIdx.x;
+  const uint32_t P = p.P, s = p.H / P;
+  const uint32_t wdx = tid / P, part = tid % P;
+  const uint32_t WH = p.W * p.H;
+  if (wdx < p.W) {
+    ge_p3 U, T;
+    bool u_set = false, t_set = false;
+    for (int i = (int)s - 1; i >= 0; i--) {
+      ge_p3 B;
+      if (bucket_value(mw, g * WH + wdx * p.H + part * s + (uint32_t)i, B)) {
+        if (u_set) p3_add(U, B);
+        else { U = B; u_set = true; }
+      }
+      if (u_set) {
+        if (t_set) p3_add(T, U);
+        else { T = U; t_set = true; }
+      }
+    }
+    if (!u_set) ge_p3_identity(U);
+    if (!t_set) ge_p3_identity(T);
+    Ts[tid] = T;
+    Us[tid] = U;
+  }
+  __syncthreads();
+  if (wdx < p.W && part == 0) {
+    ge_p3 r, t;
+    ge_p3_identity(r);
+    ge_p3_identity(t);
+    for (uint32_t q = P - 1; q >= 1; q--) {
+      p3_add(r, Us[tid + q]);
+      p3_add(t, r);
+    }
+    for (uint32_t d = s; d > 1; d >>= 1) p3_dbl(t);
+    for (uint32_t q = 0; q < P; q++) p3_add(t, Ts[tid + q]);
+    Ss[wdx] = t;
+  }
+  __syncthreads();
+  if (tid < 4) {
+    const int c = (int)tid;
+    fe acc = reinterpret_cast<const fe *>(&Ss[p.W - 1])[c];
+    fe r, q, qc;
+    for (int wI = (int)p.W - 2; wI >= 0; wI--) {
+      for (uint32_t d = 0; d < p.c; d++) {
+        quad::dbl(r, acc);
+        quad::p1p1_to_p3(acc, r);
+      }
+      q = reinterpret_cast<const fe *>(&Ss[wI])[c];
+      quad::to_cached(qc, q);
+      quad::add(r, acc, qc);
+      quad::p1p1_to_p3(acc, r);
+    }
+    bool ok;
+    if (SR) {
+      fe id;
+      quad::p3_identity(id);
+      ok = quad::ristretto_equal(acc, id);
+    } else {
+      ok = quad::is_identity_times8(acc);
+    }
+    if (c == 0) mw.group_ok[g] = ok ? 1 : 0;
+  }
+}
+
+template <bool SR>
+static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                               const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const fe *btab_q,
+                               const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                               const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  w.niels = mw.pts;
+  hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
+  if (e != hipSuccess) return e;
+  const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_msm_sort<SR>, dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx, count_ptr, n, w,
+                     mw, p, seed, btab_q, aligned);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
+  hipLaunchKernelGGL(k_msm_accum, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_msm_group<SR>, dim3(p.groups), dim3(kMsmGroupBlock), 0, stream, count_ptr, n, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream);
+}
+
+hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                              const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                              const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (sr) return launch_check<true>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream);
+  return launch_check<false>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream);
+}
+
+hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                    const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
+                                    Ed25519Work w_ed, Ed25519Work w_sr, MsmWork m_ed, MsmWork m_sr,
+                                    const MsmParams &p, const MsmSeed &seed_ed, const MsmSeed &seed_sr,
+                                    uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, int8_t *status,
+                                    hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint8_t *out = reinterpret_cast<uint8_t *>(status);
+  hipError_t e = launch_partition(kind, n, counts, idx_ed, idx_sr, out, stream);
+  if (e != hipSuccess) return e;
+  e = launch_check<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, m_ed, p, seed_ed, out,
+                          stream);
+  if (e != hipSuccess) return e;
+  return launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p, seed_sr,
+                            out, stream);
+}
+
+}  // namespace tmv

@@ -6,9 +6,11 @@
 // fails the call returns < 0 and the caller decides (the Go shim
 // re-verifies on CPU).  Product code never links the test oracle.
 #include <hip/hip_runtime.h>
+#include <sys/random.h>
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <list>
 #include <unordered_map>
@@ -136,8 +138,12 @@ struct KeyIndex {
 // Scratch of one launch stream: prep outputs (Ed25519Work), mixed-batch
 // partition, and the event that orders reuse of these buffers.
 struct Workspace {
-  DeviceBuf work, work2, idx;
+  DeviceBuf work, work2, idx, msm, msm2;
   hipEvent_t done = nullptr;
+  // last batch-equation launch on this stream (for tmv_batch_stats)
+  const uint8_t *group_ok[2] = {nullptr, nullptr};
+  uint32_t groups = 0, m_log2 = 0;
+  const uint32_t *counts = nullptr;  // mixed launches: per-kind entry counts on the device
 };
 
 struct Device {
@@ -172,6 +178,9 @@ struct Device {
 // TMV_KERNEL=quad|single overrides (A/B measurement).
 uint32_t g_quad_max = 0;
 int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
+// Batch equation (msm.h) from this many entries up (TMV_MSM_MIN; 0 = never
+// by default, callers opt in with TMV_FLAG_BATCH_EQUATION).
+uint32_t g_msm_min = 0;
 
 void read_env() {
   static std::once_flag once;
@@ -181,7 +190,30 @@ void read_env() {
     if (k && !strcmp(k, "single")) g_kernel_override = 0;
     const char *t = getenv("TMV_QUAD_MAX");
     g_quad_max = t ? (uint32_t)strtoul(t, nullptr, 10) : 49152u;
+    const char *mm = getenv("TMV_MSM_MIN");
+    g_msm_min = mm ? (uint32_t)strtoul(mm, nullptr, 10) : 0u;
   });
+}
+
+// Batch-equation parameters for n entries.  Group size: the caller's, else
+// 64 (a group of m fails with probability ~ m x the rate of entries that are
+// invalid yet decode; 64 keeps the per-entry fallback near 10% of a batch
+// with 0.2% such entries, as in BASELINE configs[1]).  Window: minimises
+// bucket additions + per-window running sums for that m (c in [4, 9]).
+tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c) {
+  if (m_log2 == 0) m_log2 = 6;
+  m_log2 = std::max<uint32_t>(5, std::min<uint32_t>(10, m_log2));
+  if (c == 0) {
+    const double m = double(1u << m_log2);
+    double best = 1e30;
+    for (uint32_t cc = 4; cc <= 9; cc++) {
+      const double W = (254 + cc - 1) / cc, WR = (129 + cc - 1) / cc, H = double(1u << (cc - 1));
+      const double cost = m * (W + WR) + 2.2 * W * H;
+      if (cost < best) { best = cost; c = cc; }
+    }
+  }
+  c = std::max<uint32_t>(4, std::min<uint32_t>(9, c));
+  return tmv::MsmParams::make(n, m_log2, c);
 }
 
 // Packed staging layout for one shard: pk | sig | off | msg (16-B aligned).
@@ -196,11 +228,84 @@ struct Layout {
   }
 };
 
+// How one launch verifies: per entry, or through the batch equation with
+// these parameters and this randomness.
+struct LaunchOpts {
+  bool batch_eq = false;
+  tmv::MsmParams p{};
+  tmv::MsmSeed seed[2]{};  // [kind]
+};
+
 }  // namespace
 
 struct tmv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
+  // batch-equation options (tmv_set_batch_options)
+  uint32_t msm_m_log2 = 0, msm_c = 0;
+  bool fixed_seed = false, stats = false;
+  uint8_t seed[32] = {0};
+  std::atomic<uint64_t> launches{0};
+  std::atomic<uint64_t> groups{0}, groups_failed{0};
+  std::mutex opt_mu;
 };
+
+// Options of one launch of n entries: per-entry or batch equation (flags,
+// else TMV_MSM_MIN), parameters and fresh randomness.
+static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n) {
+  read_env();
+  LaunchOpts o;
+  if (flags & TMV_FLAG_PER_ENTRY) o.batch_eq = false;
+  else if (flags & TMV_FLAG_BATCH_EQUATION) o.batch_eq = true;
+  else o.batch_eq = g_msm_min > 0 && n >= g_msm_min;
+  if (!o.batch_eq) return o;
+  uint8_t key[32];
+  {
+    std::lock_guard<std::mutex> lk(ctx->opt_mu);
+    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c);
+    if (ctx->fixed_seed) std::memcpy(key, ctx->seed, 32);
+  }
+  if (!ctx->fixed_seed) {
+    size_t got = 0;
+    while (got < 32) {  // the reference draws z from rand.Reader (crypto/ed25519/ed25519.go:232)
+      const ssize_t r = getrandom(key + got, 32 - got, 0);
+      if (r > 0) got += (size_t)r;
+    }
+  }
+  const uint64_t ctr = ctx->launches.fetch_add(1);
+  for (int k = 0; k < 2; k++) {
+    std::memcpy(o.seed[k].key, key, 32);
+    o.seed[k].nonce[0] = (uint32_t)ctr;
+    o.seed[k].nonce[1] = (uint32_t)(ctr >> 32);
+    o.seed[k].nonce[2] = (uint32_t)k;
+  }
+  return o;
+}
+
+// Group verdicts of the last batch-equation launch on stream s (synchronised
+// by the caller) into the context's counters.
+static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
+  auto it = d.ws.find(s);
+  if (it == d.ws.end() || !it->second->group_ok[0]) return;
+  Workspace &w = *it->second;
+  uint32_t live[2] = {0, 0};
+  if (w.counts) {
+    uint32_t c[2];
+    if (hipMemcpy(c, w.counts, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) return;
+    for (int k = 0; k < 2; k++) live[k] = (c[k] + (1u << w.m_log2) - 1) >> w.m_log2;
+  } else {
+    live[0] = w.groups;
+  }
+  for (int k = 0; k < 2; k++) {
+    if (!w.group_ok[k] || !live[k]) continue;
+    std::vector<uint8_t> ok(live[k]);
+    if (hipMemcpy(ok.data(), w.group_ok[k], live[k], hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t failed = 0;
+    for (uint8_t v : ok) failed += v ? 0 : 1;
+    ctx->groups += live[k];
+    ctx->groups_failed += failed;
+  }
+  w.group_ok[0] = w.group_ok[1] = nullptr;
+}
 
 static int init_device(Device &d) {
   hipError_t e = hipSetDevice(d.id);
@@ -379,7 +484,8 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
 
 // The workspace of stream s, big enough for n entries, with this launch
 // ordered after the previous user of that workspace.  Caller holds d.mu.
-static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s, int *rc) {
+static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s, int *rc,
+                               const tmv::MsmParams *mp = nullptr) {
   auto &slot = d.ws[s];
   if (!slot) {
     slot = std::make_unique<Workspace>();
@@ -389,7 +495,9 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
   Workspace &w = *slot;
   const size_t need = tmv::Ed25519Work::bytes(n);
   const size_t idx_need = 2ull * 4 * n + 64;
-  if (need > w.work.cap || (mixed && (need > w.work2.cap || idx_need > w.idx.cap))) {
+  const size_t msm_need = mp ? tmv::MsmWork::bytes(n, *mp) : 0;
+  if (need > w.work.cap || (mixed && (need > w.work2.cap || idx_need > w.idx.cap)) || msm_need > w.msm.cap ||
+      (mixed && msm_need > w.msm2.cap)) {
     (void)hipEventSynchronize(w.done);  // old buffers may still be in use
     hipError_t e;
     if ((e = w.work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
@@ -397,13 +505,41 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
       if ((e = w.work2.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work2)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
       if ((e = w.idx.ensure(idx_need, false)) != hipSuccess) { set_error("hipMalloc(idx)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
     }
+    if (msm_need) {
+      if ((e = w.msm.ensure(msm_need, false)) != hipSuccess) { set_error("hipMalloc(msm)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
+      if (mixed && (e = w.msm2.ensure(msm_need, false)) != hipSuccess) {
+        set_error("hipMalloc(msm2)", e);
+        *rc = TMV_ERR_NOMEM;
+        return nullptr;
+      }
+    }
   }
   *rc = 0;
   return &w;
 }
 
-static int launch_sr25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
-                          uint32_t n, int8_t *status, hipStream_t s) {
+static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *pk, const uint8_t *sig,
+                       const uint8_t *msg, const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s) {
+  int rc;
+  Workspace *ws = reserve_work(d, n, false, s, &rc, &o.p);
+  if (!ws) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
+  tmv::MsmWork mw = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
+  hipError_t e = tmv::launch_batch_check(sr, pk, sig, msg, off, nullptr, nullptr, n, d.d_btab_q, d.d_prefix, w, mw,
+                                         o.p, o.seed[sr ? 1 : 0], out, s);
+  if (e != hipSuccess) { set_error("batch check launch", e); return TMV_ERR_LAUNCH; }
+  ws->group_ok[0] = mw.group_ok;
+  ws->group_ok[1] = nullptr;
+  ws->groups = (n + o.p.m() - 1) >> o.p.m_log2;
+  ws->m_log2 = o.p.m_log2;
+  ws->counts = nullptr;
+  (void)hipEventRecord(ws->done, s);
+  return 0;
+}
+
+static int launch_sr25519(Device &d, const LaunchOpts &o, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                          const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
+  if (o.batch_eq) return batch_check(d, o, true, pk, sig, msg, off, n, reinterpret_cast<uint8_t *>(status), s);
   int rc;
   Workspace *ws = reserve_work(d, n, false, s, &rc);
   if (!ws) return rc;
@@ -414,17 +550,30 @@ static int launch_sr25519(Device &d, const uint8_t *pk, const uint8_t *sig, cons
   return 0;
 }
 
-static int launch_mixed(Device &d, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
-                        const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
+static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
+                        const uint8_t *msg, const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
   int rc;
-  Workspace *ws = reserve_work(d, n, true, s, &rc);
+  Workspace *ws = reserve_work(d, n, true, s, &rc, o.batch_eq ? &o.p : nullptr);
   if (!ws) return rc;
   tmv::Ed25519Work w1 = tmv::Ed25519Work::carve(ws->work.ptr, n);
   tmv::Ed25519Work w2 = tmv::Ed25519Work::carve(ws->work2.ptr, n);
   uint32_t *ib = static_cast<uint32_t *>(ws->idx.ptr);
   uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n;
-  hipError_t e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed,
-                                          idx_sr, status, s);
+  hipError_t e;
+  if (o.batch_eq) {
+    tmv::MsmWork m1 = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
+    tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p);
+    e = tmv::launch_mixed_batch_check(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, m1, m2, o.p,
+                                      o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s);
+    ws->group_ok[0] = m1.group_ok;
+    ws->group_ok[1] = m2.group_ok;
+    ws->groups = o.p.groups;
+    ws->m_log2 = o.p.m_log2;
+    ws->counts = counts;
+  } else {
+    e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed, idx_sr,
+                                 status, s);
+  }
   if (e != hipSuccess) { set_error("mixed launch", e); return TMV_ERR_LAUNCH; }
   (void)hipEventRecord(ws->done, s);
   return 0;
@@ -444,8 +593,9 @@ static int launch_cached(Device &d, bool sr, const uint8_t *pk, const uint8_t *s
 
 // Enqueue ed25519 verification of n device-resident entries on stream s.
 // Caller holds d.mu.  Chooses the quad or single-lane kernel.
-static int launch_ed25519(Device &d, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+static int launch_ed25519(Device &d, const LaunchOpts &o, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                           const uint32_t *off, uint32_t n, uint8_t *valid, hipStream_t s) {
+  if (o.batch_eq) return batch_check(d, o, false, pk, sig, msg, off, n, valid, s);
   read_env();
   const bool quad = g_kernel_override == 1 || (g_kernel_override == -1 && n <= g_quad_max);
   hipError_t e;
@@ -504,6 +654,8 @@ void tmv_close(tmv_ctx *ctx) {
       kv.second->work.release();
       kv.second->work2.release();
       kv.second->idx.release();
+      kv.second->msm.release();
+      kv.second->msm2.release();
       if (kv.second->done) (void)hipEventDestroy(kv.second->done);
     }
     d->ws.clear();
@@ -531,8 +683,9 @@ enum class Scheme { Ed25519, Sr25519, Mixed, Ed25519Cached, Sr25519Cached };
 
 // Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
 // Layout: pk | sig | off | msg | kind (16-B aligned pieces).
-static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
-                            const uint8_t *msg, const uint32_t *msg_off, uint32_t lo, uint32_t hi) {
+static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch, const uint8_t *kind,
+                            const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                            uint32_t lo, uint32_t hi) {
   const uint32_t n = hi - lo;
   const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
   Layout L(n, mbytes);
@@ -568,13 +721,15 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
   uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
   const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
   uint8_t *out = static_cast<uint8_t *>(d.d_out.ptr);
+  const LaunchOpts o = (sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached) ? LaunchOpts{}
+                                                                                         : make_opts(ctx, flags, n);
   int rc;
   switch (sch) {
     case Scheme::Ed25519:
-      rc = launch_ed25519(d, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, out, d.stream);
+      rc = launch_ed25519(d, o, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, out, d.stream);
       break;
     case Scheme::Sr25519:
-      rc = launch_sr25519(d, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out), d.stream);
+      rc = launch_sr25519(d, o, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out), d.stream);
       break;
     case Scheme::Ed25519Cached:
     case Scheme::Sr25519Cached:
@@ -582,7 +737,7 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
                          reinterpret_cast<uint32_t *>(dd + kind_at), n, out, d.stream);
       break;
     default:
-      rc = launch_mixed(d, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out),
+      rc = launch_mixed(d, o, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out),
                         d.stream);
   }
   if (rc != 0) return rc;
@@ -596,7 +751,7 @@ static int stage_and_launch(Device &d, Scheme sch, const uint8_t *kind, const ui
 // Host-buffer batch: shard by contiguous index ranges over the context's
 // devices, stage, launch, gather.  out gets 1 byte per entry.
 static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
-                     const uint8_t *msg, const uint32_t *msg_off, uint32_t n, uint8_t *out) {
+                     const uint8_t *msg, const uint32_t *msg_off, uint32_t n, uint8_t *out, uint32_t flags = 0) {
   if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
   if (n == 0) return TMV_NOT_ALL;
   if (!pk || !sig || !msg_off || !out || (sch == Scheme::Mixed && !kind) || (!msg && msg_off[n] != msg_off[0])) {
@@ -612,13 +767,14 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
   int rc = 0;
   for (uint32_t s = 0; s < shards && rc == 0; s++)
-    rc = stage_and_launch(*ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
+    rc = stage_and_launch(ctx, flags, *ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
   for (uint32_t s = 0; s < shards; s++) {
     Device &d = *ctx->devs[s];
     (void)hipSetDevice(d.id);
     hipError_t e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
     if (rc == 0) std::memcpy(out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
+    if (rc == 0 && ctx->stats) collect_stats(ctx, d, d.stream);
   }
   if (rc != 0) return rc;
   for (uint32_t i = 0; i < n; i++)
@@ -652,12 +808,42 @@ int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk,
 
 int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
-  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0;
+  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0 && !(flags & TMV_FLAG_BATCH_EQUATION);
   Scheme sch;
   if (key_kind == TMV_KIND_ED25519) sch = cache ? Scheme::Ed25519Cached : Scheme::Ed25519;
   else if (key_kind == TMV_KIND_SR25519) sch = cache ? Scheme::Sr25519Cached : Scheme::Sr25519;
   else { set_error("unsupported key kind"); return TMV_ERR_ARG; }
-  return run_batch(ctx, sch, nullptr, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out));
+  return run_batch(ctx, sch, nullptr, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out), flags);
+}
+
+int tmv_verify_mixed_batch_ex(tmv_ctx *ctx, uint32_t flags, const uint8_t *kind, const uint8_t *pk,
+                              const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off, uint32_t n,
+                              int8_t *status_out) {
+  return run_batch(ctx, Scheme::Mixed, kind, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out),
+                   flags);
+}
+
+int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bits, const uint8_t *seed32,
+                          uint32_t opt_flags) {
+  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
+  if ((group_log2 && (group_log2 < 5 || group_log2 > 10)) || (window_bits && (window_bits < 4 || window_bits > 9))) {
+    set_error("group_log2 must be 0 or 5..10, window_bits 0 or 4..9");
+    return TMV_ERR_ARG;
+  }
+  std::lock_guard<std::mutex> lk(ctx->opt_mu);
+  ctx->msm_m_log2 = group_log2;
+  ctx->msm_c = window_bits;
+  ctx->fixed_seed = seed32 != nullptr;
+  if (seed32) std::memcpy(ctx->seed, seed32, 32);
+  ctx->stats = (opt_flags & TMV_BATCHOPT_STATS) != 0;
+  return 0;
+}
+
+int tmv_batch_stats(tmv_ctx *ctx, uint64_t *groups, uint64_t *groups_failed) {
+  if (!ctx) return TMV_ERR_ARG;
+  if (groups) *groups = ctx->groups.load();
+  if (groups_failed) *groups_failed = ctx->groups_failed.load();
+  return 0;
 }
 
 int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t *used, uint32_t *capacity) {
@@ -684,8 +870,30 @@ int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kin
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  const LaunchOpts o = make_opts(ctx, 0, n);
   std::lock_guard<std::mutex> lk(dev->mu);
-  int rc = launch_mixed(*dev, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
+  int rc = launch_mixed(*dev, o, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
+  return rc != 0 ? rc : TMV_NOT_ALL;
+}
+
+int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint32_t flags, const uint8_t *d_kind,
+                               const uint8_t *d_pk, const uint8_t *d_sig, const uint8_t *d_msg,
+                               const uint32_t *d_msg_off, uint32_t n, int8_t *d_status, void *stream) {
+  Device *dev = find_device(ctx, device);
+  if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (n == 0) return TMV_NOT_ALL;
+  if (key_kind == TMV_KIND_MIXED && !d_kind) { set_error("mixed batch without kinds"); return TMV_ERR_ARG; }
+  if (key_kind > TMV_KIND_MIXED) { set_error("unsupported key kind"); return TMV_ERR_ARG; }
+  hipError_t e = hipSetDevice(dev->id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  const LaunchOpts o = make_opts(ctx, flags, n);
+  std::lock_guard<std::mutex> lk(dev->mu);
+  uint8_t *out = reinterpret_cast<uint8_t *>(d_status);
+  int rc;
+  if (key_kind == TMV_KIND_ED25519) rc = launch_ed25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, out, s);
+  else if (key_kind == TMV_KIND_SR25519) rc = launch_sr25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
+  else rc = launch_mixed(*dev, o, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
   return rc != 0 ? rc : TMV_NOT_ALL;
 }
 
@@ -713,8 +921,9 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  const LaunchOpts o = make_opts(ctx, 0, n);
   std::lock_guard<std::mutex> lk(dev->mu);
-  int rc = launch_ed25519(*dev, d_pk, d_sig, d_msg, d_msg_off, n, d_valid, s);
+  int rc = launch_ed25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, d_valid, s);
   return rc != 0 ? rc : TMV_NOT_ALL;
 }
 

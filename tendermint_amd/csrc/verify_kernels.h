@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include "curve25519.h"
 #include "merlin_dev.h"
+#include "msm.h"
 
 namespace tmv {
 
@@ -16,6 +17,7 @@ struct Ed25519Work {
   fe *Rc;          // n x 4 fe, CachedQ layout of R
   uint32_t *k;     // n x 8 words, k mod l
   uint8_t *flags;  // 4n bytes: decode ok for A (4e), R (4e+1)
+  niels_pt *niels; // batch check only (else null): [2e] = -R_e, [2e+1] = -A_e
   static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4) + 256; }
   // carve a workspace for n entries out of base (16-byte aligned pieces)
   static Ed25519Work carve(void *base, uint32_t n) {
@@ -25,6 +27,7 @@ struct Ed25519Work {
     w.Rc = reinterpret_cast<fe *>(b + 160ull * n);
     w.k = reinterpret_cast<uint32_t *>(b + 320ull * n);
     w.flags = b + 352ull * n;
+    w.niels = nullptr;
     return w;
   }
 };
@@ -56,6 +59,33 @@ hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uin
                                const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
                                Ed25519Work w_ed, Ed25519Work w_sr, uint32_t *counts, uint32_t *idx_ed,
                                uint32_t *idx_sr, int8_t *status, hipStream_t stream);
+
+// Batch-equation pipeline (msm.h): k_prep -> k_msm_sort -> k_msm_accum ->
+// k_msm_group -> k_verify_quad over the failed groups only.  Single key kind
+// (sr = false: ed25519, true: sr25519); idx/count_ptr as for the mixed path.
+hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                              const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                              const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream);
+// Mixed batch through the batch equation: partition, then one pipeline per kind.
+hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                    const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
+                                    Ed25519Work w_ed, Ed25519Work w_sr, MsmWork m_ed, MsmWork m_sr,
+                                    const MsmParams &p, const MsmSeed &seed_ed, const MsmSeed &seed_sr,
+                                    uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, int8_t *status,
+                                    hipStream_t stream);
+
+// Pieces of the pipelines, shared with msm_kernels.hip.
+template <bool SR>
+hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                       const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const strobe_t *prefix,
+                       Ed25519Work w, int aligned, hipStream_t stream);
+template <bool SR>
+hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                                const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
+                                uint8_t *out, int aligned, hipStream_t stream);
+hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
+                            uint8_t *out, hipStream_t stream);
 
 hipError_t launch_ed25519_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                  const uint32_t *msg_off, uint32_t n, const ge_precomp *btable,

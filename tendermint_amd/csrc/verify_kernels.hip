@@ -11,22 +11,9 @@
 #include "quad.h"
 #include "sr25519_core.h"
 #include "verify_kernels.h"
+#include "kernel_util.h"
 
 namespace tmv {
-
-__device__ __forceinline__ void load_words_unaligned(uint32_t w[8], const uint8_t *p) {
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-    w[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
-           ((uint32_t)p[4 * i + 3] << 24);
-}
-
-__device__ __forceinline__ void load_words_aligned(uint32_t w[8], const uint8_t *p) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
-  const uint4 a = q[0], b = q[1];
-  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-}
 
 __global__ void __launch_bounds__(kVerifyBlock)
 k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
@@ -59,10 +46,6 @@ k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig
 //
 // k_prep stores -A in P3Q layout, R (ed25519: CachedQ; sr25519: P3Q) and k;
 // decode failures go to flags (4 bytes per entry: A ok, R ok, s ok, -).
-
-__device__ __forceinline__ uint32_t entry_count(const uint32_t *count_ptr, uint32_t n) {
-  return count_ptr ? *count_ptr : n;
-}
 
 // Task-uniform waves: lanes [0, m) decode A, [m, 2m) decode R and [2m, 3m)
 // compute the challenge, so no wave mixes decompression with hashing.
@@ -108,6 +91,15 @@ k_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const ui
   else ok = ge_decode_zip215(P, isA ? a_w : r_w);
   if (!ok) ge_p3_identity(P);  // keep limbs bounded; the flag rejects the entry
   w.flags[4 * e + (isA ? 0 : 1)] = ok ? 1 : 0;
+  if (w.niels) {  // -P in affine Niels form for the batch equation (Z = 1)
+    niels_pt np;
+    fe t;
+    fe_sub(t, P.Y, P.X); fe_carry(np.ypx, t);
+    fe_add(t, P.Y, P.X); fe_carry(np.ymx, t);
+    fe_mul(t, P.T, consts::d2()); fe_neg(np.xy2d, t);
+    np.pad[0] = np.pad[1] = 0;
+    w.niels[2ull * e + (isA ? 1 : 0)] = np;
+  }
   fe *dst = (isA ? w.negA : w.Rc) + 4ull * e;
   if (isA || SR) {
     fe t;
@@ -169,7 +161,8 @@ constexpr int kQuadSigs = kQuadBlock / 4;
 template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
-              uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned) {
+              uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
+              const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
   __shared__ fe tabA[kQuadSigs * 8 * 4];
   __shared__ fe tabB[kBaseQuadEntries * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
@@ -181,6 +174,26 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   const bool live = raw < m;
   const uint32_t e = live ? raw : m - 1;
   const uint32_t i = idx ? idx[e] : e;
+  // Batch equation held for this block's group (groups are >= 32 entries, so
+  // the test is block-uniform): every entry that passed decoding and the S
+  // check is valid; the rest keep their pre-check status.
+  if (group_ok && group_ok[(blockIdx.x * kQuadSigs) >> group_log2]) {
+    if (!live || c != 0) return;
+    uint32_t s_raw[8], s_w[8];
+    if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+    else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+    bool s_ok;
+    if (SR) {
+      s_ok = sr25519_decode_s(s_w, s_raw);
+    } else {
+      s_ok = sc_is_canonical(s_raw);
+    }
+    const bool a_ok = w.flags[4 * e] != 0;
+    const bool r_ok = w.flags[4 * e + 1] != 0;
+    const int status = SR ? (!a_ok ? -1 : (!s_ok ? -2 : (r_ok ? 1 : 0))) : ((a_ok && r_ok && s_ok) ? 1 : 0);
+    out[i] = (uint8_t)(int8_t)status;
+    return;
+  }
   for (int t = threadIdx.x; t < kBaseQuadEntries * 4; t += kQuadBlock) tabB[t] = btab_q[t];
 
   uint32_t s_raw[8], s_w[8];
@@ -511,9 +524,43 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
   hipLaunchKernelGGL(k_verify_quad<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
-                     btab_q, out, aligned);
+                     btab_q, out, aligned, (const uint8_t *)nullptr, 0u);
   return hipGetLastError();
 }
+
+// Row H: after the batch equation, re-verify only the entries of failed
+// groups (blocks of passing groups exit after writing the pre-check status).
+template <bool SR>
+hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                                const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
+                                uint8_t *out, int aligned, hipStream_t stream) {
+  const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
+  hipLaunchKernelGGL(k_verify_quad<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
+                     btab_q, out, aligned, group_ok, group_log2);
+  return hipGetLastError();
+}
+template hipError_t launch_quad_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
+                                                const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
+                                                hipStream_t);
+template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
+                                               const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
+                                               hipStream_t);
+
+template <bool SR>
+hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                       const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const strobe_t *prefix,
+                       Ed25519Work w, int aligned, hipStream_t stream) {
+  const uint32_t pblocks = (uint32_t)((3ull * n + kVerifyBlock - 1) / kVerifyBlock);
+  hipLaunchKernelGGL(k_prep<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
+                     count_ptr, n, w, prefix, aligned);
+  return hipGetLastError();
+}
+template hipError_t launch_prep<false>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
+                                       const uint32_t *, const uint32_t *, uint32_t, const strobe_t *, Ed25519Work,
+                                       int, hipStream_t);
+template hipError_t launch_prep<true>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
+                                      const uint32_t *, const uint32_t *, uint32_t, const strobe_t *, Ed25519Work,
+                                      int, hipStream_t);
 
 hipError_t launch_ed25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                       const uint32_t *msg_off, uint32_t n, const fe *btab_q, Ed25519Work w,
@@ -541,6 +588,14 @@ hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uin
   e = launch_pipeline<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, out, stream);
   if (e != hipSuccess) return e;
   return launch_pipeline<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, out, stream);
+}
+
+hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
+                            uint8_t *out, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_partition, dim3((n + 255) / 256), dim3(256), 0, stream, kind, n, counts, idx_ed, idx_sr, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_ed25519_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,

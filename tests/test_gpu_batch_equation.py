@@ -1,0 +1,151 @@
+"""GPU parity of the batch equation: the
+random-linear-combination group check (k_msm_sort / k_msm_accum /
+k_msm_group) with the per-entry fallback over failing groups must give the
+same validity vector as the oracle, and honest groups must actually pass the
+equation (tmv_batch_stats), so a broken MSM cannot hide behind the fallback.
+"""
+import numpy as np
+import pytest
+
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import (make_c2_batch, make_commit_batch, make_mixed_batch,
+                                            make_sr25519_batch)
+
+pytestmark = pytest.mark.gpu
+
+SEED = bytes(range(32))
+ED, SR = N.TMV_KIND_ED25519, N.TMV_KIND_SR25519
+BEQ = N.TMV_FLAG_BATCH_EQUATION
+
+
+@pytest.fixture(scope="module")
+def bctx():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = N.Context(1)
+    c.set_batch_options(seed=SEED, stats=True)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def honest():
+    return make_commit_batch(1500)
+
+
+def _run(ctx, kind, b, **opts):
+    ctx.set_batch_options(seed=opts.pop("seed", SEED), stats=True, **opts)
+    s0 = ctx.batch_stats()
+    ok, st = ctx.verify_batch_ex(kind, BEQ, b.pk, b.sig, b.msg, b.off)
+    s1 = ctx.batch_stats()
+    return ok, st, s1["groups"] - s0["groups"], s1["failed"] - s0["failed"]
+
+
+def test_c2_full_size_bit_exact(bctx, golden):
+    g = golden("c2_expected.json")
+    b = make_c2_batch()
+    ok, st, groups, failed = _run(bctx, ED, b)
+    bits = np.packbits(st.astype(np.uint8), bitorder="little").tobytes().hex()
+    assert bits == g["valid_bits_hex"] and not ok
+    assert groups == (10_000 + 63) // 64
+    # 1% edge cases, of which only the bit flips decode and fail the equation
+    assert 0 < failed <= 20, failed
+
+
+def test_honest_groups_pass(bctx, honest):
+    ok, st, groups, failed = _run(bctx, ED, honest)
+    assert ok and (st == 1).all()
+    assert groups == (1500 + 63) // 64 and failed == 0
+
+
+@pytest.mark.parametrize("m_log2,c", [(5, 4), (6, 5), (7, 6), (8, 7), (9, 8), (10, 9), (6, 9), (10, 4)])
+def test_group_window_sweep(bctx, honest, m_log2, c):
+    ok, st, groups, failed = _run(bctx, ED, honest, group_log2=m_log2, window_bits=c)
+    assert ok and (st == 1).all() and failed == 0
+    assert groups == (1500 + (1 << m_log2) - 1) >> m_log2
+    b = make_c2_batch(2000, seed=5, edge_scale=5.0)
+    ok, st, _, failed = _run(bctx, ED, b, group_log2=m_log2, window_bits=c)
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    assert np.array_equal(st.astype(np.uint8), ref) and not ok
+
+
+def test_zip215_small_order_matrix_passes_equation(bctx, golden):
+    """All 196 small-order (A, R) pairs with S = 0 are valid under the
+    cofactored equation: every group must pass, none may fall back."""
+    g = golden("zip215_small_order.json")
+    msg = bytes.fromhex(g["msg"])
+    ents = [(bytes.fromhex(a), msg, bytes.fromhex(r) + bytes(32)) for a, r in g["pairs_all_valid_with_S0"]]
+    ok, st, groups, failed = _run(bctx, ED, _B(*C.pack(ents)), group_log2=5)
+    assert ok and (st == 1).all() and len(st) == 196
+    assert groups == 7 and failed == 0
+
+
+class _B:
+    def __init__(self, pk, sig, msg, off):
+        self.pk, self.sig, self.msg, self.off = pk, sig, msg, off
+
+
+def test_golden_edge_vectors(bctx, golden):
+    vs = golden("ed25519_vectors.json")["vectors"]
+    b = _B(*C.pack([(bytes.fromhex(v["pk"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])) for v in vs]))
+    ok, st, _, _ = _run(bctx, ED, b, group_log2=5)
+    assert [bool(x) for x in st] == [v["valid"] for v in vs] and not ok
+
+
+@pytest.mark.parametrize("n", [1, 2, 31, 33, 64, 65, 1000])
+def test_ragged_sizes(bctx, honest, n):
+    b = _B(*C.pack([honest.entry(i) for i in range(n)]))
+    ok, st, groups, failed = _run(bctx, ED, b)
+    assert ok and (st == 1).all() and groups == (n + 63) // 64 and failed == 0
+
+
+def test_fresh_randomness(bctx):
+    """Production mode: a new getrandom() key per call; the vector is the same."""
+    b = make_c2_batch(3000, seed=77, edge_scale=3.0)
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    bctx.set_batch_options(seed=None, stats=True)
+    for _ in range(3):
+        ok, st = bctx.verify_batch_ex(ED, BEQ, b.pk, b.sig, b.msg, b.off)
+        assert np.array_equal(st.astype(np.uint8), ref)
+
+
+def test_sr25519_vs_oracle(bctx):
+    b = make_sr25519_batch(2000, bad_frac=0.03)
+    ok, st, groups, failed = _run(bctx, SR, b)
+    ref = C.sr25519_status_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    assert np.array_equal(st, ref) and ok == bool((ref == 1).all())
+    assert failed < groups
+
+
+def test_sr25519_honest_groups_pass(bctx):
+    b = make_sr25519_batch(700, bad_frac=0.0, seed=11)
+    ok, st, groups, failed = _run(bctx, SR, b)
+    assert ok and (st == 1).all() and groups == 11 and failed == 0
+
+
+def test_mixed_vs_per_entry(bctx):
+    kind, b = make_mixed_batch(3000, seed=21)
+    bctx.set_batch_options(seed=SEED, stats=True)
+    s0 = bctx.batch_stats()
+    ok, st = bctx.verify_mixed_batch_ex(BEQ, kind, b.pk, b.sig, b.msg, b.off)
+    s1 = bctx.batch_stats()
+    ok2, ref = bctx.verify_mixed_batch_ex(N.TMV_FLAG_PER_ENTRY, kind, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st, ref) and ok == ok2
+    groups, failed = s1["groups"] - s0["groups"], s1["failed"] - s0["failed"]
+    assert groups == (1500 + 63) // 64 * 2 and failed < groups
+
+
+def test_device_resident_entry_point(bctx):
+    import torch
+    b = make_c2_batch(4096, seed=3)
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(b, k))).to(dev) for k in ("pk", "sig", "msg", "off")}
+    out = torch.zeros(b.n, dtype=torch.int8, device=dev)
+    torch.cuda.synchronize()
+    bctx.verify_batch_device_ex(0, ED, BEQ, 0, t["pk"].data_ptr(), t["sig"].data_ptr(), t["msg"].data_ptr(),
+                                t["off"].data_ptr(), b.n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref)
