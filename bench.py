@@ -5,14 +5,17 @@
 
 A *step* = one pass of the hot path over one synthetic C2 batch
 (BASELINE.json configs[1]: 10,000 ed25519 signatures over commit-vote
-sign-bytes, 1% corrupted / ZIP-215 edge cases) already resident in HBM:
-k_prep + k_verify_quad producing the exact validity vector.  Steps are
-independent batches; `--inflight F`
-keeps F of them in flight on F streams (default 8), each with its own workspace and
-output, as a node verifying a stream of batches does (a single 10k batch
-runs about one wave per SIMD and is latency-bound).
-`--inflight 1` times strictly one batch after another.  With N > 1 (one
-process per GPU, torchrun) every rank verifies its own 10k batches (weak
+sign-bytes, 1% corrupted / ZIP-215 edge cases) already resident in HBM,
+producing that batch's exact validity vector.  Each rank holds K distinct
+C2 batches; one launch (tmv_verify_batches_device) verifies K of them at once
+(`--per-launch K`, default 8): the batches are gathered on the device, run
+through one pipeline and each gets its own vector, as a node draining a
+queue of batches does (a single 10k batch fills about one wave per SIMD and
+is latency-bound).  `--inflight F` keeps F launches in flight
+on F streams.  `--method batch` (default) uses the random-linear-combination
+group check with per-entry fallback (voi's BatchVerifier.Verify, SURVEY rows
+G-I); `--method per-entry` verifies every signature singly.  With N > 1 (one
+process per GPU, torchrun) every rank verifies its own batches (weak
 scaling) and the packed validity bitmaps are all-gathered over RCCL on one
 communication stream, the only cross-GPU exchange the path has.
 
@@ -102,11 +105,18 @@ def cpu_baseline(batch, seconds_target: float = 12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=10_000)
-    ap.add_argument("--inflight", type=int, default=8)
+    ap.add_argument("--per-launch", type=int, default=8,
+                    help="independent batches per pipeline launch (tmv_verify_batches_device)")
+    ap.add_argument("--inflight", type=int, default=2, help="launches in flight (streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--method", choices=["batch", "per-entry"], default="batch",
+                    help="batch: random-linear-combination group check + per-entry fallback "
+                         "(voi's BatchVerifier.Verify); per-entry: every signature verified singly")
+    ap.add_argument("--group-log2", type=int, default=0)
+    ap.add_argument("--window", type=int, default=0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,61 +129,71 @@ def main():
     torch.cuda.set_device(dev)
 
     ctx = N.Context(1 << local_rank)
-    # each rank gets its own shard of signatures (distinct keys/messages)
-    batch = make_c2_batch(args.batch, seed=0xED25519 + rank)
-    n = batch.n
-    d_pk = torch.from_numpy(batch.pk).to(dev)
-    d_sig = torch.from_numpy(batch.sig).to(dev)
-    d_msg = torch.from_numpy(batch.msg).to(dev)
-    d_off = torch.from_numpy(batch.off.view(np.int32)).to(dev)
+    ctx.set_batch_options(group_log2=args.group_log2, window_bits=args.window)
+    flags = N.TMV_FLAG_BATCH_EQUATION if args.method == "batch" else N.TMV_FLAG_PER_ENTRY
+    K = max(1, min(32, args.per_launch))
     F = max(1, args.inflight)
-    d_valid = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(F)]
+    # K distinct C2 batches per rank (own keys / messages), resident in HBM
+    batches = [make_c2_batch(args.batch, seed=0xED25519 + 1000 * rank + j) for j in range(K)]
+    batch = batches[0]
+    n = batch.n
+    d_in = []
+    for b in batches:
+        d_in.append((torch.from_numpy(b.pk).to(dev), torch.from_numpy(b.sig).to(dev), torch.from_numpy(b.msg).to(dev),
+                     torch.from_numpy(b.off.view(np.int32)).to(dev), int(b.off[-1] - b.off[0])))
+    d_valid = [[torch.zeros(n, dtype=torch.int8, device=dev) for _ in range(K)] for _ in range(F)]
+    refs = [[N.BatchRef(pk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(), n, mb,
+                        d_valid[f][j].data_ptr()) for j, (pk, sig, msg, off, mb) in enumerate(d_in)]
+            for f in range(F)]
     counts = [n] * world
     streams = [torch.cuda.Stream(dev) for _ in range(F)]
     comm = torch.cuda.Stream(dev) if world > 1 else None
 
-    def step(i, ev_pair=None):
-        st = streams[i % F]
+    def launch(i, kk=K, ev_pair=None):
+        f = i % F
+        st = streams[f]
         if ev_pair is not None:
             ev_pair[0].record(st)
-        ctx.ed25519_verify_batch_device(local_rank, d_pk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
-                                        d_off.data_ptr(), n, d_valid[i % F].data_ptr(), st.cuda_stream)
+        ctx.verify_batches_device(local_rank, N.TMV_KIND_ED25519, flags, refs[f][:kk], st.cuda_stream)
         if ev_pair is not None:
             ev_pair[1].record(st)
         if world > 1:
-            # collectives in issue order on one stream, after this batch
+            # collectives in issue order on one stream, after this launch
             comm.wait_stream(st)
             with torch.cuda.stream(comm):
-                all_gather_validity(d_valid[i % F], counts)
+                for j in range(kk):
+                    all_gather_validity(d_valid[f][j], counts)
             st.wait_stream(comm)
 
-    # single-batch latency (one stream, one batch at a time), untimed for value
+    # single-batch latency (one batch per launch, one at a time), untimed for value
     lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
     for _ in range(2):
-        step(0)
+        launch(0, 1)
     torch.cuda.synchronize(dev)
     for i in range(10):
-        step(0, lat_ev[i])
+        launch(0, 1, lat_ev[i])
         torch.cuda.synchronize(dev)
     batch_ms = statistics.median(a.elapsed_time(b) for a, b in lat_ev)
 
-    for i in range(args.warmup):
-        step(i)
+    launches = max(1, (args.steps + K - 1) // K)
+    steps = launches * K
+    for i in range(max(1, args.warmup // K)):
+        launch(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, evs[i])
+    for i in range(launches):
+        launch(i, K, evs[i])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
-    valid_count = int(d_valid[0].sum().item())
-    assert all(int(d_valid[i].sum().item()) == valid_count for i in range(min(F, args.steps)))
+    launch_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
+    valid = [int((d_valid[f][j] == 1).sum().item()) for f in range(min(F, launches)) for j in range(K)]
+    assert all(v == 9950 for v in valid), valid  # C2: 100 edge cases, 50 of them valid (factory.py)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -181,17 +201,14 @@ def main():
 
     result = None
     if rank == 0:
-        total = n * world * args.steps
+        total = n * world * steps
         value = total / elapsed
-        # aggregate rate of the launches in flight on this GPU (the timed span
-        # covers args.steps launches; each launch's own duration, kern_ms,
-        # overlaps with up to F-1 others)
-        gpu_rate = n * args.steps / elapsed
-        # end-to-end through the host C-ABI (pinned staging, H2D, kernel, D2H)
+        gpu_rate = n * steps / elapsed
+        # end-to-end through the host C-ABI (pinned staging, H2D, kernels, D2H)
         e2e = []
-        for _ in range(max(3, min(args.steps, 10))):
+        for _ in range(5):
             t1 = time.perf_counter()
-            ctx.ed25519_verify_batch(batch.pk, batch.sig, batch.msg, batch.off)
+            ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, batch.pk, batch.sig, batch.msg, batch.off)
             e2e.append(time.perf_counter() - t1)
         e2e_rate = n / statistics.median(e2e)
         # p50 / p99 of types.VerifyCommit on a 150-validator commit (C1): the
@@ -208,25 +225,27 @@ def main():
             assert err is None
         lat.sort()
         peak = _load_peak()
-        achieved = gpu_rate * MULS_PER_SIG
+        # canonical work per launch of K batches / its average
+        # duration (HIP events on the launch stream)
+        achieved = n * K * MULS_PER_SIG / (launch_ms * 1e-3)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "verifies/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (deterministic C2 generator, OpenSSL-signed commit-vote sign-bytes)",
             "config": {"workload": "C2: 10k ed25519 ZIP-215 batch, 1% corrupted/edge-case sigs (BASELINE configs[1])",
-                       "batch_per_gpu": n, "msg_bytes_avg": round(float(batch.msg.size) / n, 1),
+                       "batch_per_step": n, "batches_per_launch": K, "launches_in_flight": F,
+                       "method": args.method, "msg_bytes_avg": round(float(batch.msg.size) / n, 1),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
-            "valid_count": valid_count,
-            "inflight": F,
+            "valid_per_batch": valid[0],
             "batch_latency_ms": round(batch_ms, 4),
             "serial_verifies_per_s": round(n / (batch_ms * 1e-3), 1),
             "end_to_end_verifies_per_s": round(e2e_rate, 1),
@@ -236,11 +255,12 @@ def main():
             "roofline": {"bound": "valu-int-mul", "achieved": round(achieved / 1e12, 4),
                          "peak": round(peak / 1e12, 4), "unit": "Tmul/s", "frac": round(achieved / peak, 4),
                          "traffic": _load_traffic(),
-                         "kernel": ("k_prep + k_verify_quad" if n <= 49152 else "k_ed25519_verify"),
-                         "kernel_avg_ms": round(kern_ms, 4),
-                         "launches_in_flight": F,
-                         "achieved_from": "launches x 10k sigs x 2.7e5 products / timed span (launches overlap)",
-                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d))"},
+                         "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if args.method == "batch"
+                                    else "k_prep + k_verify_quad"),
+                         "launch_avg_ms": round(launch_ms, 4),
+                         "achieved_from": f"{K} x {n} sigs x 2.7e5 canonical products / average launch "
+                                          "duration (HIP events on the launch stream)",
+                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d), single-verify equivalent)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(batch)

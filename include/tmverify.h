@@ -153,6 +153,27 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
                                const uint8_t *d_pk, const uint8_t *d_sig, const uint8_t *d_msg,
                                const uint32_t *d_msg_off, uint32_t n, int8_t *d_status, void *stream);
 
+/* Several independent device-resident batches in one pipeline: the batches
+ * are gathered into one contiguous batch on the device, verified together
+ * (per-entry or batch equation, per flags) and each batch's statuses are
+ * written to its own d_status (as tmv_verify_batch_device_ex).  Verdicts are
+ * per entry, so this equals n_batches separate calls; it only widens the
+ * launches (a node draining a queue of batches, blocksync look-ahead).
+ * msg_bytes = msg_off[n] - msg_off[0].  Up to 32 batches; key_kind
+ * TMV_KIND_ED25519 or TMV_KIND_SR25519.  Asynchronous like the other
+ * device-resident entry points. */
+typedef struct tmv_batch_ref {
+  const uint8_t *pk;
+  const uint8_t *sig;
+  const uint8_t *msg;
+  const uint32_t *msg_off;
+  uint32_t n;
+  uint32_t msg_bytes;
+  int8_t *status;
+} tmv_batch_ref;
+int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32_t flags,
+                              const tmv_batch_ref *batches, uint32_t n_batches, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,11 +39,18 @@ EXPORTS = [
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
     "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
-    "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex",
+    "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_verify_commit", "tmv_verify_commits",
 ]
+
+
+class BatchRef(ctypes.Structure):
+    """tmv_batch_ref (include/tmverify.h): one device-resident batch."""
+    _fields_ = [("pk", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("msg", ctypes.c_void_p),
+                ("msg_off", ctypes.c_void_p), ("n", ctypes.c_uint32), ("msg_bytes", ctypes.c_uint32),
+                ("status", ctypes.c_void_p)]
 
 
 class NativeError(RuntimeError):
@@ -93,6 +100,8 @@ def lib() -> ctypes.CDLL:
         L.tmv_verify_mixed_batch_ex.argtypes = [vp, ctypes.c_uint32, u8p, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
         L.tmv_verify_batch_device_ex.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32, vp, vp, vp, vp,
                                                  vp, ctypes.c_uint32, vp, vp]
+        L.tmv_verify_batches_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32,
+                                                ctypes.POINTER(BatchRef), ctypes.c_uint32, vp]
         L.tmv_ed25519_verify_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         L.tmv_verify_mixed_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         _lib = L
@@ -231,6 +240,12 @@ class Context:
         self._check(self._lib.tmv_verify_batch_device_ex(self._h, device, key_kind, flags, d_kind or None, d_pk,
                                                          d_sig, d_msg, d_off, n, d_status, stream or None),
                     "tmv_verify_batch_device_ex")
+
+    def verify_batches_device(self, device: int, key_kind: int, flags: int, refs, stream: int = 0) -> None:
+        """refs: sequence of BatchRef (device pointers)."""
+        arr = (BatchRef * len(refs))(*refs)
+        self._check(self._lib.tmv_verify_batches_device(self._h, device, key_kind, flags, arr, len(refs),
+                                                        stream or None), "tmv_verify_batches_device")
 
     def key_cache_stats(self):
         h, m = ctypes.c_uint64(), ctypes.c_uint64()

@@ -1,0 +1,71 @@
+// Multi-batch launches (tmv_verify_batches_device): K independent device
+// batches are gathered into one contiguous batch, verified by one pipeline,
+// and each batch's statuses are scattered back to its own output.  Entries
+// never mix verdicts across batches (the per-entry vector is exact); batching
+// only widens the launches, the way a node draining a queue of commits or
+// blocks would.  Pure data movement (HBM-bound).
+#include <hip/hip_runtime.h>
+#include "verify_kernels.h"
+
+namespace tmv {
+
+__device__ __forceinline__ uint32_t batch_of(const BatchRefs &r, uint32_t e) {
+  uint32_t b = 0;
+  for (uint32_t k = 1; k < r.nb; k++) b = (e >= r.start[k]) ? k : b;
+  return b;
+}
+
+// One lane per entry: key and signature (16-byte vector copies when the
+// source is aligned), rebased message offset, message bytes.
+__global__ void __launch_bounds__(256)
+k_gather(BatchRefs r, uint8_t *__restrict__ pk, uint8_t *__restrict__ sig, uint32_t *__restrict__ off,
+         uint8_t *__restrict__ msg) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t N = r.start[r.nb];
+  if (e >= N) return;
+  const uint32_t b = batch_of(r, e), i = e - r.start[b];
+  const uint8_t *spk = r.pk[b] + 32ull * i, *ssig = r.sig[b] + 64ull * i;
+  if (((((uintptr_t)spk) | ((uintptr_t)ssig)) & 15) == 0) {
+    const uint4 *a = reinterpret_cast<const uint4 *>(spk);
+    const uint4 *s = reinterpret_cast<const uint4 *>(ssig);
+    uint4 *da = reinterpret_cast<uint4 *>(pk + 32ull * e);
+    uint4 *ds = reinterpret_cast<uint4 *>(sig + 64ull * e);
+    da[0] = a[0]; da[1] = a[1];
+    ds[0] = s[0]; ds[1] = s[1]; ds[2] = s[2]; ds[3] = s[3];
+  } else {
+    for (int t = 0; t < 32; t++) pk[32ull * e + t] = spk[t];
+    for (int t = 0; t < 64; t++) sig[64ull * e + t] = ssig[t];
+  }
+  const uint32_t *so = r.off[b];
+  const uint32_t o0 = so[i], o1 = so[i + 1];
+  const uint32_t dst = r.msg_base[b] + (o0 - so[0]);
+  off[e] = dst;
+  if (e + 1 == N) off[N] = r.msg_base[b] + (o1 - so[0]);
+  const uint8_t *sm = r.msg[b];
+  for (uint32_t t = o0; t < o1; t++) msg[dst + (t - o0)] = sm[t];
+}
+
+__global__ void __launch_bounds__(256)
+k_scatter(BatchRefs r, const int8_t *__restrict__ status) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= r.start[r.nb]) return;
+  const uint32_t b = batch_of(r, e);
+  r.out[b][e - r.start[b]] = status[e];
+}
+
+hipError_t launch_gather(const BatchRefs &r, uint8_t *pk, uint8_t *sig, uint32_t *off, uint8_t *msg,
+                         hipStream_t stream) {
+  const uint32_t N = r.start[r.nb];
+  if (N == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather, dim3((N + 255) / 256), dim3(256), 0, stream, r, pk, sig, off, msg);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const BatchRefs &r, const int8_t *status, hipStream_t stream) {
+  const uint32_t N = r.start[r.nb];
+  if (N == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter, dim3((N + 255) / 256), dim3(256), 0, stream, r, status);
+  return hipGetLastError();
+}
+
+}  // namespace tmv

@@ -19,10 +19,12 @@
 //   k_msm_accum  one lane per kChunk consecutive sorted entries: runs of one
 //                bucket are summed (mixed additions, Niels points); runs that
 //                cross a chunk edge leave partial sums
-//   k_msm_group  one workgroup per group: bucket values (merging partials),
-//                per-window running sums split over lanes, then the Horner
-//                combination over windows in quad-lane arithmetic and the
-//                group verdict
+//   k_msm_wpart  one lane per (group, window, part): running sums over the
+//                part's H/P buckets (bucket values merge chunk partials)
+//   k_msm_wsum   one lane per (group, window): joins the P parts into the
+//                window sum S_w = sum_j (j+1) bucket_j
+//   k_msm_horner one quad per group: T_g = sum_w 2^(c w) S_w (Horner, quad-lane
+//                arithmetic) and the group verdict
 #pragma once
 #include <stdint.h>
 #include "curve25519.h"
@@ -32,7 +34,6 @@ namespace tmv {
 constexpr int kMsmChunk = 8;                 // sorted entries per accumulation lane
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
-constexpr int kMsmGroupBlock = 256;
 
 // Affine Niels point padded to one 128-byte line.
 struct alignas(16) niels_pt {
@@ -48,7 +49,7 @@ struct MsmParams {
   uint32_t H;        // buckets per window = 2^(c-1)
   uint32_t cap;      // sorted-entry slots per group (multiple of kMsmChunk)
   uint32_t groups;   // groups allocated = ceil(n / m)
-  uint32_t P;        // lanes per window in k_msm_group (power of two <= H)
+  uint32_t P;        // lanes per window in k_msm_wpart (power of two <= H)
 
   TMV_HD uint32_t m() const { return 1u << m_log2; }
   TMV_HD uint32_t buckets_per_group() const { return W * H; }
@@ -65,9 +66,15 @@ struct MsmParams {
     const uint32_t slots = (2 * m + 1) * p.W;
     p.cap = (slots + kMsmChunk - 1) / kMsmChunk * kMsmChunk;
     p.groups = (n + m - 1) >> m_log2;
-    uint32_t P = 1;
-    while (2 * P <= p.H && 2 * P * p.W <= (uint32_t)kMsmGroupBlock) P *= 2;
-    p.P = P;
+    // P minimises the latency chain: 2 H/P running-sum additions per part,
+    // then 3 P additions + log2(H/P) doublings to join the parts
+    uint32_t best = ~0u;
+    for (uint32_t P = 1; P <= p.H; P *= 2) {
+      uint32_t lg = 0;
+      while ((p.H / P) >> (lg + 1)) lg++;
+      const uint32_t chain = 2 * (p.H / P) + 3 * P + lg;
+      if (chain < best) { best = chain; p.P = P; }
+    }
     return p;
   }
 };
@@ -82,6 +89,8 @@ struct MsmWork {
   ge_p3 *bk_sum;       // groups x W x H: sums of buckets that fit in one chunk
   ge_p3 *part_first;   // chunks: run that began in an earlier chunk and ends here
   ge_p3 *part_last;    // chunks: run that continues into the next chunk
+  ge_p3 *wpart;        // groups x W x P x 2: (T, U) of each window part
+  ge_p3 *wsum;         // groups x W: window sums
   uint8_t *group_ok;   // groups
   uint32_t n_pts;      // index of B (= 2n)
 
@@ -89,7 +98,7 @@ struct MsmWork {
     const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
     const size_t chunks = ent / kMsmChunk;
     return (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
-           2 * chunks * sizeof(ge_p3) + G + 16 * 10;
+           2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 16 * 12;
   }
   static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
     auto up = [](size_t x) { return (x + 15) & ~size_t(15); };
@@ -106,6 +115,8 @@ struct MsmWork {
     w.bk_sum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + bk * sizeof(ge_p3));
     w.part_first = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.part_last = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
+    w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.P * sizeof(ge_p3));
+    w.wsum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * sizeof(ge_p3));
     w.group_ok = b + o;
     w.n_pts = 2 * n;
     return w;

@@ -262,10 +262,14 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 // One lane per chunk of kMsmChunk sorted entries: sums each run of equal
 // bucket ids with mixed additions.  A run that is the whole bucket goes to
 // bk_sum; a run cut by the chunk's end goes to part_last, one cut by its
-// start to part_first (k_msm_group joins them).
+// start to part_first (k_msm_wpart joins them).
 __global__ void __launch_bounds__(256)
-k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, uint32_t per_xcd) {
+  // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD a
+  // contiguous range of chunks so a group's points stay in one L2
+  if ((blockIdx.x >> 3) >= per_xcd) return;
+  const uint32_t lb = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const uint32_t t = lb * blockDim.x + threadIdx.x;
   const uint32_t cpg = p.chunks_per_group();
   const uint32_t g = t / cpg;
   if (g >= p.groups) return;
@@ -319,79 +323,92 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   flush(cur, rs, base + j, acc);
 }
 
-// One workgroup per group: window sums S_w = sum_j (j+1) bucket_j, split
-// over P lanes per window (lane part q sums buckets [q s, (q+1) s) with the
-// running-sum trick; S_w = sum_q T_q + s * sum_q q U_q), then
-// T_g = sum_w 2^(c w) S_w by Horner on one quad, and the group verdict.
+// Window parts: lane (g, w, q) sums buckets [q s, (q+1) s) of window w with
+// the running-sum trick: T = sum_i (i+1) B_{qs+i}, U = sum_i B_{qs+i}.
+__global__ void __launch_bounds__(256)
+k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t per_group = p.W * p.P;
+  const uint32_t g = t / per_group;
+  if (g >= p.groups || (g << p.m_log2) >= entry_count(count_ptr, n)) return;
+  const uint32_t r = t - g * per_group, wdx = r / p.P, part = r % p.P;
+  const uint32_t s = p.H / p.P;
+  ge_p3 U, T;
+  bool u_set = false, t_set = false;
+  for (int i = (int)s - 1; i >= 0; i--) {
+    ge_p3 B;
+    if (bucket_value(mw, g * p.W * p.H + wdx * p.H + part * s + (uint32_t)i, B)) {
+      if (u_set) p3_add(U, B);
+      else { U = B; u_set = true; }
+    }
+    if (u_set) {
+      if (t_set) p3_add(T, U);
+      else { T = U; t_set = true; }
+    }
+  }
+  if (!u_set) ge_p3_identity(U);
+  if (!t_set) ge_p3_identity(T);
+  mw.wpart[2ull * t] = T;
+  mw.wpart[2ull * t + 1] = U;
+}
+
+// Window sums: S_w = sum_q T_q + s * sum_q q U_q (s = H / P).
+__global__ void __launch_bounds__(256)
+k_msm_wsum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = t / p.W;
+  if (g >= p.groups || (g << p.m_log2) >= entry_count(count_ptr, n)) return;
+  const ge_p3 *wp = mw.wpart + 2ull * t * p.P;
+  ge_p3 acc;
+  if (p.P > 1) {
+    ge_p3 r = wp[2 * (p.P - 1) + 1];
+    acc = r;
+    for (uint32_t q = p.P - 2; q >= 1; q--) {
+      p3_add(r, wp[2 * q + 1]);
+      p3_add(acc, r);
+    }
+    for (uint32_t d = p.H / p.P; d > 1; d >>= 1) p3_dbl(acc);
+    for (uint32_t q = 0; q < p.P; q++) p3_add(acc, wp[2 * q]);
+  } else {
+    acc = wp[0];
+  }
+  mw.wsum[t] = acc;
+}
+
+// Group verdicts: one quad per group (lane c holds coordinate c), 16 groups
+// per wave; T_g = sum_w 2^(c w) S_w by Horner, then
+//   ed25519: [8] T_g == O;  sr25519: T_g is the Ristretto identity.
 template <bool SR>
-__global__ void __launch_bounds__(kMsmGroupBlock)
-k_msm_group(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
-  __shared__ ge_p3 Ts[kMsmGroupBlock];
-  __shared__ ge_p3 Us[kMsmGroupBlock];
-  __shared__ ge_p3 Ss[64];
-  const uint32_t g = blockIdx.x;
-  if ((g << p.m_log2) >= entry_count(count_ptr, n)) return;  // block-uniform
-  const uint32_t tid = threadIdx.x;
-  const uint32_t P = p.P, s = p.H / P;
-  const uint32_t wdx = tid / P, part = tid % P;
-  const uint32_t WH = p.W * p.H;
-  if (wdx < p.W) {
-    ge_p3 U, T;
-    bool u_set = false, t_set = false;
-    for (int i = (int)s - 1; i >= 0; i--) {
-      ge_p3 B;
-      if (bucket_value(mw, g * WH + wdx * p.H + part * s + (uint32_t)i, B)) {
-        if (u_set) p3_add(U, B);
-        else { U = B; u_set = true; }
-      }
-      if (u_set) {
-        if (t_set) p3_add(T, U);
-        else { T = U; t_set = true; }
-      }
-    }
-    if (!u_set) ge_p3_identity(U);
-    if (!t_set) ge_p3_identity(T);
-    Ts[tid] = T;
-    Us[tid] = U;
-  }
-  __syncthreads();
-  if (wdx < p.W && part == 0) {
-    ge_p3 r, t;
-    ge_p3_identity(r);
-    ge_p3_identity(t);
-    for (uint32_t q = P - 1; q >= 1; q--) {
-      p3_add(r, Us[tid + q]);
-      p3_add(t, r);
-    }
-    for (uint32_t d = s; d > 1; d >>= 1) p3_dbl(t);
-    for (uint32_t q = 0; q < P; q++) p3_add(t, Ts[tid + q]);
-    Ss[wdx] = t;
-  }
-  __syncthreads();
-  if (tid < 4) {
-    const int c = (int)tid;
-    fe acc = reinterpret_cast<const fe *>(&Ss[p.W - 1])[c];
-    fe r, q, qc;
-    for (int wI = (int)p.W - 2; wI >= 0; wI--) {
-      for (uint32_t d = 0; d < p.c; d++) {
-        quad::dbl(r, acc);
-        quad::p1p1_to_p3(acc, r);
-      }
-      q = reinterpret_cast<const fe *>(&Ss[wI])[c];
-      quad::to_cached(qc, q);
-      quad::add(r, acc, qc);
+__global__ void __launch_bounds__(64)
+k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
+  if (blockIdx.x * 16 >= live_groups) return;  // block-uniform
+  const uint32_t raw = blockIdx.x * 16 + (threadIdx.x >> 2);
+  const bool live = raw < live_groups;
+  const uint32_t g = live ? raw : live_groups - 1;  // whole quads stay active for DPP
+  const int c = (int)(threadIdx.x & 3);
+  const ge_p3 *S = mw.wsum + (size_t)g * p.W;
+  fe acc = reinterpret_cast<const fe *>(&S[p.W - 1])[c];
+  fe r, q, qc;
+  for (int wI = (int)p.W - 2; wI >= 0; wI--) {
+    for (uint32_t d = 0; d < p.c; d++) {
+      quad::dbl(r, acc);
       quad::p1p1_to_p3(acc, r);
     }
-    bool ok;
-    if (SR) {
-      fe id;
-      quad::p3_identity(id);
-      ok = quad::ristretto_equal(acc, id);
-    } else {
-      ok = quad::is_identity_times8(acc);
-    }
-    if (c == 0) mw.group_ok[g] = ok ? 1 : 0;
+    q = reinterpret_cast<const fe *>(&S[wI])[c];
+    quad::to_cached(qc, q);
+    quad::add(r, acc, qc);
+    quad::p1p1_to_p3(acc, r);
   }
+  bool ok;
+  if (SR) {
+    fe id;
+    quad::p3_identity(id);
+    ok = quad::ristretto_equal(acc, id);
+  } else {
+    ok = quad::is_identity_times8(acc);
+  }
+  if (live && c == 0) mw.group_ok[g] = ok ? 1 : 0;
 }
 
 template <bool SR>
@@ -409,9 +426,16 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
                      mw, p, seed, btab_q, aligned);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
-  hipLaunchKernelGGL(k_msm_accum, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
+  hipLaunchKernelGGL(k_msm_accum, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_group<SR>, dim3(p.groups), dim3(kMsmGroupBlock), 0, stream, count_ptr, n, mw, p);
+  const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
+  hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint64_t rows = (uint64_t)p.groups * p.W;
+  hipLaunchKernelGGL(k_msm_wsum, dim3((uint32_t)((rows + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_msm_horner<SR>, dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream);
 }

@@ -138,7 +138,7 @@ struct KeyIndex {
 // Scratch of one launch stream: prep outputs (Ed25519Work), mixed-batch
 // partition, and the event that orders reuse of these buffers.
 struct Workspace {
-  DeviceBuf work, work2, idx, msm, msm2;
+  DeviceBuf work, work2, idx, msm, msm2, gather;
   hipEvent_t done = nullptr;
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
@@ -656,6 +656,7 @@ void tmv_close(tmv_ctx *ctx) {
       kv.second->idx.release();
       kv.second->msm.release();
       kv.second->msm2.release();
+      kv.second->gather.release();
       if (kv.second->done) (void)hipEventDestroy(kv.second->done);
     }
     d->ws.clear();
@@ -895,6 +896,69 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
   else if (key_kind == TMV_KIND_SR25519) rc = launch_sr25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
   else rc = launch_mixed(*dev, o, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
   return rc != 0 ? rc : TMV_NOT_ALL;
+}
+
+int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32_t flags,
+                              const tmv_batch_ref *batches, uint32_t n_batches, void *stream) {
+  Device *dev = find_device(ctx, device);
+  if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (key_kind != TMV_KIND_ED25519 && key_kind != TMV_KIND_SR25519) {
+    set_error("tmv_verify_batches_device: key_kind must be ed25519 or sr25519");
+    return TMV_ERR_ARG;
+  }
+  if (n_batches == 0 || n_batches > tmv::kMaxBatches || !batches) {
+    set_error("tmv_verify_batches_device: 1..32 batches");
+    return TMV_ERR_ARG;
+  }
+  tmv::BatchRefs r{};
+  r.nb = n_batches;
+  uint64_t N = 0, M = 0;
+  for (uint32_t b = 0; b < n_batches; b++) {
+    const tmv_batch_ref &x = batches[b];
+    if (x.n && (!x.pk || !x.sig || !x.msg_off || !x.status || (!x.msg && x.msg_bytes))) {
+      set_error("tmv_verify_batches_device: null pointer in a non-empty batch");
+      return TMV_ERR_ARG;
+    }
+    r.pk[b] = x.pk; r.sig[b] = x.sig; r.msg[b] = x.msg; r.off[b] = x.msg_off; r.out[b] = x.status;
+    r.start[b] = (uint32_t)N;
+    r.msg_base[b] = (uint32_t)M;
+    N += x.n;
+    M += x.msg_bytes;
+  }
+  if (N > 0xffffffffull / 64 || M > 0xffffffffull) { set_error("tmv_verify_batches_device: too large"); return TMV_ERR_ARG; }
+  r.start[n_batches] = (uint32_t)N;
+  r.msg_base[n_batches] = (uint32_t)M;
+  if (N == 0) return TMV_NOT_ALL;
+  hipError_t e = hipSetDevice(dev->id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  const uint32_t n = (uint32_t)N;
+  const LaunchOpts o = make_opts(ctx, flags, n);
+  std::lock_guard<std::mutex> lk(dev->mu);
+  int rc;
+  Workspace *ws = reserve_work(*dev, n, false, s, &rc, o.batch_eq ? &o.p : nullptr);
+  if (!ws) return rc;
+  Layout L(n, (size_t)M);
+  const size_t need = L.total + align16(n);
+  if (need > ws->gather.cap) {
+    (void)hipEventSynchronize(ws->done);
+    if ((e = ws->gather.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(gather)", e); return TMV_ERR_NOMEM; }
+  }
+  uint8_t *g = static_cast<uint8_t *>(ws->gather.ptr);
+  uint32_t *goff = reinterpret_cast<uint32_t *>(g + L.off);
+  int8_t *gst = reinterpret_cast<int8_t *>(g + L.total);
+  if ((e = tmv::launch_gather(r, g + L.pk, g + L.sig, goff, g + L.msg, s)) != hipSuccess) {
+    set_error("gather launch", e);
+    return TMV_ERR_LAUNCH;
+  }
+  if (key_kind == TMV_KIND_ED25519)
+    rc = launch_ed25519(*dev, o, g + L.pk, g + L.sig, g + L.msg, goff, n, reinterpret_cast<uint8_t *>(gst), s);
+  else
+    rc = launch_sr25519(*dev, o, g + L.pk, g + L.sig, g + L.msg, goff, n, gst, s);
+  if (rc != 0) return rc;
+  if ((e = tmv::launch_scatter(r, gst, s)) != hipSuccess) { set_error("scatter launch", e); return TMV_ERR_LAUNCH; }
+  (void)hipEventRecord(ws->done, s);
+  return TMV_NOT_ALL;
 }
 
 }  // extern "C"

@@ -87,6 +87,23 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
 hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
                             uint8_t *out, hipStream_t stream);
 
+// Multi-batch launches (gather_kernels.hip): up to kMaxBatches device
+// batches, passed by value as kernel arguments.
+constexpr uint32_t kMaxBatches = 32;
+struct BatchRefs {
+  const uint8_t *pk[kMaxBatches];
+  const uint8_t *sig[kMaxBatches];
+  const uint8_t *msg[kMaxBatches];
+  const uint32_t *off[kMaxBatches];
+  int8_t *out[kMaxBatches];
+  uint32_t start[kMaxBatches + 1];     // first gathered entry of each batch
+  uint32_t msg_base[kMaxBatches + 1];  // first gathered message byte of each batch
+  uint32_t nb;
+};
+hipError_t launch_gather(const BatchRefs &r, uint8_t *pk, uint8_t *sig, uint32_t *off, uint8_t *msg,
+                         hipStream_t stream);
+hipError_t launch_scatter(const BatchRefs &r, const int8_t *status, hipStream_t stream);
+
 hipError_t launch_ed25519_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                  const uint32_t *msg_off, uint32_t n, const ge_precomp *btable,
                                  uint8_t *valid, hipStream_t stream);

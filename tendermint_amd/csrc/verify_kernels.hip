@@ -164,7 +164,6 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
               const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
   __shared__ fe tabA[kQuadSigs * 8 * 4];
-  __shared__ fe tabB[kBaseQuadEntries * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
   const uint32_t m = entry_count(count_ptr, n);
   if (blockIdx.x * kQuadSigs >= m) return;  // block-uniform
@@ -194,7 +193,6 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
     out[i] = (uint8_t)(int8_t)status;
     return;
   }
-  for (int t = threadIdx.x; t < kBaseQuadEntries * 4; t += kQuadBlock) tabB[t] = btab_q[t];
 
   uint32_t s_raw[8], s_w[8];
   if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
@@ -241,7 +239,14 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
 
   fe acc;
   quad::p3_identity(acc);
+  // The 20 KB table of B multiples is read through L1 (not staged in LDS,
+  // which would cap the kernel near one wave per SIMD); each even window's
+  // entry is loaded before its four doublings so the latency is hidden.
   for (int wdx = 63; wdx >= 0; wdx--) {
+    const int db = dig[q][1][wdx >> 1];
+    const int ab = db < 0 ? -db : db;
+    fe bent;
+    if ((wdx & 1) == 0) bent = btab_q[(ab ? ab - 1 : 0) * 4 + c];
     if (wdx != 63) {
 #pragma unroll
       for (int d = 0; d < 4; d++) {
@@ -259,9 +264,7 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
     quad::add(r, acc, ent);
     quad::p1p1_to_p3(acc, r);
     if ((wdx & 1) == 0) {  // B digit d_j weighs 256^j = 16^(2j)
-      const int db = dig[q][1][wdx >> 1];
-      const int ab = db < 0 ? -db : db;
-      ent = tabB[(ab ? ab - 1 : 0) * 4 + c];
+      ent = bent;
       fe_cmov(ent, idq, ab == 0);
       quad::cached_cneg(ent, db < 0);
       quad::add(r, acc, ent);

@@ -149,3 +149,39 @@ def test_device_resident_entry_point(bctx):
                                 t["off"].data_ptr(), b.n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref)
+
+
+@pytest.mark.parametrize("flags", [BEQ, N.TMV_FLAG_PER_ENTRY])
+def test_multi_batch_launch(bctx, flags):
+    """tmv_verify_batches_device: several independent batches (different
+    sizes, one empty, one unaligned) in one launch equal separate checks."""
+    import torch
+    dev = torch.device("cuda:0")
+    specs = [(make_c2_batch(700, seed=41, edge_scale=8.0), 0), (make_c2_batch(0, seed=42), 0),
+             (make_c2_batch(1300, seed=43, edge_scale=4.0), 3), (make_sr25519_batch(0), 0),
+             (make_c2_batch(65, seed=44, edge_scale=20.0), 1)]
+    keep, refs, want = [], [], []
+    for b, shift in specs:
+        if b.n == 0:
+            refs.append(N.BatchRef(0, 0, 0, 0, 0, 0, 0))
+            continue
+        raw = {}
+        for k in ("pk", "sig", "msg"):
+            a = getattr(b, k)
+            buf = torch.zeros(len(a) + 16, dtype=torch.uint8, device=dev)
+            buf[shift:shift + len(a)] = torch.from_numpy(a).to(dev)
+            raw[k] = buf
+        off = torch.from_numpy(b.off.view(np.int32)).to(dev)
+        out = torch.full((b.n,), -7, dtype=torch.int8, device=dev)
+        keep += [raw, off, out]
+        refs.append(N.BatchRef(raw["pk"].data_ptr() + shift, raw["sig"].data_ptr() + shift,
+                               raw["msg"].data_ptr() + shift, off.data_ptr(), b.n, int(b.off[-1] - b.off[0]),
+                               out.data_ptr()))
+        _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+        want.append((out, ref))
+    bctx.set_batch_options(seed=SEED, stats=True)
+    torch.cuda.synchronize()
+    bctx.verify_batches_device(0, ED, flags, refs, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for out, ref in want:
+        assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref)
