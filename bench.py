@@ -8,11 +8,11 @@ A *step* = one pass of the hot path over one synthetic C2 batch
 sign-bytes, 1% corrupted / ZIP-215 edge cases) already resident in HBM,
 producing that batch's exact validity vector.  Each rank holds K distinct
 C2 batches; one launch (tmv_verify_batches_device) verifies K of them at once
-(`--per-launch K`, default 8): the batches are gathered on the device, run
+(`--per-launch K`, default 16): the batches are gathered on the device, run
 through one pipeline and each gets its own vector, as a node draining a
 queue of batches does (a single 10k batch fills about one wave per SIMD and
 is latency-bound).  `--inflight F` keeps F launches in flight
-on F streams.  `--method batch` (default) uses the random-linear-combination
+on F streams (default 4, the HIP hardware queues per process).  `--method batch` (default) uses the random-linear-combination
 group check with per-entry fallback (voi's BatchVerifier.Verify, SURVEY rows
 G-I); `--method per-entry` verifies every signature singly.  With N > 1 (one
 process per GPU, torchrun) every rank verifies its own batches (weak
@@ -33,6 +33,7 @@ import os
 import statistics
 import sys
 import time
+from concurrent.futures import ProcessPoolExecutor
 
 import numpy as np
 import torch
@@ -102,15 +103,19 @@ def cpu_baseline(batch, seconds_target: float = 12.0):
                       f"{threads} pthreads; Go/curve25519-voi not buildable here (no toolchain)"}
 
 
+def _c2(a):
+    return make_c2_batch(a[0], seed=a[1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=96)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=192)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--batch", type=int, default=10_000)
-    ap.add_argument("--per-launch", type=int, default=8,
+    ap.add_argument("--per-launch", type=int, default=16,
                     help="independent batches per pipeline launch (tmv_verify_batches_device)")
-    ap.add_argument("--inflight", type=int, default=2, help="launches in flight (streams)")
+    ap.add_argument("--inflight", type=int, default=4, help="launches in flight (streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--method", choices=["batch", "per-entry"], default="batch",
                     help="batch: random-linear-combination group check + per-entry fallback "
@@ -122,6 +127,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    K = max(1, min(32, args.per_launch))
+    F = max(1, args.inflight)
+    # K distinct C2 batches per rank (own keys / messages), generated on the
+    # host before this process touches the GPU (worker processes are forked)
+    with ProcessPoolExecutor(min(8, K)) as ex:
+        batches = list(ex.map(_c2, [(args.batch, 0xED25519 + 1000 * rank + j) for j in range(K)]))
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -131,10 +142,6 @@ def main():
     ctx = N.Context(1 << local_rank)
     ctx.set_batch_options(group_log2=args.group_log2, window_bits=args.window)
     flags = N.TMV_FLAG_BATCH_EQUATION if args.method == "batch" else N.TMV_FLAG_PER_ENTRY
-    K = max(1, min(32, args.per_launch))
-    F = max(1, args.inflight)
-    # K distinct C2 batches per rank (own keys / messages), resident in HBM
-    batches = [make_c2_batch(args.batch, seed=0xED25519 + 1000 * rank + j) for j in range(K)]
     batch = batches[0]
     n = batch.n
     d_in = []
@@ -177,7 +184,8 @@ def main():
 
     launches = max(1, (args.steps + K - 1) // K)
     steps = launches * K
-    for i in range(max(1, args.warmup // K)):
+    # every stream's workspace is allocated by its first launch: warm all of them
+    for i in range(max(2 * F, args.warmup // K)):
         launch(i)
     torch.cuda.synchronize(dev)
     if world > 1:

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Profiles the bench workload on the GPU box (run under gpurun).
-#   kernel trace + stats, then PMC passes (one counter group per pass, no
-#   tracing domains mixed with --pmc).  Outputs under gpurun_out/prof_rNN/.
-# Stops at the first timeout / crash (exit 124, 137, 134, 139).
+#   kernel trace + stats of the default bench, then PMC passes (one counter
+#   group per pass, no tracing domains mixed with --pmc).  Outputs under
+#   gpurun_out/prof_<tag>/.  Stops at the first timeout / crash.
 R=${1:-r01}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
@@ -15,10 +15,10 @@ run() {
   case $rc in 124|137|134|139) echo "stopping after $name"; exit $rc;; esac
   return 0
 }
-run list rocprofv3 -L
+B="python3 bench.py --no-cpu-baseline --steps 64 --warmup 16"
 run trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py
-run fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
-run write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
-run valu rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES --output-format csv -d $OUT/valu -o valu -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
-run busy rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VALU_MUL_I32 --output-format csv -d $OUT/busy -o busy -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1
+run fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- $B
+run write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- $B
+run valu rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES --output-format csv -d $OUT/valu -o valu -- $B
+run busy rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VALU_MUL_I32 --output-format csv -d $OUT/busy -o busy -- $B
 echo done
