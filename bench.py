@@ -8,7 +8,7 @@ A *step* = one pass of the hot path over one synthetic C2 batch
 sign-bytes, 1% corrupted / ZIP-215 edge cases) already resident in HBM,
 producing that batch's exact validity vector.  Each rank holds K distinct
 C2 batches; one launch (tmv_verify_batches_device) verifies K of them at once
-(`--per-launch K`, default 16): the batches are gathered on the device, run
+(`--per-launch K`, default 32): the batches are gathered on the device, run
 through one pipeline and each gets its own vector, as a node draining a
 queue of batches does (a single 10k batch fills about one wave per SIMD and
 is latency-bound).  `--inflight F` keeps F launches in flight
@@ -45,7 +45,7 @@ sys.path.insert(0, REPO)
 from tendermint_amd import _native as N  # noqa: E402
 from tendermint_amd.shard import all_gather_validity  # noqa: E402
 from tendermint_amd import host as H  # noqa: E402
-from tendermint_amd.testing.factory import make_c1_commit, make_c2_batch  # noqa: E402
+from tendermint_amd.testing.factory import Batch, make_c1_commit, make_c2_batch  # noqa: E402
 
 METRIC = "ed25519 verifies/sec at 1/2/4/8 GPUs + p50 VerifyCommit latency, 150 vals"
 # Canonical algorithmic work per verified signature:
@@ -110,10 +110,10 @@ def _c2(a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=192)
+    ap.add_argument("--steps", type=int, default=384)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--batch", type=int, default=10_000)
-    ap.add_argument("--per-launch", type=int, default=16,
+    ap.add_argument("--per-launch", type=int, default=32,
                     help="independent batches per pipeline launch (tmv_verify_batches_device)")
     ap.add_argument("--inflight", type=int, default=4, help="launches in flight (streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -212,13 +212,15 @@ def main():
         total = n * world * steps
         value = total / elapsed
         gpu_rate = n * steps / elapsed
-        # end-to-end through the host C-ABI (pinned staging, H2D, kernels, D2H)
+        # end-to-end through the host C-ABI (pinned staging, H2D, kernels,
+        # D2H): the K batches of one launch as one host-resident batch
+        hb = Batch.concat(batches)
         e2e = []
         for _ in range(5):
             t1 = time.perf_counter()
-            ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, batch.pk, batch.sig, batch.msg, batch.off)
+            ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, hb.pk, hb.sig, hb.msg, hb.off)
             e2e.append(time.perf_counter() - t1)
-        e2e_rate = n / statistics.median(e2e)
+        e2e_rate = hb.n / statistics.median(e2e)
         # p50 / p99 of types.VerifyCommit on a 150-validator commit (C1): the
         # C++ L3 path (sign-bytes, tally, batch verifier, error mapping) +
         # H2D + GPU kernels + D2H, through tmv_verify_commit.
@@ -257,6 +259,7 @@ def main():
             "batch_latency_ms": round(batch_ms, 4),
             "serial_verifies_per_s": round(n / (batch_ms * 1e-3), 1),
             "end_to_end_verifies_per_s": round(e2e_rate, 1),
+            "end_to_end_note": f"{hb.n} host-resident signatures per call (pinned staging + PCIe + kernels + D2H)",
             "verify_commit_150_p50_ms": round(lat[len(lat) // 2], 4),
             "verify_commit_150_p99_ms": round(lat[int(len(lat) * 0.99) - 1], 4),
             "verify_commit_note": "types.VerifyCommit (C1: 150 validators) via tmv_verify_commit, host-resident commit",
@@ -266,6 +269,10 @@ def main():
                          "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if args.method == "batch"
                                     else "k_prep + k_verify_quad"),
                          "launch_avg_ms": round(launch_ms, 4),
+                         "aggregate_achieved": round(gpu_rate * MULS_PER_SIG / 1e12, 4),
+                         "aggregate_frac": round(gpu_rate * MULS_PER_SIG / peak, 4),
+                         "aggregate_note": f"{F} launches overlap, so each launch's own duration (above) is longer "
+                                           "than the timed span / launches; aggregate = verifies/s x 2.7e5",
                          "achieved_from": f"{K} x {n} sigs x 2.7e5 canonical products / average launch "
                                           "duration (HIP events on the launch stream)",
                          "work_per_sig": "2.7e5 int32 products (SURVEY 8(d), single-verify equivalent)"},

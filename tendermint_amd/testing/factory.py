@@ -100,6 +100,17 @@ class Batch:
         return (self.pk[32 * i:32 * i + 32].tobytes(), self.msg[self.off[i]:self.off[i + 1]].tobytes(),
                 self.sig[64 * i:64 * i + 64].tobytes())
 
+    @staticmethod
+    def concat(batches) -> "Batch":
+        """Entries of several batches in order, as one batch."""
+        pk = np.concatenate([b.pk for b in batches])
+        sig = np.concatenate([b.sig for b in batches])
+        msg = np.concatenate([b.msg for b in batches])
+        lens = np.concatenate([b.off[1:] - b.off[:-1] for b in batches])
+        off = np.zeros(len(lens) + 1, np.uint32)
+        off[1:] = np.cumsum(lens)
+        return Batch(pk, sig, msg, off, [k for b in batches for k in b.kinds])
+
     def tile(self, n: int) -> "Batch":
         """Repeat entries cyclically up to n (throughput runs on >10k)."""
         idx = np.arange(n) % self.n

@@ -4,7 +4,7 @@ batches per launch K, launches in flight F, method and group size, over 8
 distinct C2 batches reused cyclically.  One JSON line per configuration.
 
   python tools/multi_sweep.py --configs b:6:8:2,b:6:16:2,pe:0:8:2 [--repeat 3]
-config = method(b|pe):group_log2:K:F
+config = method(b|pe):group_log2:K:F[:window]
 """
 import argparse
 import json
@@ -40,9 +40,10 @@ def main():
              torch.from_numpy(b.off.view(np.int32)).to(dev), int(b.off[-1] - b.off[0]), b.n) for b in batches]
     ctx = N.Context(1)
     for cfg in args.configs.split(","):
-        meth, mlog, K, F = cfg.split(":")
-        mlog, K, F = int(mlog), int(K), int(F)
-        ctx.set_batch_options(group_log2=mlog)
+        parts = cfg.split(":")
+        meth, mlog, K, F = parts[0], int(parts[1]), int(parts[2]), int(parts[3])
+        win = int(parts[4]) if len(parts) > 4 else 0
+        ctx.set_batch_options(group_log2=mlog, window_bits=win)
         flags = N.TMV_FLAG_BATCH_EQUATION if meth == "b" else N.TMV_FLAG_PER_ENTRY
         outs = [[torch.zeros(10_000, dtype=torch.int8, device=dev) for _ in range(K)] for _ in range(F)]
         refs = [[N.BatchRef(d_in[j % 8][0].data_ptr(), d_in[j % 8][1].data_ptr(), d_in[j % 8][2].data_ptr(),
@@ -63,7 +64,7 @@ def main():
             torch.cuda.synchronize()
             rates.append(10_000 * K * args.launches / (time.perf_counter() - t0))
         ok = all(int((o == 1).sum().item()) == 9950 for row in outs for o in row)
-        print(json.dumps({"method": meth, "group_log2": mlog, "K": K, "F": F,
+        print(json.dumps({"method": meth, "group_log2": mlog, "window": win, "K": K, "F": F,
                           "verifies_per_s": round(statistics.median(rates)), "spread": round(max(rates) / min(rates), 3),
                           "valid_ok": ok}), flush=True)
 
