@@ -148,11 +148,11 @@ def main():
     for b in batches:
         d_in.append((torch.from_numpy(b.pk).to(dev), torch.from_numpy(b.sig).to(dev), torch.from_numpy(b.msg).to(dev),
                      torch.from_numpy(b.off.view(np.int32)).to(dev), int(b.off[-1] - b.off[0])))
-    d_valid = [[torch.zeros(n, dtype=torch.int8, device=dev) for _ in range(K)] for _ in range(F)]
+    # one contiguous status vector per in-flight launch; batch j is a slice
+    d_valid = [torch.zeros(K * n, dtype=torch.int8, device=dev) for _ in range(F)]
     refs = [[N.BatchRef(pk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(), n, mb,
-                        d_valid[f][j].data_ptr()) for j, (pk, sig, msg, off, mb) in enumerate(d_in)]
+                        d_valid[f][j * n:(j + 1) * n].data_ptr()) for j, (pk, sig, msg, off, mb) in enumerate(d_in)]
             for f in range(F)]
-    counts = [n] * world
     streams = [torch.cuda.Stream(dev) for _ in range(F)]
     comm = torch.cuda.Stream(dev) if world > 1 else None
 
@@ -165,11 +165,11 @@ def main():
         if ev_pair is not None:
             ev_pair[1].record(st)
         if world > 1:
-            # collectives in issue order on one stream, after this launch
+            # one collective per launch (the K vectors are contiguous), in
+            # issue order on one stream, after this launch
             comm.wait_stream(st)
             with torch.cuda.stream(comm):
-                for j in range(kk):
-                    all_gather_validity(d_valid[f][j], counts)
+                all_gather_validity(d_valid[f][:kk * n], [kk * n] * world)
             st.wait_stream(comm)
 
     # single-batch latency (one batch per launch, one at a time), untimed for value
@@ -200,7 +200,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
-    valid = [int((d_valid[f][j] == 1).sum().item()) for f in range(min(F, launches)) for j in range(K)]
+    valid = [int((d_valid[f][j * n:(j + 1) * n] == 1).sum().item()) for f in range(min(F, launches)) for j in range(K)]
     assert all(v == 9950 for v in valid), valid  # C2: 100 edge cases, 50 of them valid (factory.py)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

@@ -24,7 +24,8 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def pack_bits(valid: torch.Tensor) -> torch.Tensor:
-    """uint8 0/1 vector -> little-endian bit-packed uint8 (8 entries per byte)."""
+    """Status vector -> little-endian bit-packed uint8 (8 entries per byte),
+    bit set iff the status is 1 (sr25519 Add-error statuses are negative)."""
     n = valid.numel()
     pad = (-n) % 8
     key = valid.device
@@ -32,7 +33,7 @@ def pack_bits(valid: torch.Tensor) -> torch.Tensor:
     if w is None:
         w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=valid.device)
         _WEIGHTS[key] = w
-    v = torch.nn.functional.pad(valid.reshape(-1).to(torch.int32), (0, pad)).view(-1, 8)
+    v = torch.nn.functional.pad((valid.reshape(-1) == 1).to(torch.int32), (0, pad)).view(-1, 8)
     return (v * w).sum(1).to(torch.uint8)
 
 

@@ -59,3 +59,31 @@ def test_all_gather_world2():
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def _status_worker(rank, world, port, q):
+    """The bench's N > 1 exchange: each rank's contiguous int8 status vector
+    of K batches (sr25519 Add errors are negative) gathered as one bitmap."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    K, n = 3, 1001
+    g = torch.Generator().manual_seed(99 + rank)
+    st = torch.randint(-2, 2, (K * n,), generator=g, dtype=torch.int8)
+    got = all_gather_validity(st, [K * n] * world)
+    mine = got[rank * K * n:(rank + 1) * K * n]
+    q.put((rank, bool(torch.equal(mine, (st == 1).to(torch.uint8))), int(got.numel())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_gather_statuses_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_status_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == [(0, True, 6006), (1, True, 6006)]
