@@ -36,7 +36,7 @@ class GpuBatch : public tmh::BatchVerifier {
   tmh::Error Add(const tmh::PubKey &key, const tmh::Bytes &msg, const tmh::Bytes &sig) override {
     tmh::AddCheck ac = tmh::CheckAdd(kind_, key, sig);
     if (ac.sync) return ac.sync;
-    push(key.bytes.data(), msg, ac.sig64.data(), ac.deferred_sig);
+    push(key.bytes.data(), msg, ac.sig64, ac.deferred_sig);
     return std::nullopt;
   }
 
@@ -204,40 +204,52 @@ void parallel_for(size_t n, size_t min_per_thread, F fn) {
 // Signature backend over the device: entries split by key kind, each kind one
 // tmv_verify_batch_ex call with the key cache (validator keys repeat).  The
 // packed arrays are filled in parallel from precomputed offsets.
+// Packing buffers reused across calls on a thread: fresh multi-megabyte
+// vectors would be new mappings, page-faulted in on every call.
+struct PackBuffers {
+  std::vector<uint32_t> idx, off;
+  std::vector<uint8_t> pk, sig, msg;
+  std::vector<int8_t> out;
+};
+
 struct GpuBackend {
   tmv_ctx *ctx;
   int infra = 0;
-  std::vector<int8_t> operator()(const std::vector<const tmh::SigEntry *> &es) {
-    std::vector<int8_t> st(es.size(), 0);
+  void operator()(const std::vector<const tmh::SigEntry *> &es, std::vector<int8_t> &st) {
+    static thread_local PackBuffers tls;
+    PackBuffers &pb = tls;  // the workers below must use this thread's buffers, not their own
+    st.assign(es.size(), 0);
     for (int kind = 0; kind < 2; kind++) {
       const tmh::KeyType kt = kind == 0 ? tmh::KeyType::Ed25519 : tmh::KeyType::Sr25519;
-      std::vector<uint32_t> idx;
-      std::vector<uint32_t> off{0};
+      pb.idx.clear();
+      pb.off.assign(1, 0);
       for (size_t i = 0; i < es.size(); i++) {
         const tmh::SigEntry &e = *es[i];
         if (e.kind != kt) continue;
-        if (e.pk->size() != 32 || e.sig.size() != 64) continue;  // VerifySignature: false
-        idx.push_back((uint32_t)i);
-        off.push_back(off.back() + (uint32_t)e.msg.size());
+        if (e.pk->size() != 32 || e.sig_len != 64) continue;  // VerifySignature: false
+        pb.idx.push_back((uint32_t)i);
+        pb.off.push_back(pb.off.back() + e.msg_len);
       }
-      if (idx.empty()) continue;
-      const size_t m = idx.size();
-      std::vector<uint8_t> pk(32 * m), sig(64 * m), msg(std::max<uint32_t>(1, off.back()));
-      parallel_for((m + 255) / 256, 4, [&](size_t c) {
-        for (size_t t = c * 256; t < std::min(m, c * 256 + 256); t++) {
-          const tmh::SigEntry &e = *es[idx[t]];
-          std::memcpy(&pk[32 * t], e.pk->data(), 32);
-          std::memcpy(&sig[64 * t], e.sig.data(), 64);
-          if (!e.msg.empty()) std::memcpy(&msg[off[t]], e.msg.data(), e.msg.size());
+      if (pb.idx.empty()) continue;
+      const size_t m = pb.idx.size();
+      pb.pk.resize(32 * m);
+      pb.sig.resize(64 * m);
+      pb.msg.resize(std::max<uint32_t>(1, pb.off.back()));
+      pb.out.resize(m);
+      parallel_for((m + 1023) / 1024, 1, [&](size_t c) {
+        for (size_t t = c * 1024; t < std::min(m, c * 1024 + 1024); t++) {
+          const tmh::SigEntry &e = *es[pb.idx[t]];
+          std::memcpy(&pb.pk[32 * t], e.pk->data(), 32);
+          std::memcpy(&pb.sig[64 * t], e.sig, 64);
+          if (e.msg_len) std::memcpy(&pb.msg[pb.off[t]], e.msg, e.msg_len);
         }
       });
-      std::vector<int8_t> out(m);
       const int rc = tmv_verify_batch_ex(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE,
-                                         pk.data(), sig.data(), msg.data(), off.data(), (uint32_t)m, out.data());
+                                         pb.pk.data(), pb.sig.data(), pb.msg.data(), pb.off.data(), (uint32_t)m,
+                                         pb.out.data());
       if (rc < 0) { infra = rc; continue; }
-      for (size_t t = 0; t < m; t++) st[idx[t]] = out[t];
+      for (size_t t = 0; t < m; t++) st[pb.idx[t]] = pb.out[t];
     }
-    return st;
   }
 };
 
@@ -252,26 +264,6 @@ struct PhaseTimer {
     std::fprintf(stderr, "[tmv_verify_commits] %-8s %9.3f ms\n", what,
                  std::chrono::duration<double, std::milli>(now - t).count());
     t = now;
-  }
-};
-
-// Identity of a signature entry for cross-job dedup: same commit object,
-// same signature index, same public key object, same verifier kind.
-struct EntryKey {
-  const void *commit;
-  const void *pk;
-  int32_t sig_idx;
-  bool batch;
-  bool operator==(const EntryKey &o) const {
-    return commit == o.commit && pk == o.pk && sig_idx == o.sig_idx && batch == o.batch;
-  }
-};
-struct EntryKeyHash {
-  size_t operator()(const EntryKey &k) const {
-    uint64_t h = (uint64_t)(uintptr_t)k.commit * 0x9e3779b97f4a7c15ull;
-    h ^= (uint64_t)(uintptr_t)k.pk + 0x632be59bd9b4e019ull + (h << 6) + (h >> 2);
-    h ^= (uint64_t)(uint32_t)k.sig_idx * 2 + (k.batch ? 1 : 0) + (h << 6) + (h >> 2);
-    return (size_t)h;
   }
 };
 
@@ -361,32 +353,40 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
                                          jb.trust_den);
   });
   tm.mark("plan");
-  // dedupe identical entries across plans (same commit object, index, key)
+  // dedupe identical entries across plans: same commit object and signature
+  // index, same public key object, same verifier kind and the same message
+  // (one slot per (commit, index, kind) instead of a hash map)
   std::vector<const tmh::SigEntry *> uniq;
   std::vector<std::vector<uint32_t>> where(n_jobs);
-  std::unordered_map<EntryKey, uint32_t, EntryKeyHash> seen;
   const bool dedup = n_jobs > 1;
+  std::vector<std::vector<uint32_t>> slot(dedup ? 2 * commits.size() : 0);
   for (uint32_t j = 0; j < n_jobs; j++) {
     const tmh::CommitPlan &pl = plans[j];
     if (pl.early) continue;
     where[j].resize(pl.entries.size());
+    std::vector<uint32_t> *sl = nullptr;
+    if (dedup && jc[j] != SIZE_MAX) {
+      sl = &slot[2 * jc[j] + (pl.batch ? 1 : 0)];
+      if (sl->empty()) sl->assign(pl.commit->signatures.size(), UINT32_MAX);
+    }
     for (size_t e = 0; e < pl.entries.size(); e++) {
-      if (dedup) {
-        const EntryKey key{pl.commit, pl.entries[e].pk, pl.sig_idx[e], pl.batch};
-        auto [it, fresh] = seen.emplace(key, (uint32_t)uniq.size());
-        if (!fresh && uniq[it->second]->msg == pl.entries[e].msg) {
-          where[j][e] = it->second;
+      const tmh::SigEntry &en = pl.entries[e];
+      if (sl) {
+        uint32_t &u = (*sl)[(size_t)pl.sig_idx[e]];
+        if (u != UINT32_MAX && uniq[u]->pk == en.pk && uniq[u]->same_message(en)) {
+          where[j][e] = u;
           continue;
         }
-        it->second = (uint32_t)uniq.size();
+        u = (uint32_t)uniq.size();
       }
       where[j][e] = (uint32_t)uniq.size();
-      uniq.push_back(&pl.entries[e]);
+      uniq.push_back(&en);
     }
   }
   tm.mark("dedup");
   GpuBackend be{ctx};
-  std::vector<int8_t> st = uniq.empty() ? std::vector<int8_t>() : be(uniq);
+  std::vector<int8_t> st;
+  if (!uniq.empty()) be(uniq, st);
   tm.mark("verify");
   if (be.infra < 0) {
     if (errs && err_stride) put_err(errs, err_stride, tmv_last_error());

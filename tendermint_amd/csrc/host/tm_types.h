@@ -199,8 +199,9 @@ inline uint8_t *PutBytesField(uint8_t *p, uint8_t tag, const Bytes &b) {
 // omitted; the timestamp is always present).  block_id == nullptr or a nil
 // BlockID omits field 4 (types/canonical.go:18-32).  Sizes are computed first
 // and the message is written in one pass into one buffer.
-inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t height, int32_t round,
-                           const BlockID *block_id, const Timestamp &ts) {
+// Appends the encoding to `out` (no allocation when `out` has capacity).
+inline void AppendVoteSignBytes(Bytes &out, const std::string &chain_id, int32_t type, int64_t height,
+                                int32_t round, const BlockID *block_id, const Timestamp &ts) {
   const bool has_bid = block_id && !block_id->IsNil();
   size_t psh_len = 0, cb_len = 0;
   if (has_bid) {
@@ -221,8 +222,9 @@ inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t he
   body += 1 + UvarintLen(t_len) + t_len;
   if (!chain_id.empty()) body += 1 + UvarintLen(chain_id.size()) + chain_id.size();
 
-  Bytes out(UvarintLen(body) + body);
-  uint8_t *p = PutUvarintP(out.data(), body);
+  const size_t at = out.size();
+  out.resize(at + UvarintLen(body) + body);
+  uint8_t *p = PutUvarintP(out.data() + at, body);
   if (type != 0) { *p++ = 0x08; p = PutUvarintP(p, (uint64_t)(uint32_t)type); }
   if (height != 0) { *p++ = 0x11; p = PutFixed64P(p, height); }
   if (round != 0) { *p++ = 0x19; p = PutFixed64P(p, (int64_t)round); }
@@ -246,6 +248,12 @@ inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t he
     std::memcpy(p, chain_id.data(), chain_id.size());
     p += chain_id.size();
   }
+}
+
+inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t height, int32_t round,
+                           const BlockID *block_id, const Timestamp &ts) {
+  Bytes out;
+  AppendVoteSignBytes(out, chain_id, type, height, round, block_id, ts);
   return out;
 }
 
@@ -256,10 +264,15 @@ struct Commit {
   std::vector<CommitSig> signatures;
   // types/block.go:836-862: only the timestamp and the flag differ per index
   Bytes VoteSignBytes(const std::string &chain_id, int32_t idx) const {
+    Bytes out;
+    AppendVoteSignBytes(out, chain_id, idx);
+    return out;
+  }
+  void AppendVoteSignBytes(Bytes &out, const std::string &chain_id, int32_t idx) const {
     const CommitSig &cs = signatures[(size_t)idx];
     // BlockIDFor: the commit's BlockID for a Commit flag, else the nil BlockID
-    return tmh::VoteSignBytes(chain_id, kPrecommitType, height, round,
-                              cs.block_id_flag == BlockIDFlagCommit ? &block_id : nullptr, cs.timestamp);
+    tmh::AppendVoteSignBytes(out, chain_id, kPrecommitType, height, round,
+                             cs.block_id_flag == BlockIDFlagCommit ? &block_id : nullptr, cs.timestamp);
   }
 };
 
@@ -340,8 +353,13 @@ inline std::pair<int64_t, bool> SafeMul(int64_t a, int64_t b) {
 struct AddCheck {
   Error sync;
   std::string deferred_sig;
-  Bytes sig64;  // the 64 bytes handed to the device (zeros when the length is wrong)
+  const uint8_t *sig64 = nullptr;  // the 64 bytes handed to the device (zeros when the length is wrong)
 };
+
+inline const uint8_t *ZeroSignature() {
+  static const uint8_t z[64] = {0};
+  return z;
+}
 
 inline bool ScalarCanonical(const uint8_t s[32]) {
   static const uint8_t L[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7,
@@ -363,7 +381,7 @@ inline AddCheck CheckAdd(KeyType batch_kind, const PubKey &key, const Bytes &sig
       return r;
     }
     if (sig.size() != 64) { r.sync = std::string("invalid signature"); return r; }
-    r.sig64 = sig;
+    r.sig64 = sig.data();
     return r;
   }
   if (key.type != KeyType::Sr25519) { r.sync = std::string("sr25519: pubkey is not sr25519"); return r; }
@@ -371,12 +389,12 @@ inline AddCheck CheckAdd(KeyType batch_kind, const PubKey &key, const Bytes &sig
     r.sync = "sr25519: invalid public key: sr25519: bad PublicKey size: " + std::to_string(key.bytes.size());
     return r;
   }
-  r.sig64.assign(64, 0);  // a zero signature has no schnorrkel marker: the device reports -2
+  r.sig64 = ZeroSignature();  // a zero signature has no schnorrkel marker: the device reports -2
   if (sig.size() != 64) {
     r.deferred_sig = "sr25519: unable to decode signature: sr25519: bad Signature size: " + std::to_string(sig.size());
     return r;
   }
-  r.sig64 = sig;
+  r.sig64 = sig.data();
   uint8_t sc[32];
   std::memcpy(sc, sig.data() + 32, 32);
   if (!(sc[31] & 0x80)) {
@@ -397,11 +415,18 @@ constexpr int kBatchVerifyThreshold = 2;  // types/validation.go:12
 
 // One signature to verify: status 1 valid, 0 invalid, -1 / -2 device-found
 // sr25519 Add errors (public key / signature encoding).
+// A view: the message lives in the plan's sign-bytes arena, the signature in
+// the commit (both outlive the backend call).
 struct SigEntry {
   KeyType kind;
   const Bytes *pk;
-  Bytes msg;
-  Bytes sig;
+  const uint8_t *msg;
+  uint32_t msg_len;
+  uint32_t sig_len;
+  const uint8_t *sig;
+  bool same_message(const SigEntry &o) const {
+    return msg_len == o.msg_len && (msg_len == 0 || std::memcmp(msg, o.msg, msg_len) == 0);
+  }
 };
 using SigBackend = std::function<std::vector<int8_t>(const std::vector<SigEntry> &)>;
 
@@ -414,6 +439,7 @@ struct CommitPlan {
   bool defer_add = false;            // sr25519 batch: device statuses -1/-2 are Add errors
   int64_t tallied = 0, needed = 0;
   std::vector<SigEntry> entries;     // in Add order
+  Bytes msg_arena;                   // sign-bytes of the entries, back to back
   std::vector<int> sig_idx;          // commit.Signatures index of each entry
   std::vector<std::string> deferred_sig;
   std::vector<uint8_t> crosses;      // single: this entry crosses the threshold (early ok)
@@ -445,6 +471,9 @@ struct CommitVerifier {
       pl.defer_add = bkind == KeyType::Sr25519;
     }
     std::unordered_map<int32_t, int> seen;
+    std::vector<uint32_t> msg_at;
+    pl.msg_arena.reserve(commit.signatures.size() * 128);
+    pl.entries.reserve(commit.signatures.size());
     for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
       const CommitSig &cs = commit.signatures[idx];
       if (ignore(cs)) continue;
@@ -463,25 +492,32 @@ struct CommitVerifier {
         seen[vi] = (int)idx;
         val = v;
       }
-      SigEntry e{val->pub_key.type, &val->pub_key.bytes, commit.VoteSignBytes(chain_id, (int32_t)idx), {}};
+      SigEntry e{val->pub_key.type, &val->pub_key.bytes, nullptr, 0, 0, nullptr};
       if (pl.batch) {
         AddCheck ac = CheckAdd(bkind, val->pub_key, cs.signature);
         if (ac.sync) {  // bv.Add error, returned verbatim (:211-213)
           pl.early = ac.sync;
           return;
         }
-        e.sig = std::move(ac.sig64);
+        e.sig = ac.sig64;
+        e.sig_len = 64;
         pl.deferred_sig.push_back(std::move(ac.deferred_sig));
       } else {
-        e.sig = cs.signature;
+        e.sig = cs.signature.data();
+        e.sig_len = (uint32_t)cs.signature.size();
       }
-      pl.entries.push_back(std::move(e));
+      msg_at.push_back((uint32_t)pl.msg_arena.size());
+      commit.AppendVoteSignBytes(pl.msg_arena, chain_id, (int32_t)idx);
+      e.msg_len = (uint32_t)(pl.msg_arena.size() - msg_at.back());
+      pl.entries.push_back(e);
       pl.sig_idx.push_back((int)idx);
       if (count(cs)) pl.tallied += val->voting_power;
       const bool cross = !count_all && pl.tallied > pl.needed;
       pl.crosses.push_back(cross ? 1 : 0);
       if (cross) break;
     }
+    // the arena no longer grows: point the entries at their messages
+    for (size_t i = 0; i < pl.entries.size(); i++) pl.entries[i].msg = pl.msg_arena.data() + msg_at[i];
   }
 
   // Signature results -> the reference's return value.

@@ -68,11 +68,11 @@ __device__ __forceinline__ void p3_dbl(ge_p3 &a) {
 // Bucket b's sum; false if the bucket is empty.  A bucket that fits in one
 // chunk was stored whole by k_msm_accum; a longer one is the run that left
 // its first chunk, the middle chunks and the run that ended in its last.
-__device__ bool bucket_value(const MsmWork &mw, uint32_t b, ge_p3 &out) {
+__device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &out) {
   const uint32_t cnt = mw.bk_cnt[b];
   if (cnt == 0) return false;
   const uint32_t bs = mw.bk_start[b];
-  const uint32_t t0 = bs / kMsmChunk, t1 = (bs + cnt - 1) / kMsmChunk;
+  const uint32_t t0 = bs / L, t1 = (bs + cnt - 1) / L;
   if (t0 == t1) {
     out = mw.bk_sum[b];
     return true;
@@ -259,10 +259,11 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   for (uint32_t t = scan[kMsmSortBlock] + tid; t < p.cap; t += kMsmSortBlock) ent_bk[t] = kMsmEmpty;
 }
 
-// One lane per chunk of kMsmChunk sorted entries: sums each run of equal
+// One lane per chunk of L sorted entries: sums each run of equal
 // bucket ids with mixed additions.  A run that is the whole bucket goes to
 // bk_sum; a run cut by the chunk's end goes to part_last, one cut by its
 // start to part_first (k_msm_wpart joins them).
+template <int L>
 __global__ void __launch_bounds__(256)
 k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, uint32_t per_xcd) {
   // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD a
@@ -274,13 +275,13 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, uint
   const uint32_t g = t / cpg;
   if (g >= p.groups) return;
   if ((g << p.m_log2) >= entry_count(count_ptr, n)) return;
-  const uint32_t base = t * kMsmChunk;
-  uint32_t bk[kMsmChunk], pt[kMsmChunk];
+  const uint32_t base = t * L;
+  uint32_t bk[L], pt[L];
   {
     const uint4 *b4 = reinterpret_cast<const uint4 *>(mw.ent_bk + base);
     const uint4 *p4 = reinterpret_cast<const uint4 *>(mw.ent_pt + base);
 #pragma unroll
-    for (int q = 0; q < kMsmChunk / 4; q++) {
+    for (int q = 0; q < L / 4; q++) {
       const uint4 x = b4[q], y = p4[q];
       bk[4 * q] = x.x; bk[4 * q + 1] = x.y; bk[4 * q + 2] = x.z; bk[4 * q + 3] = x.w;
       pt[4 * q] = y.x; pt[4 * q + 1] = y.y; pt[4 * q + 2] = y.z; pt[4 * q + 3] = y.w;
@@ -290,7 +291,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, uint
   auto flush = [&](uint32_t b, uint32_t rs, uint32_t re, const ge_p3 &acc) {
     const uint32_t bs = mw.bk_start[b], be = bs + mw.bk_cnt[b];
     if (rs == bs && re == be) mw.bk_sum[b] = acc;
-    else if (re == base + kMsmChunk && re < be) mw.part_last[t] = acc;
+    else if (re == base + L && re < be) mw.part_last[t] = acc;
     else mw.part_first[t] = acc;
   };
   ge_p3 acc;
@@ -299,7 +300,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, uint
   uint32_t j = 0;
   bool more = true;
 #pragma unroll
-  for (int q = 0; q < kMsmChunk; q++) {
+  for (int q = 0; q < L; q++) {
     more = more && bk[q] != kMsmEmpty;  // padding only follows the last bucket
     if (!more) continue;
     if (bk[q] != cur) {
@@ -337,7 +338,7 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   bool u_set = false, t_set = false;
   for (int i = (int)s - 1; i >= 0; i--) {
     ge_p3 B;
-    if (bucket_value(mw, g * p.W * p.H + wdx * p.H + part * s + (uint32_t)i, B)) {
+    if (bucket_value(mw, p.L, g * p.W * p.H + wdx * p.H + part * s + (uint32_t)i, B)) {
       if (u_set) p3_add(U, B);
       else { U = B; u_set = true; }
     }
@@ -427,7 +428,12 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
   const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
-  hipLaunchKernelGGL(k_msm_accum, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+  if (p.L == 8)
+    hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+  else if (p.L == 16)
+    hipLaunchKernelGGL(k_msm_accum<16>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+  else
+    hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
   hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <list>
 #include <unordered_map>
@@ -124,10 +125,10 @@ struct KeyIndex {
       if (e.state == 1 && std::memcmp(e.key.data(), k33, 33) == 0) { e.state = 2; live--; return; }
     }
   }
-  void rehash() {
+  void rehash() {  // drops tombstones; doubles the table when over a quarter full
     std::vector<Ent> old;
     old.swap(t);
-    t.assign(old.size(), Ent{{}, 0, 0});
+    t.assign(4 * live >= old.size() ? 2 * old.size() : old.size(), Ent{{}, 0, 0});
     live = used = 0;
     for (const Ent &e : old)
       if (e.state == 1) insert(e.key.data(), e.slot);
@@ -183,6 +184,7 @@ int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
 // (0.5 ms for 10k) beats the batch check's longer chain (~1 ms); above it
 // the batch check does 2-3x less work.  Flags override per call.
 uint32_t g_msm_min = 16384;
+uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk length (A/B measurement)
 
 void read_env() {
   static std::once_flag once;
@@ -194,6 +196,8 @@ void read_env() {
     g_quad_max = t ? (uint32_t)strtoul(t, nullptr, 10) : 49152u;
     const char *mm = getenv("TMV_MSM_MIN");
     if (mm) g_msm_min = (uint32_t)strtoul(mm, nullptr, 10);
+    const char *mc = getenv("TMV_MSM_CHUNK");
+    if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
   });
 }
 
@@ -215,8 +219,24 @@ tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c) {
     }
   }
   c = std::max<uint32_t>(4, std::min<uint32_t>(9, c));
-  return tmv::MsmParams::make(n, m_log2, c);
+  tmv::MsmParams p = tmv::MsmParams::make(n, m_log2, c);
+  if (g_msm_chunk == 8 || g_msm_chunk == 16 || g_msm_chunk == 32) p.L = g_msm_chunk;
+  return p;
 }
+
+// Phase timing of the host-buffer path, printed to stderr when
+// TMV_HOST_TIMING is set (profiling aid; the host layer prints its own).
+struct EngineTimer {
+  bool on = getenv("TMV_HOST_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char *what, uint32_t n) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[tmv_engine] %-8s %9.3f ms (n=%u)\n", what,
+            std::chrono::duration<double, std::milli>(now - t).count(), n);
+    t = now;
+  }
+};
 
 // Packed staging layout for one shard: pk | sig | off | msg (16-B aligned).
 struct Layout {
@@ -412,34 +432,72 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   const uint64_t epoch = ++d.kepoch;
   std::vector<uint32_t> miss_idx;
   std::vector<uint32_t> miss_slot;
+  // 1) read-only lookups, in parallel for large batches (runs of one key
+  //    reuse the previous answer)
+  auto lookup = [&](uint32_t lo, uint32_t hi) {
+    uint8_t key[33];
+    key[0] = sr ? 1 : 0;
+    const uint8_t *last_pk = nullptr;
+    uint32_t last_slot = UINT32_MAX;
+    for (uint32_t i = lo; i < hi; i++) {
+      const uint8_t *p = pk + 32ull * i;
+      if (last_pk && std::memcmp(p, last_pk, 32) == 0) { slots_out[i] = last_slot; continue; }
+      std::memcpy(key + 1, p, 32);
+      last_slot = slots_out[i] = d.kindex.find(key);
+      last_pk = p;
+    }
+  };
+  const uint32_t nth = n >= 16384 ? std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
+  if (nth > 1) {
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nth; t++) th.emplace_back(lookup, (uint32_t)((uint64_t)n * t / nth), (uint32_t)((uint64_t)n * (t + 1) / nth));
+    lookup(0, (uint32_t)((uint64_t)n / nth));
+    for (auto &x : th) x.join();
+  } else {
+    lookup(0, n);
+  }
+  // 2) pin every key found to this batch (epoch) before any miss may evict
+  uint32_t distinct = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t slot = slots_out[i];
+    if (slot == UINT32_MAX || d.kslot_epoch[slot] == epoch) continue;
+    d.kslot_epoch[slot] = epoch;
+    distinct++;
+    d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
+    d.khits++;
+  }
+  // 3) misses.  First decide, before touching the index, whether the batch
+  //    fits: bailing out after inserting keys whose tables were never built
+  //    would leave stale entries behind.
   uint8_t key[33];
   key[0] = sr ? 1 : 0;
-  uint32_t distinct = 0;
-  uint32_t last_slot = UINT32_MAX;
-  const uint8_t *last_pk = nullptr;
-  for (uint32_t i = 0; i < n; i++) {
-    const uint8_t *p = pk + 32ull * i;
-    if (last_pk && std::memcmp(p, last_pk, 32) == 0) {  // runs of one key
-      slots_out[i] = last_slot;
-      continue;
-    }
-    std::memcpy(key + 1, p, 32);
-    uint32_t slot = d.kindex.find(key);
-    if (slot != UINT32_MAX) {
-      if (d.kslot_epoch[slot] != epoch) {
-        d.kslot_epoch[slot] = epoch;
+  {
+    KeyIndex fresh;
+    bool any = false;
+    for (uint32_t i = 0; i < n && distinct <= d.kcap; i++) {
+      if (slots_out[i] != UINT32_MAX) continue;
+      if (!any) { fresh.init(std::min<size_t>(n, d.kcap + 1)); any = true; }
+      std::memcpy(key + 1, pk + 32ull * i, 32);
+      if (fresh.find(key) == UINT32_MAX) {
+        fresh.insert(key, 0);
         distinct++;
-        d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
-        d.khits++;
       }
-    } else {
-      if (++distinct > d.kcap) return 1;
+    }
+    if (distinct > d.kcap) return 1;
+  }
+  //    then give each missing key a slot (LRU victims are never keys of this
+  //    batch: every key found above is pinned to this epoch)
+  for (uint32_t i = 0; i < n; i++) {
+    if (slots_out[i] != UINT32_MAX) continue;
+    const uint8_t *p = pk + 32ull * i;
+    std::memcpy(key + 1, p, 32);
+    uint32_t slot = d.kindex.find(key);  // inserted by an earlier miss of this batch
+    if (slot == UINT32_MAX) {
       if (d.kindex.size() < d.kcap && d.klru.size() < d.kcap) {
         slot = (uint32_t)d.klru.size();
         d.klru.push_front(slot);
       } else {
         slot = d.klru.back();  // least recently used; never one pinned by this batch
-        if (d.kslot_epoch[slot] == epoch) return 1;
         d.kindex.erase(d.kslot_key[slot].data());
         d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
       }
@@ -452,8 +510,6 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
       d.kmisses++;
     }
     slots_out[i] = slot;
-    last_slot = slot;
-    last_pk = p;
   }
   const uint32_t m = (uint32_t)miss_idx.size();
   if (m) {
@@ -701,6 +757,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
   if ((e = d.d_in.ensure(total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  EngineTimer tm;
   uint8_t *h = static_cast<uint8_t *>(d.h_in.ptr);
   par_memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
   par_memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
@@ -709,6 +766,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
   for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
   if (mbytes) par_memcpy(h + L.msg, msg + base, mbytes);
   if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
+  tm.mark("stage", n);
   if (cached) {
     const int kr = resolve_keys(d, sch == Scheme::Sr25519Cached, pk + 32ull * lo, n,
                                 reinterpret_cast<uint32_t *>(h + kind_at), d.stream);
@@ -717,6 +775,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
       sch = sch == Scheme::Sr25519Cached ? Scheme::Sr25519 : Scheme::Ed25519;
     }
   }
+  tm.mark("keys", n);
   if ((e = hipMemcpyAsync(d.d_in.ptr, h, total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
@@ -769,8 +828,10 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   for (uint32_t s = 0; s <= shards; s++) bounds[s] = (uint32_t)((uint64_t)n * s / shards);
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
   int rc = 0;
+  EngineTimer tm;
   for (uint32_t s = 0; s < shards && rc == 0; s++)
     rc = stage_and_launch(ctx, flags, *ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
+  tm.mark("launched", n);
   for (uint32_t s = 0; s < shards; s++) {
     Device &d = *ctx->devs[s];
     (void)hipSetDevice(d.id);
@@ -779,6 +840,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     if (rc == 0) std::memcpy(out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
     if (rc == 0 && ctx->stats) collect_stats(ctx, d, d.stream);
   }
+  tm.mark("synced", n);
   if (rc != 0) return rc;
   for (uint32_t i = 0; i < n; i++)
     if (out[i] != 1) return TMV_NOT_ALL;

@@ -26,16 +26,16 @@ Bytes fake_sig(const Bytes &pk, const Bytes &msg) {
   return s;
 }
 
-int8_t fake_status(const SigEntry &e) {
-  if (e.kind == KeyType::Sr25519) {
-    if (!e.pk->empty() && (*e.pk)[0] == 0xFF) return -1;
-    if (e.sig.size() != 64 || !(e.sig[63] & 0x80)) return -2;
-    Bytes want = fake_sig(*e.pk, e.msg);
+int8_t fake_status(KeyType kind, const Bytes &pk, const Bytes &msg, const Bytes &sig) {
+  if (kind == KeyType::Sr25519) {
+    if (!pk.empty() && pk[0] == 0xFF) return -1;
+    if (sig.size() != 64 || !(sig[63] & 0x80)) return -2;
+    Bytes want = fake_sig(pk, msg);
     want[63] |= 0x80;
-    return want == e.sig ? 1 : 0;
+    return want == sig ? 1 : 0;
   }
-  if (e.sig.size() != 64) return 0;
-  return fake_sig(*e.pk, e.msg) == e.sig ? 1 : 0;
+  if (sig.size() != 64) return 0;
+  return fake_sig(pk, msg) == sig ? 1 : 0;
 }
 
 }  // namespace
@@ -62,9 +62,10 @@ int tmv_verify_batch_ex(tmv_ctx *, uint8_t key_kind, uint32_t, const uint8_t *pk
   bool all = n > 0;
   for (uint32_t i = 0; i < n; i++) {
     const Bytes key(pk + 32 * i, pk + 32 * i + 32);
-    SigEntry e{key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, &key,
-               Bytes(msg + msg_off[i], msg + msg_off[i + 1]), Bytes(sig + 64 * i, sig + 64 * i + 64)};
-    status_out[i] = g_skip_hash ? 1 : fake_status(e);
+    status_out[i] = g_skip_hash ? 1
+                                : fake_status(key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, key,
+                                              Bytes(msg + msg_off[i], msg + msg_off[i + 1]),
+                                              Bytes(sig + 64 * i, sig + 64 * i + 64));
     all = all && status_out[i] == 1;
   }
   return all ? TMV_ALL_VALID : TMV_NOT_ALL;

@@ -181,6 +181,15 @@ def test_verify_many_equals_single_fake(fake):
     assert sum(r is None for r in many) > 20 and sum(r is not None for r in many) > 20
 
 
+def test_verify_many_equals_single_fake_large(fake):
+    """Large enough (≈15k entries) for the multi-threaded packing and the
+    shared-commit dedup slots of tmv_verify_commits."""
+    jobs = F.random_jobs("fake", 3000, seed=9)
+    many = F.fake_verify_commits(fake, jobs)
+    single = [F.single_result(fake, jb) for jb in jobs]
+    assert many == single
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("scheme", ["ed25519", "sr25519"])
 def test_verify_many_equals_single_gpu(ctx, scheme):

@@ -67,6 +67,12 @@ for lo in (0, 50, 100, 150, 0, 60):
     assert np.array_equal(st.astype(np.uint8), ref[idx]), lo
 ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
 assert np.array_equal(st.astype(np.uint8), ref)
+# the over-capacity batch must not leave keys without tables behind
+for lo in (0, 50, 100, 150, 120, 10):
+    idx = list(range(lo, min(lo + 50, b.n)))
+    sub = Batch.from_entries([b.entry(i) for i in idx])
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, sub.pk, sub.sig, sub.msg, sub.off)
+    assert np.array_equal(st.astype(np.uint8), ref[idx]), ("after overflow", lo)
 s = ctx.key_cache_stats()
 assert s["used"] <= 64 and s["capacity"] == 64, s
 print("ok", s)
