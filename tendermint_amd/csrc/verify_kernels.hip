@@ -15,6 +15,10 @@
 
 namespace tmv {
 
+#ifndef TMV_DECODE_WAVES
+#define TMV_DECODE_WAVES 2  // 3 fits ed25519 decode in 168 VGPRs but spills 76 B/lane: measured slower
+#endif
+
 __global__ void __launch_bounds__(kVerifyBlock)
 k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
                  const uint8_t *__restrict__ msg, const uint32_t *__restrict__ msg_off, uint32_t n,
@@ -47,48 +51,28 @@ k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig
 // k_prep stores -A in P3Q layout, R (ed25519: CachedQ; sr25519: P3Q) and k;
 // decode failures go to flags (4 bytes per entry: A ok, R ok, s ok, -).
 
-// Task-uniform waves: lanes [0, m) decode A, [m, 2m) decode R and [2m, 3m)
-// compute the challenge, so no wave mixes decompression with hashing.
+// Two kernels, so each gets its own register budget: k_prep_decode (lanes
+// [0, m) decode A, [m, 2m) decode R; 3 waves/SIMD for ed25519) and
+// k_prep_hash (one lane per entry: SHA-512 + Barrett, or the merlin
+// transcript).
 template <bool SR>
-__global__ void __launch_bounds__(kVerifyBlock)
-k_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
-       const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
-       Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned) {
+__global__ void __launch_bounds__(kVerifyBlock, SR ? 2 : TMV_DECODE_WAVES)
+k_prep_decode(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
+              const uint32_t *count_ptr, uint32_t n, Ed25519Work w, int aligned) {
   const uint32_t m = entry_count(count_ptr, n);
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 3 * m) return;
-  const uint32_t task = j / m;
-  const uint32_t e = j - task * m;
+  if (j >= 2 * m) return;
+  const bool isA = j < m;
+  const uint32_t e = isA ? j : j - m;
   const uint32_t i = idx ? idx[e] : e;
-  uint32_t a_w[8], r_w[8];
-  if (task != 1) {
-    if (aligned) load_words_aligned(a_w, pk + 32ull * i);
-    else load_words_unaligned(a_w, pk + 32ull * i);
-  }
-  if (task != 0) {
-    if (aligned) load_words_aligned(r_w, sig + 64ull * i);
-    else load_words_unaligned(r_w, sig + 64ull * i);
-  }
-  if (task == 2) {
-    uint32_t k[8];
-    const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
-    if (SR) {
-      sr25519_challenge(k, *prefix, a_w, r_w, msg + o0, o1 - o0);
-    } else {
-      uint32_t h[16];
-      sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
-      sc_reduce512(k, h);
-    }
-    uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
-    kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
-    kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
-    return;
-  }
-  const bool isA = task == 0;
+  uint32_t p_w[8];
+  const uint8_t *src = isA ? pk + 32ull * i : sig + 64ull * i;
+  if (aligned) load_words_aligned(p_w, src);
+  else load_words_unaligned(p_w, src);
   ge_p3 P;
   bool ok;
-  if (SR) ok = ristretto_decode(P, isA ? a_w : r_w);
-  else ok = ge_decode_zip215(P, isA ? a_w : r_w);
+  if (SR) ok = ristretto_decode(P, p_w);
+  else ok = ge_decode_zip215(P, p_w);
   if (!ok) ge_p3_identity(P);  // keep limbs bounded; the flag rejects the entry
   w.flags[4 * e + (isA ? 0 : 1)] = ok ? 1 : 0;
   if (w.niels) {  // -P in affine Niels form for the batch equation (Z = 1)
@@ -118,6 +102,37 @@ k_prep(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const ui
     dst[2] = c.T2d;
     dst[3] = c.Z;
   }
+}
+
+template <bool SR>
+__global__ void __launch_bounds__(kVerifyBlock)
+k_prep_hash(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
+            const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+            uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned) {
+  const uint32_t m = entry_count(count_ptr, n);
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m) return;
+  const uint32_t i = idx ? idx[e] : e;
+  uint32_t a_w[8], r_w[8];
+  if (aligned) {
+    load_words_aligned(a_w, pk + 32ull * i);
+    load_words_aligned(r_w, sig + 64ull * i);
+  } else {
+    load_words_unaligned(a_w, pk + 32ull * i);
+    load_words_unaligned(r_w, sig + 64ull * i);
+  }
+  uint32_t k[8];
+  const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
+  if (SR) {
+    sr25519_challenge(k, *prefix, a_w, r_w, msg + o0, o1 - o0);
+  } else {
+    uint32_t h[16];
+    sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
+    sc_reduce512(k, h);
+  }
+  uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
+  kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
+  kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
 }
 
 // Signed radix-16 recoding written straight to LDS (lanes with c >= 2 skip).
@@ -520,10 +535,7 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
                                   uint8_t *out, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = is_aligned(pk, sig);
-  const uint32_t pblocks = (uint32_t)((3ull * n + kVerifyBlock - 1) / kVerifyBlock);
-  hipLaunchKernelGGL(k_prep<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
-                     count_ptr, n, w, prefix, aligned);
-  hipError_t e = hipGetLastError();
+  hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
   hipLaunchKernelGGL(k_verify_quad<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
@@ -553,8 +565,13 @@ template <bool SR>
 hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                        const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const strobe_t *prefix,
                        Ed25519Work w, int aligned, hipStream_t stream) {
-  const uint32_t pblocks = (uint32_t)((3ull * n + kVerifyBlock - 1) / kVerifyBlock);
-  hipLaunchKernelGGL(k_prep<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
+  const uint32_t dblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
+  hipLaunchKernelGGL(k_prep_decode<SR>, dim3(dblocks), dim3(kVerifyBlock), 0, stream, pk, sig, idx, count_ptr, n, w,
+                     aligned);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t hblocks = (n + kVerifyBlock - 1) / kVerifyBlock;
+  hipLaunchKernelGGL(k_prep_hash<SR>, dim3(hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
                      count_ptr, n, w, prefix, aligned);
   return hipGetLastError();
 }
