@@ -99,6 +99,53 @@ def merlin_test_vector() -> bytes:
     return out.tobytes()
 
 
+L_ORDER = 2**252 + 27742317777372353535851937790883648493
+
+
+def ed25519_prechecks(pk: np.ndarray, sig: np.ndarray) -> np.ndarray:
+    """Per entry: A and R decode (ZIP-215 lax) and S < l — the entries a
+    random-linear-combination batch check includes (test infrastructure: the
+    expected group verdicts follow from these and the validity vector)."""
+    L = lib()
+    n = len(pk) // 32
+    out = np.zeros(n, bool)
+    x, y = np.zeros(32, np.uint8), np.zeros(32, np.uint8)
+    for i in range(n):
+        a = np.ascontiguousarray(pk[32 * i:32 * i + 32])
+        r = np.ascontiguousarray(sig[64 * i:64 * i + 32])
+        s = int.from_bytes(sig[64 * i + 32:64 * i + 64].tobytes(), "little")
+        out[i] = (s < L_ORDER and bool(L.oracle_ge_decode_lax(_p(a), _p(x), _p(y)))
+                  and bool(L.oracle_ge_decode_lax(_p(r), _p(x), _p(y))))
+    return out
+
+
+def sr25519_prechecks(pk: np.ndarray, sig: np.ndarray) -> np.ndarray:
+    """As ed25519_prechecks for sr25519: A and R Ristretto-decode, the
+    schnorrkel marker is set and the cleared scalar is < l."""
+    L = lib()
+    n = len(pk) // 32
+    out = np.zeros(n, bool)
+    x, y = np.zeros(32, np.uint8), np.zeros(32, np.uint8)
+    for i in range(n):
+        a = np.ascontiguousarray(pk[32 * i:32 * i + 32])
+        r = np.ascontiguousarray(sig[64 * i:64 * i + 32])
+        sb = bytearray(sig[64 * i + 32:64 * i + 64].tobytes())
+        marker = bool(sb[31] & 0x80)
+        sb[31] &= 0x7F
+        out[i] = (marker and int.from_bytes(bytes(sb), "little") < L_ORDER
+                  and bool(L.oracle_ristretto_decode(_p(a), _p(x), _p(y)))
+                  and bool(L.oracle_ristretto_decode(_p(r), _p(x), _p(y))))
+    return out
+
+
+def failing_groups(precheck: np.ndarray, valid: np.ndarray, m: int) -> int:
+    """Groups of m consecutive entries that must fail the batch equation:
+    those holding an entry that passes the pre-checks but is invalid."""
+    bad = precheck & ~valid.astype(bool)
+    n = len(bad)
+    return int(sum(bad[g:g + m].any() for g in range(0, n, m)))
+
+
 def pack(entries):
     """[(pk, msg, sig)] -> (pk[n*32], sig[n*64], msg[], off[n+1]) numpy arrays."""
     n = len(entries)

@@ -50,8 +50,9 @@ def test_c2_full_size_bit_exact(bctx, golden):
     bits = np.packbits(st.astype(np.uint8), bitorder="little").tobytes().hex()
     assert bits == g["valid_bits_hex"] and not ok
     assert groups == (10_000 + 63) // 64
-    # 1% edge cases, of which only the bit flips decode and fail the equation
-    assert 0 < failed <= 20, failed
+    # exactly the groups holding a bit-flipped entry that still decodes fail
+    want = C.failing_groups(C.ed25519_prechecks(b.pk, b.sig), st == 1, 64)
+    assert 0 < want <= 20 and failed == want, (failed, want)
 
 
 def test_honest_groups_pass(bctx, honest):
@@ -60,15 +61,32 @@ def test_honest_groups_pass(bctx, honest):
     assert groups == (1500 + 63) // 64 and failed == 0
 
 
+_C2S = {}
+
+
+def _c2_small():
+    if "b" not in _C2S:
+        _C2S["b"] = make_c2_batch(2000, seed=5, edge_scale=5.0)
+    return _C2S["b"]
+
+
+def _c2_small_pre():
+    if "pre" not in _C2S:
+        b = _c2_small()
+        _C2S["pre"] = C.ed25519_prechecks(b.pk, b.sig)
+    return _C2S["pre"]
+
+
 @pytest.mark.parametrize("m_log2,c", [(5, 4), (6, 5), (7, 6), (8, 7), (9, 8), (10, 9), (6, 9), (10, 4)])
 def test_group_window_sweep(bctx, honest, m_log2, c):
     ok, st, groups, failed = _run(bctx, ED, honest, group_log2=m_log2, window_bits=c)
     assert ok and (st == 1).all() and failed == 0
     assert groups == (1500 + (1 << m_log2) - 1) >> m_log2
-    b = make_c2_batch(2000, seed=5, edge_scale=5.0)
+    b = _c2_small()
     ok, st, _, failed = _run(bctx, ED, b, group_log2=m_log2, window_bits=c)
     _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
     assert np.array_equal(st.astype(np.uint8), ref) and not ok
+    assert failed == C.failing_groups(_c2_small_pre(), ref == 1, 1 << m_log2)
 
 
 def test_zip215_small_order_matrix_passes_equation(bctx, golden):
@@ -116,7 +134,8 @@ def test_sr25519_vs_oracle(bctx):
     ok, st, groups, failed = _run(bctx, SR, b)
     ref = C.sr25519_status_packed(b.pk, b.sig, b.msg, b.off, threads=8)
     assert np.array_equal(st, ref) and ok == bool((ref == 1).all())
-    assert failed < groups
+    want = C.failing_groups(C.sr25519_prechecks(b.pk, b.sig), ref == 1, 64)
+    assert 0 < want < groups and failed == want, (failed, want)
 
 
 def test_sr25519_honest_groups_pass(bctx):
