@@ -74,10 +74,13 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-def _load_traffic():
-    p = os.path.join(REPO, "profiles", "traffic_r01.json")
+def _load_traffic(method: str):
+    """HBM bytes per launch of 32 C2 batches from the committed PMC passes
+    (tools/profile_round.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE)."""
+    name = "pmc_batch.json" if method == "batch" else "pmc_per_entry.json"
     try:
-        with open(p) as f:
+        with open(os.path.join(REPO, "profiles", "r01_msm", name)) as f:
             return json.load(f).get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -265,7 +268,9 @@ def main():
             "verify_commit_note": "types.VerifyCommit (C1: 150 validators) via tmv_verify_commit, host-resident commit",
             "roofline": {"bound": "valu-int-mul", "achieved": round(achieved / 1e12, 4),
                          "peak": round(peak / 1e12, 4), "unit": "Tmul/s", "frac": round(achieved / peak, 4),
-                         "traffic": _load_traffic(),
+                         "traffic": _load_traffic(args.method) if K == 32 else None,
+                         "traffic_note": "HBM bytes per launch (PMC, profiles/r01_msm/pmc_*.json); algorithmic "
+                                         "input bytes per launch = 32 x 10k x ~222 B = 71 MB",
                          "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if args.method == "batch"
                                     else "k_prep + k_verify_quad"),
                          "launch_avg_ms": round(launch_ms, 4),

@@ -15,7 +15,7 @@ run() {
   case $rc in 124|137|134|139) echo "stopping after $name"; exit $rc;; esac
   return 0
 }
-B="python3 bench.py --no-cpu-baseline --steps 64 --warmup 16"
+B="python3 tools/pmc_driver.py --launches 4"
 run trace rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py
 run fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- $B
 run write rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- $B
