@@ -185,6 +185,9 @@ int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
 // the batch check does 2-3x less work.  Flags override per call.
 uint32_t g_msm_min = 16384;
 uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk length (A/B measurement)
+// Key-cached batches up to this size run as one fused latency kernel
+// (TMV_CACHED_FUSED_MAX; commit-sized calls such as VerifyCommit).
+uint32_t g_cached_fused_max = 4096;
 
 void read_env() {
   static std::once_flag once;
@@ -196,6 +199,8 @@ void read_env() {
     g_quad_max = t ? (uint32_t)strtoul(t, nullptr, 10) : 49152u;
     const char *mm = getenv("TMV_MSM_MIN");
     if (mm) g_msm_min = (uint32_t)strtoul(mm, nullptr, 10);
+    const char *cf = getenv("TMV_CACHED_FUSED_MAX");
+    if (cf) g_cached_fused_max = (uint32_t)strtoul(cf, nullptr, 10);
     const char *mc = getenv("TMV_MSM_CHUNK");
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
   });
@@ -643,7 +648,9 @@ static int launch_cached(Device &d, bool sr, const uint8_t *pk, const uint8_t *s
   Workspace *ws = reserve_work(d, n, false, s, &rc);
   if (!ws) return rc;
   tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
-  hipError_t e = tmv::launch_verify_cached(sr, pk, sig, msg, off, slots, n, d.kt, d.d_bcomb, d.d_prefix, w, out, s);
+  read_env();
+  hipError_t e = tmv::launch_verify_cached(sr, pk, sig, msg, off, slots, n, d.kt, d.d_bcomb, d.d_prefix, w, out,
+                                           g_cached_fused_max, s);
   if (e != hipSuccess) { set_error("cached verify launch", e); return TMV_ERR_LAUNCH; }
   (void)hipEventRecord(ws->done, s);
   return 0;

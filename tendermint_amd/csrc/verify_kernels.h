@@ -46,10 +46,12 @@ struct KeyTable {
 
 hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
                             hipStream_t stream);
+// fused_max: batches up to this size use the one-kernel latency form
+// (k_verify_cached_fused), larger ones k_prep_cached + k_verify_comb.
 hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                 const uint32_t *msg_off, const uint32_t *key_slot, uint32_t n, KeyTable kt,
                                 const fe *bcomb, const strobe_t *prefix, Ed25519Work w, uint8_t *out,
-                                hipStream_t stream);
+                                uint32_t fused_max, hipStream_t stream);
 
 hipError_t launch_sr25519_verify_quad(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                       const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,

@@ -498,6 +498,139 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
   if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
 }
 
+// Latency form of the key-cached path (small batches: VerifyCommit).  The
+// comb sum needs k but not R, so one workgroup of two waves covers 16
+// signatures: wave 0 hashes (lane 4q for signature q), recodes and runs the
+// 96 comb additions per quad while lanes 0..15 of wave 1 decode the R's; the
+// waves meet once, for the final check (R through LDS).  The critical path
+// is max(hash + comb, R decode) instead of their sum.
+template <bool SR>
+__global__ void __launch_bounds__(2 * kQuadBlock)
+k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
+                      const uint8_t *__restrict__ msg, const uint32_t *__restrict__ msg_off,
+                      const uint32_t *__restrict__ key_slot, uint32_t n, KeyTable kt, const fe *__restrict__ bcomb,
+                      const strobe_t *__restrict__ prefix, uint8_t *__restrict__ out, int aligned) {
+  __shared__ int8_t dig[kQuadSigs][2][64];
+  __shared__ fe Rs[kQuadSigs][4];
+  __shared__ uint8_t rok[kQuadSigs];
+  const uint32_t base = blockIdx.x * kQuadSigs;
+  if (base >= n) return;  // block-uniform
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave == 1) {
+    if (lane < kQuadSigs) {
+      const uint32_t i = min(base + lane, n - 1);
+      uint32_t r_w[8];
+      if (aligned) load_words_aligned(r_w, sig + 64ull * i);
+      else load_words_unaligned(r_w, sig + 64ull * i);
+      ge_p3 P;
+      const bool ok = SR ? ristretto_decode(P, r_w) : ge_decode_zip215(P, r_w);
+      if (!ok) ge_p3_identity(P);
+      rok[lane] = ok ? 1 : 0;
+      if (SR) {
+        Rs[lane][0] = P.X; Rs[lane][1] = P.Y;
+        fe t; fe_one(t); Rs[lane][2] = t;
+        Rs[lane][3] = P.T;
+      } else {  // CachedQ of R, negated by the final check
+        ge_cached cc;
+        ge_p3_to_cached(cc, P);
+        fe t;
+        fe_carry(t, cc.YmX); Rs[lane][0] = t;
+        fe_carry(t, cc.YpX); Rs[lane][1] = t;
+        Rs[lane][2] = cc.T2d;
+        Rs[lane][3] = cc.Z;
+      }
+    }
+    __syncthreads();
+    return;
+  }
+  const int c = lane & 3;
+  const int q = lane >> 2;
+  const uint32_t raw = base + q;
+  const bool live = raw < n;
+  const uint32_t i = live ? raw : n - 1;
+  uint32_t k_w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c == 0) {
+    uint32_t a_w[8], r_w[8];
+    if (aligned) {
+      load_words_aligned(a_w, pk + 32ull * i);
+      load_words_aligned(r_w, sig + 64ull * i);
+    } else {
+      load_words_unaligned(a_w, pk + 32ull * i);
+      load_words_unaligned(r_w, sig + 64ull * i);
+    }
+    const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
+    if (SR) {
+      sr25519_challenge(k_w, *prefix, a_w, r_w, msg + o0, o1 - o0);
+    } else {
+      uint32_t h[16];
+      sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
+      sc_reduce512(k_w, h);
+    }
+  }
+  uint32_t s_raw[8], s_w[8];
+  if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+  else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+  bool s_ok;
+  if (SR) {
+    s_ok = sr25519_decode_s(s_w, s_raw);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
+    s_ok = sc_is_canonical(s_w);
+  }
+  if (!s_ok) s_w[7] &= 0x0fffffffu;
+  if (c == 1) recode256_store(&dig[q][1][0], s_w);
+  else if (c == 0) recode16_store(&dig[q][0][0], k_w, true);
+  // the digits were written by other lanes of this wave: order the LDS
+  // stores before the loads without waiting for the decoding wave
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const uint32_t slot = key_slot[i];
+  const bool a_ok = kt.ok[slot] != 0;
+  const fe *krow = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
+  fe acc, r, idq;
+  quad::p3_identity(acc);
+  quad::cached_identity(idq);
+  auto entry_at = [&](int t, int &dsg) -> const fe * {
+    if (t < 64) {
+      dsg = dig[q][0][t];
+      const int a = dsg < 0 ? -dsg : dsg;
+      return krow + ((t * 8) + (a ? a - 1 : 0)) * 4 + c;
+    }
+    dsg = dig[q][1][t - 64];
+    const int a = dsg < 0 ? -dsg : dsg;
+    return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
+  };
+  int dnext;
+  fe nxt = *entry_at(0, dnext);
+  for (int t = 0; t < 96; t++) {
+    const int d = dnext;
+    fe ent = nxt;
+    if (t + 1 < 96) nxt = *entry_at(t + 1, dnext);
+    fe_cmov(ent, idq, d == 0);
+    quad::cached_cneg(ent, d < 0);
+    quad::add(r, acc, ent);
+    quad::p1p1_to_p3(acc, r);
+  }
+  __syncthreads();  // R decoded by wave 1
+  const bool r_ok = rok[q] != 0;
+  int status;
+  if (SR) {
+    const fe Rq = Rs[q][c];
+    const bool eq = quad::ristretto_equal(acc, Rq);
+    status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
+  } else {
+    fe Rq = Rs[q][c];
+    quad::cached_cneg(Rq, true);
+    quad::add(r, acc, Rq);
+    quad::p1p1_to_p3(acc, r);
+    status = (quad::is_identity_times8(acc) && s_ok && a_ok && r_ok) ? 1 : 0;
+  }
+  if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
+}
+
 hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
                             hipStream_t stream) {
   if (m == 0) return hipSuccess;
@@ -510,9 +643,17 @@ hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots,
 hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                 const uint32_t *msg_off, const uint32_t *key_slot, uint32_t n, KeyTable kt,
                                 const fe *bcomb, const strobe_t *prefix, Ed25519Work w, uint8_t *out,
-                                hipStream_t stream) {
+                                uint32_t fused_max, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  if (n <= fused_max) {  // latency-bound: one fused kernel
+    const uint32_t blocks = (n + kQuadSigs - 1) / kQuadSigs;
+    if (sr) hipLaunchKernelGGL(k_verify_cached_fused<true>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig, msg,
+                               msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+    else hipLaunchKernelGGL(k_verify_cached_fused<false>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig, msg,
+                            msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+    return hipGetLastError();
+  }
   const uint32_t pblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
   if (sr) hipLaunchKernelGGL(k_prep_cached<true>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
   else hipLaunchKernelGGL(k_prep_cached<false>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);

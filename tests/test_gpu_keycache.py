@@ -83,3 +83,32 @@ print("ok", s)
                          timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ok" in out.stdout
+
+
+def test_two_kernel_form_matches_oracle():
+    """Batches above TMV_CACHED_FUSED_MAX take k_prep_cached + k_verify_comb
+    instead of the fused latency kernel; both must give the oracle's vector."""
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, '.'); sys.path.insert(0, 'oracle')
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import make_c2_batch, make_sr25519_batch
+ctx = N.Context(1)
+b = make_c2_batch(1000, seed=35, edge_scale=6.0)
+_, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=4)
+for _ in range(2):
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st.astype(np.uint8), ref)
+s = make_sr25519_batch(600, seed=36, bad_frac=0.05)
+ref = C.sr25519_status_packed(s.pk, s.sig, s.msg, s.off, threads=4)
+ok, st = ctx.verify_batch_ex(N.TMV_KIND_SR25519, N.TMV_FLAG_KEY_CACHE, s.pk, s.sig, s.msg, s.off)
+assert np.array_equal(st, ref)
+print("ok")
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TMV_CACHED_FUSED_MAX="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ok" in out.stdout
