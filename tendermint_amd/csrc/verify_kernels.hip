@@ -419,8 +419,36 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
   }
 }
 
+// The 96 table additions of the key-cached path with kCombAhead entries in
+// flight: the tables live in HBM / the Infinity Cache (a key is 80 KB), so
+// one entry of prefetch left the loop waiting on memory latency.
+constexpr int kCombAhead = 8;
+
+template <class EntryAt>
+__device__ __forceinline__ void comb_accumulate(fe &acc, const fe &idq, EntryAt entry_at) {
+  // named registers, not an array, so the ring stays out of scratch
+  fe b0, b1, b2, b3, b4, b5, b6, b7;
+  int d0, d1, d2, d3, d4, d5, d6, d7;
+  b0 = *entry_at(0, d0); b1 = *entry_at(1, d1); b2 = *entry_at(2, d2); b3 = *entry_at(3, d3);
+  b4 = *entry_at(4, d4); b5 = *entry_at(5, d5); b6 = *entry_at(6, d6); b7 = *entry_at(7, d7);
+  fe r;
+  auto step = [&](fe &b, int &d, int next) {
+    fe ent = b;
+    const int dd = d;
+    if (next < 96) b = *entry_at(next, d);
+    fe_cmov(ent, idq, dd == 0);
+    quad::cached_cneg(ent, dd < 0);
+    quad::add(r, acc, ent);
+    quad::p1p1_to_p3(acc, r);
+  };
+  for (int t0 = 0; t0 < 96; t0 += kCombAhead) {
+    step(b0, d0, t0 + 8); step(b1, d1, t0 + 9); step(b2, d2, t0 + 10); step(b3, d3, t0 + 11);
+    step(b4, d4, t0 + 12); step(b5, d5, t0 + 13); step(b6, d6, t0 + 14); step(b7, d7, t0 + 15);
+  }
+}
+
 // acc = sum_i e_i(k) 16^i(-A) [key comb] + sum_j d_j(s) 256^j B [base comb];
-// no doublings.  Table entries are prefetched one addition ahead.
+// no doublings.  Table entries are prefetched kCombAhead additions ahead.
 template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_slot, uint32_t n, Ed25519Work w,
@@ -472,17 +500,7 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
     const int a = dsg < 0 ? -dsg : dsg;
     return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
   };
-  int dnext;
-  fe nxt = *entry_at(0, dnext);
-  for (int t = 0; t < 96; t++) {
-    const int d = dnext;
-    fe ent = nxt;
-    if (t + 1 < 96) nxt = *entry_at(t + 1, dnext);
-    fe_cmov(ent, idq, d == 0);
-    quad::cached_cneg(ent, d < 0);
-    quad::add(r, acc, ent);
-    quad::p1p1_to_p3(acc, r);
-  }
+  comb_accumulate(acc, idq, entry_at);
   int status;
   if (SR) {
     const fe Rq = w.Rc[4ull * i + c];
@@ -603,17 +621,7 @@ k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict_
     const int a = dsg < 0 ? -dsg : dsg;
     return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
   };
-  int dnext;
-  fe nxt = *entry_at(0, dnext);
-  for (int t = 0; t < 96; t++) {
-    const int d = dnext;
-    fe ent = nxt;
-    if (t + 1 < 96) nxt = *entry_at(t + 1, dnext);
-    fe_cmov(ent, idq, d == 0);
-    quad::cached_cneg(ent, d < 0);
-    quad::add(r, acc, ent);
-    quad::p1p1_to_p3(acc, r);
-  }
+  comb_accumulate(acc, idq, entry_at);
   __syncthreads();  // R decoded by wave 1
   const bool r_ok = rok[q] != 0;
   int status;
