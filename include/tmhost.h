@@ -88,6 +88,13 @@ size_t tmv_vote_sign_bytes(const char *chain_id, int32_t vote_type, int64_t heig
                            const tmv_block_id *block_id, int64_t ts_seconds, int32_t ts_nanos, uint8_t *out,
                            size_t cap);
 
+/* The vote template of tmv_verify_votes (tmverify.h) for (chain_id, type,
+ * height, round, block_id or NULL for nil): the three segments are written
+ * back to back into out (head, then block, then chain) and their lengths
+ * into lens[3].  Returns the total length; writes min(total, cap) bytes. */
+size_t tmv_vote_template_encode(const char *chain_id, int32_t vote_type, int64_t height, int32_t round,
+                                const tmv_block_id *block_id, uint8_t *out, size_t cap, uint32_t lens[3]);
+
 #define TMV_COMMIT_FULL 0           /* types.VerifyCommit */
 #define TMV_COMMIT_LIGHT 1          /* types.VerifyCommitLight */
 #define TMV_COMMIT_LIGHT_TRUSTING 2 /* types.VerifyCommitLightTrusting */

@@ -175,6 +175,48 @@ typedef struct tmv_batch_ref {
 int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32_t flags,
                               const tmv_batch_ref *batches, uint32_t n_batches, void *stream);
 
+/* ---- Device-side vote sign-bytes ----
+ * The canonical votes of one commit differ only in the timestamp and in
+ * whether field 4 (the BlockID) is present: Commit.VoteSignBytes,
+ * types/block.go:836-862, over CanonicalizeVote, types/canonical.go:52-63.
+ * The caller encodes the shared fields once per (commit, chain_id) -- a
+ * template, see tmv_vote_template_encode in tmhost.h -- and sends 16 bytes
+ * per vote instead of the ~120-byte message; the device writes
+ *   uvarint(len(body)) || head || [block] || 0x2a uvarint(len(ts)) ts || chain
+ * into HBM, where ts = [0x08 uvarint(seconds)] [0x10 uvarint(nanos)] (proto3:
+ * zero fields omitted), byte-identical to types.VoteSignBytes. */
+typedef struct tmv_vote_template {
+  const uint8_t *head;  /* fields 1-3 (type, height, round) */
+  uint32_t head_len;
+  const uint8_t *block; /* field 4, the commit's BlockID (empty when nil) */
+  uint32_t block_len;
+  const uint8_t *chain; /* field 6, chain_id (empty when "") */
+  uint32_t chain_len;
+} tmv_vote_template;
+
+#define TMV_VOTE_WITH_BLOCK 0x80000000u /* tmpl bit: BlockIDFlagCommit, field 4 included */
+
+typedef struct tmv_vote {
+  int64_t ts_seconds;
+  int32_t ts_nanos;
+  uint32_t tmpl; /* template index | TMV_VOTE_WITH_BLOCK */
+} tmv_vote;
+
+/* tmv_verify_batch_ex over device-built sign-bytes: entry i signs the
+ * message of votes[i].  Same flags, statuses and return values as
+ * tmv_verify_batch_ex (TMV_ERR_ARG for a template index >= n_tmpl). */
+int tmv_verify_votes(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const tmv_vote_template *tmpl,
+                     uint32_t n_tmpl, const tmv_vote *votes, const uint8_t *pk, const uint8_t *sig, uint32_t n,
+                     int8_t *status_out);
+
+/* The messages the device builds for tmv_verify_votes, copied back (tests,
+ * tools).  msg_off_out gets n + 1 offsets; msg_out (capacity msg_cap) the
+ * concatenated messages, or is skipped when NULL.  Returns the total length,
+ * or < 0 (TMV_ERR_ARG if msg_cap is too small). */
+int64_t tmv_vote_sign_bytes_device(tmv_ctx *ctx, const tmv_vote_template *tmpl, uint32_t n_tmpl,
+                                   const tmv_vote *votes, uint32_t n, uint8_t *msg_out, size_t msg_cap,
+                                   uint32_t *msg_off_out);
+
 #ifdef __cplusplus
 }
 #endif

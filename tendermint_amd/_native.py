@@ -32,6 +32,10 @@ TMV_FLAG_BATCH_EQUATION = 2
 TMV_FLAG_PER_ENTRY = 4
 TMV_BATCHOPT_STATS = 1
 TMV_KIND_MIXED = 2
+TMV_VOTE_WITH_BLOCK = 0x80000000
+
+# tmv_vote (include/tmverify.h), 16 bytes
+VOTE_DTYPE = np.dtype([("ts_seconds", "<i8"), ("ts_nanos", "<i4"), ("tmpl", "<u4")])
 
 # Every symbol include/tmverify.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
@@ -40,9 +44,10 @@ EXPORTS = [
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
     "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
     "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
+    "tmv_verify_votes", "tmv_vote_sign_bytes_device",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
-    "tmv_vote_sign_bytes", "tmv_verify_commit", "tmv_verify_commits",
+    "tmv_vote_sign_bytes", "tmv_vote_template_encode", "tmv_verify_commit", "tmv_verify_commits",
 ]
 
 
@@ -51,6 +56,26 @@ class BatchRef(ctypes.Structure):
     _fields_ = [("pk", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("msg", ctypes.c_void_p),
                 ("msg_off", ctypes.c_void_p), ("n", ctypes.c_uint32), ("msg_bytes", ctypes.c_uint32),
                 ("status", ctypes.c_void_p)]
+
+
+class VoteTemplate(ctypes.Structure):
+    """tmv_vote_template (include/tmverify.h): the shared segments of a commit's votes."""
+    _fields_ = [("head", ctypes.c_void_p), ("head_len", ctypes.c_uint32), ("block", ctypes.c_void_p),
+                ("block_len", ctypes.c_uint32), ("chain", ctypes.c_void_p), ("chain_len", ctypes.c_uint32)]
+
+
+def vote_templates(segments):
+    """[(head, block, chain) bytes] -> (ctypes array of VoteTemplate, keep-alive buffers)."""
+    keep = []
+    arr = (VoteTemplate * max(1, len(segments)))()
+    for t, segs in enumerate(segments):
+        ptrs = []
+        for b in segs:
+            buf = ctypes.create_string_buffer(bytes(b), max(1, len(b)))
+            keep.append(buf)
+            ptrs.append((ctypes.cast(buf, ctypes.c_void_p), len(b)))
+        arr[t] = VoteTemplate(ptrs[0][0], ptrs[0][1], ptrs[1][0], ptrs[1][1], ptrs[2][0], ptrs[2][1])
+    return arr, keep
 
 
 class NativeError(RuntimeError):
@@ -102,6 +127,11 @@ def lib() -> ctypes.CDLL:
                                                  vp, ctypes.c_uint32, vp, vp]
         L.tmv_verify_batches_device.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32,
                                                 ctypes.POINTER(BatchRef), ctypes.c_uint32, vp]
+        L.tmv_verify_votes.argtypes = [vp, ctypes.c_uint8, ctypes.c_uint32, ctypes.POINTER(VoteTemplate),
+                                       ctypes.c_uint32, vp, u8p, u8p, ctypes.c_uint32, i8p]
+        L.tmv_vote_sign_bytes_device.restype = ctypes.c_int64
+        L.tmv_vote_sign_bytes_device.argtypes = [vp, ctypes.POINTER(VoteTemplate), ctypes.c_uint32, vp,
+                                                 ctypes.c_uint32, u8p, ctypes.c_size_t, u32p]
         L.tmv_ed25519_verify_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         L.tmv_verify_mixed_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         _lib = L
@@ -202,6 +232,35 @@ class Context:
                                                        _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
                          "tmv_verify_batch_ex")
         return rc == TMV_ALL_VALID, out[:n]
+
+    def verify_votes(self, key_kind: int, flags: int, templates, votes, pk, sig):
+        """tmv_verify_votes: templates = [(head, block, chain)], votes = VOTE_DTYPE array."""
+        votes = np.ascontiguousarray(votes, VOTE_DTYPE)
+        n = len(votes)
+        arr, keep = vote_templates(templates)
+        out = np.zeros(max(n, 1), np.int8)
+        pk = pk if len(pk) else np.zeros(1, np.uint8)
+        sig = sig if len(sig) else np.zeros(1, np.uint8)
+        rc = self._check(self._lib.tmv_verify_votes(self._h, key_kind, flags, arr, len(templates),
+                                                    votes.ctypes.data if n else None, _p(pk), _p(sig), n,
+                                                    _p(out, ctypes.c_int8)), "tmv_verify_votes")
+        del keep
+        return rc == TMV_ALL_VALID, out[:n]
+
+    def vote_sign_bytes_device(self, templates, votes):
+        """The messages k_vote_signbytes writes for (templates, votes): (msg bytes, offsets)."""
+        votes = np.ascontiguousarray(votes, VOTE_DTYPE)
+        n = len(votes)
+        arr, keep = vote_templates(templates)
+        off = np.zeros(n + 1, np.uint32)
+        vp = votes.ctypes.data if n else None
+        total = self._check(self._lib.tmv_vote_sign_bytes_device(self._h, arr, len(templates), vp, n, None, 0,
+                                                                 _p(off, ctypes.c_uint32)), "tmv_vote_sign_bytes_device")
+        msg = np.zeros(max(total, 1), np.uint8)
+        self._check(self._lib.tmv_vote_sign_bytes_device(self._h, arr, len(templates), vp, n, _p(msg), len(msg),
+                                                         _p(off, ctypes.c_uint32)), "tmv_vote_sign_bytes_device")
+        del keep
+        return msg[:total].tobytes(), off
 
     def verify_mixed_batch_ex(self, flags: int, kind, pk, sig, msg, off):
         n = len(off) - 1

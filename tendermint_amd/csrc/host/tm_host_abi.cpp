@@ -174,6 +174,21 @@ size_t tmv_vote_sign_bytes(const char *chain_id, int32_t vote_type, int64_t heig
   return sb.size();
 }
 
+size_t tmv_vote_template_encode(const char *chain_id, int32_t vote_type, int64_t height, int32_t round,
+                                const tmv_block_id *block_id, uint8_t *out, size_t cap, uint32_t lens[3]) {
+  tmh::BlockID bid;
+  if (block_id) bid = block_id_of(*block_id);
+  const tmh::VoteTemplate t =
+      tmh::EncodeVoteTemplate(chain_id ? chain_id : "", vote_type, height, round, block_id ? &bid : nullptr);
+  if (lens) {
+    lens[0] = t.head_len;
+    lens[1] = t.block_len;
+    lens[2] = t.chain_len;
+  }
+  if (out) std::memcpy(out, t.bytes.data(), std::min(cap, t.bytes.size()));
+  return t.bytes.size();
+}
+
 }  // extern "C"
 
 namespace {
@@ -202,51 +217,122 @@ void parallel_for(size_t n, size_t min_per_thread, F fn) {
 }
 
 // Signature backend over the device: entries split by key kind, each kind one
-// tmv_verify_batch_ex call with the key cache (validator keys repeat).  The
-// packed arrays are filled in parallel from precomputed offsets.
+// tmv_verify_votes call with the key cache (validator keys repeat).  The
+// sign-bytes are built on the device from one template per (commit,
+// chain_id) plus 16 bytes per vote; public keys and signatures are packed in
+// parallel.
 // Packing buffers reused across calls on a thread: fresh multi-megabyte
 // vectors would be new mappings, page-faulted in on every call.
 struct PackBuffers {
   std::vector<uint32_t> idx, off;
   std::vector<uint8_t> pk, sig, msg;
+  std::vector<tmv_vote> votes;
   std::vector<int8_t> out;
 };
+
+// Entry e of plan pl.
+struct VoteRef {
+  const tmh::CommitPlan *pl;
+  uint32_t e;
+  const tmh::SigEntry &entry() const { return pl->entries[e]; }
+};
+
+// Batches below this size send host-encoded messages (one launch less on
+// the latency path, e.g. a single VerifyCommit); larger ones build the
+// sign-bytes on the device.  TMV_DEVICE_SIGNBYTES_MIN overrides.
+static uint32_t device_signbytes_min() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("TMV_DEVICE_SIGNBYTES_MIN");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 4096u;
+  }();
+  return v;
+}
 
 struct GpuBackend {
   tmv_ctx *ctx;
   int infra = 0;
-  void operator()(const std::vector<const tmh::SigEntry *> &es, std::vector<int8_t> &st) {
+  void operator()(const std::vector<VoteRef> &es, std::vector<int8_t> &st) {
     static thread_local PackBuffers tls;
     PackBuffers &pb = tls;  // the workers below must use this thread's buffers, not their own
     st.assign(es.size(), 0);
+    // one template per (commit object, chain_id)
+    std::vector<tmh::VoteTemplate> tmpls;
+    std::unordered_map<const tmh::CommitPlan *, uint32_t> plan_tmpl;
+    std::unordered_map<const tmh::Commit *, std::vector<std::pair<const std::string *, uint32_t>>> by_commit;
+    std::vector<uint32_t> ent_tmpl(es.size());
+    for (size_t i = 0; i < es.size(); i++) {
+      const tmh::CommitPlan *pl = es[i].pl;
+      auto [it, fresh] = plan_tmpl.emplace(pl, 0);
+      if (fresh) {
+        auto &chains = by_commit[pl->commit];
+        uint32_t t = UINT32_MAX;
+        for (auto &c : chains)
+          if (*c.first == pl->chain_id) t = c.second;
+        if (t == UINT32_MAX) {
+          t = (uint32_t)tmpls.size();
+          const tmh::Commit &cm = *pl->commit;
+          tmpls.push_back(tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round,
+                                                  &cm.block_id));
+          chains.emplace_back(&pl->chain_id, t);
+        }
+        it->second = t;
+      }
+      ent_tmpl[i] = it->second;
+    }
+    std::vector<tmv_vote_template> tv(tmpls.size());
+    for (size_t t = 0; t < tmpls.size(); t++) {
+      const tmh::VoteTemplate &vt = tmpls[t];
+      const uint8_t *b = vt.bytes.data();
+      tv[t] = tmv_vote_template{b, vt.head_len, b + vt.head_len, vt.block_len, b + vt.head_len + vt.block_len,
+                                vt.chain_len};
+    }
     for (int kind = 0; kind < 2; kind++) {
       const tmh::KeyType kt = kind == 0 ? tmh::KeyType::Ed25519 : tmh::KeyType::Sr25519;
       pb.idx.clear();
-      pb.off.assign(1, 0);
       for (size_t i = 0; i < es.size(); i++) {
-        const tmh::SigEntry &e = *es[i];
+        const tmh::SigEntry &e = es[i].entry();
         if (e.kind != kt) continue;
         if (e.pk->size() != 32 || e.sig_len != 64) continue;  // VerifySignature: false
         pb.idx.push_back((uint32_t)i);
-        pb.off.push_back(pb.off.back() + e.msg_len);
       }
       if (pb.idx.empty()) continue;
       const size_t m = pb.idx.size();
       pb.pk.resize(32 * m);
       pb.sig.resize(64 * m);
-      pb.msg.resize(std::max<uint32_t>(1, pb.off.back()));
+      pb.votes.resize(m);
       pb.out.resize(m);
       parallel_for((m + 1023) / 1024, 1, [&](size_t c) {
         for (size_t t = c * 1024; t < std::min(m, c * 1024 + 1024); t++) {
-          const tmh::SigEntry &e = *es[pb.idx[t]];
+          const VoteRef &r = es[pb.idx[t]];
+          const tmh::SigEntry &e = r.entry();
+          const tmh::CommitSig &cs = r.pl->commit->signatures[(size_t)r.pl->sig_idx[r.e]];
           std::memcpy(&pb.pk[32 * t], e.pk->data(), 32);
           std::memcpy(&pb.sig[64 * t], e.sig, 64);
-          if (e.msg_len) std::memcpy(&pb.msg[pb.off[t]], e.msg, e.msg_len);
+          pb.votes[t] = tmv_vote{cs.timestamp.seconds, cs.timestamp.nanos,
+                                 ent_tmpl[pb.idx[t]] |
+                                     (cs.block_id_flag == tmh::BlockIDFlagCommit ? TMV_VOTE_WITH_BLOCK : 0u)};
         }
       });
-      const int rc = tmv_verify_batch_ex(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE,
-                                         pb.pk.data(), pb.sig.data(), pb.msg.data(), pb.off.data(), (uint32_t)m,
-                                         pb.out.data());
+      int rc;
+      if (m >= device_signbytes_min()) {
+        rc = tmv_verify_votes(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE, tv.data(),
+                              (uint32_t)tv.size(), pb.votes.data(), pb.pk.data(), pb.sig.data(), (uint32_t)m,
+                              pb.out.data());
+      } else {  // host-encoded messages, same templates
+        pb.off.assign(1, 0);
+        pb.msg.clear();
+        for (size_t t = 0; t < m; t++) {
+          const tmv_vote &v = pb.votes[t];
+          const tmh::VoteTemplate &vt = tmpls[v.tmpl & ~TMV_VOTE_WITH_BLOCK];
+          tmh::AppendVoteFromTemplate(pb.msg, vt, (v.tmpl & TMV_VOTE_WITH_BLOCK) != 0,
+                                      tmh::Timestamp{v.ts_seconds, v.ts_nanos});
+          pb.off.push_back((uint32_t)pb.msg.size());
+        }
+        if (pb.msg.empty()) pb.msg.push_back(0);
+        rc = tmv_verify_batch_ex(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE,
+                                 pb.pk.data(), pb.sig.data(), pb.msg.data(), pb.off.data(), (uint32_t)m,
+                                 pb.out.data());
+      }
       if (rc < 0) { infra = rc; continue; }
       for (size_t t = 0; t < m; t++) st[pb.idx[t]] = pb.out[t];
     }
@@ -354,9 +440,10 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
   });
   tm.mark("plan");
   // dedupe identical entries across plans: same commit object and signature
-  // index, same public key object, same verifier kind and the same message
-  // (one slot per (commit, index, kind) instead of a hash map)
-  std::vector<const tmh::SigEntry *> uniq;
+  // index, same public key object, same verifier kind and the same chain_id
+  // (hence the same message; one slot per (commit, index, kind) instead of a
+  // hash map)
+  std::vector<VoteRef> uniq;
   std::vector<std::vector<uint32_t>> where(n_jobs);
   const bool dedup = n_jobs > 1;
   std::vector<std::vector<uint32_t>> slot(dedup ? 2 * commits.size() : 0);
@@ -373,14 +460,14 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
       const tmh::SigEntry &en = pl.entries[e];
       if (sl) {
         uint32_t &u = (*sl)[(size_t)pl.sig_idx[e]];
-        if (u != UINT32_MAX && uniq[u]->pk == en.pk && uniq[u]->same_message(en)) {
+        if (u != UINT32_MAX && uniq[u].entry().pk == en.pk && uniq[u].pl->chain_id == pl.chain_id) {
           where[j][e] = u;
           continue;
         }
         u = (uint32_t)uniq.size();
       }
       where[j][e] = (uint32_t)uniq.size();
-      uniq.push_back(&en);
+      uniq.push_back(VoteRef{&pl, (uint32_t)e});
     }
   }
   tm.mark("dedup");

@@ -197,57 +197,121 @@ inline uint8_t *PutBytesField(uint8_t *p, uint8_t tag, const Bytes &b) {
 // types.VoteSignBytes: MarshalDelimited(CanonicalizeVote(chainID, vote)),
 // field by field as gogoproto emits CanonicalVote (proto3: zero fields
 // omitted; the timestamp is always present).  block_id == nullptr or a nil
-// BlockID omits field 4 (types/canonical.go:18-32).  Sizes are computed first
-// and the message is written in one pass into one buffer.
-// Appends the encoding to `out` (no allocation when `out` has capacity).
-inline void AppendVoteSignBytes(Bytes &out, const std::string &chain_id, int32_t type, int64_t height,
-                                int32_t round, const BlockID *block_id, const Timestamp &ts) {
-  const bool has_bid = block_id && !block_id->IsNil();
-  size_t psh_len = 0, cb_len = 0;
-  if (has_bid) {
-    const PartSetHeader &ph = block_id->part_set_header;
-    if (ph.total != 0) psh_len += 1 + UvarintLen(ph.total);
-    if (!ph.hash.empty()) psh_len += 1 + UvarintLen(ph.hash.size()) + ph.hash.size();
-    if (!block_id->hash.empty()) cb_len += 1 + UvarintLen(block_id->hash.size()) + block_id->hash.size();
-    cb_len += 1 + UvarintLen(psh_len) + psh_len;
-  }
-  size_t t_len = 0;
-  if (ts.seconds != 0) t_len += 1 + UvarintLen((uint64_t)ts.seconds);
-  if (ts.nanos != 0) t_len += 1 + UvarintLen((uint64_t)(int64_t)ts.nanos);
-  size_t body = 0;
-  if (type != 0) body += 1 + UvarintLen((uint64_t)(uint32_t)type);
-  if (height != 0) body += 9;
-  if (round != 0) body += 9;
-  if (has_bid) body += 1 + UvarintLen(cb_len) + cb_len;
-  body += 1 + UvarintLen(t_len) + t_len;
-  if (!chain_id.empty()) body += 1 + UvarintLen(chain_id.size()) + chain_id.size();
-
-  const size_t at = out.size();
-  out.resize(at + UvarintLen(body) + body);
-  uint8_t *p = PutUvarintP(out.data() + at, body);
+// BlockID omits field 4 (types/canonical.go:18-32).  The message is split
+// into the parts shared by a commit's votes -- fields 1-3 (head), field 4
+// (block) and field 6 (chain) -- and the per-vote timestamp field 5, so that
+// the host encoder and the device one (tmv_verify_votes) assemble the same
+// pieces: uvarint(len(body)) || head || [block] || ts field || chain.
+inline size_t VoteHeadLen(int32_t type, int64_t height, int32_t round) {
+  return (type != 0 ? 1 + UvarintLen((uint64_t)(uint32_t)type) : 0) + (height != 0 ? 9 : 0) + (round != 0 ? 9 : 0);
+}
+inline uint8_t *PutVoteHead(uint8_t *p, int32_t type, int64_t height, int32_t round) {
   if (type != 0) { *p++ = 0x08; p = PutUvarintP(p, (uint64_t)(uint32_t)type); }
   if (height != 0) { *p++ = 0x11; p = PutFixed64P(p, height); }
   if (round != 0) { *p++ = 0x19; p = PutFixed64P(p, (int64_t)round); }
-  if (has_bid) {
-    const PartSetHeader &ph = block_id->part_set_header;
-    *p++ = 0x22;
-    p = PutUvarintP(p, cb_len);
-    if (!block_id->hash.empty()) p = PutBytesField(p, 0x0a, block_id->hash);
-    *p++ = 0x12;
-    p = PutUvarintP(p, psh_len);
-    if (ph.total != 0) { *p++ = 0x08; p = PutUvarintP(p, ph.total); }
-    if (!ph.hash.empty()) p = PutBytesField(p, 0x12, ph.hash);
-  }
+  return p;
+}
+// field 4 (CanonicalBlockID), empty for a nil BlockID
+inline size_t VoteBlockLen(const BlockID *block_id, size_t *psh_len_out = nullptr, size_t *cb_len_out = nullptr) {
+  if (!block_id || block_id->IsNil()) return 0;
+  const PartSetHeader &ph = block_id->part_set_header;
+  size_t psh_len = 0, cb_len = 0;
+  if (ph.total != 0) psh_len += 1 + UvarintLen(ph.total);
+  if (!ph.hash.empty()) psh_len += 1 + UvarintLen(ph.hash.size()) + ph.hash.size();
+  if (!block_id->hash.empty()) cb_len += 1 + UvarintLen(block_id->hash.size()) + block_id->hash.size();
+  cb_len += 1 + UvarintLen(psh_len) + psh_len;
+  if (psh_len_out) *psh_len_out = psh_len;
+  if (cb_len_out) *cb_len_out = cb_len;
+  return 1 + UvarintLen(cb_len) + cb_len;
+}
+inline uint8_t *PutVoteBlock(uint8_t *p, const BlockID *block_id) {
+  size_t psh_len = 0, cb_len = 0;
+  if (VoteBlockLen(block_id, &psh_len, &cb_len) == 0) return p;
+  const PartSetHeader &ph = block_id->part_set_header;
+  *p++ = 0x22;
+  p = PutUvarintP(p, cb_len);
+  if (!block_id->hash.empty()) p = PutBytesField(p, 0x0a, block_id->hash);
+  *p++ = 0x12;
+  p = PutUvarintP(p, psh_len);
+  if (ph.total != 0) { *p++ = 0x08; p = PutUvarintP(p, ph.total); }
+  if (!ph.hash.empty()) p = PutBytesField(p, 0x12, ph.hash);
+  return p;
+}
+inline size_t VoteChainLen(const std::string &chain_id) {
+  return chain_id.empty() ? 0 : 1 + UvarintLen(chain_id.size()) + chain_id.size();
+}
+inline uint8_t *PutVoteChain(uint8_t *p, const std::string &chain_id) {
+  if (chain_id.empty()) return p;
+  *p++ = 0x32;
+  p = PutUvarintP(p, chain_id.size());
+  std::memcpy(p, chain_id.data(), chain_id.size());
+  return p + chain_id.size();
+}
+// field 5 (google.protobuf.Timestamp, always present)
+inline size_t VoteTimestampInner(const Timestamp &ts) {
+  return (ts.seconds != 0 ? 1 + UvarintLen((uint64_t)ts.seconds) : 0) +
+         (ts.nanos != 0 ? 1 + UvarintLen((uint64_t)(int64_t)ts.nanos) : 0);
+}
+inline size_t VoteTimestampLen(const Timestamp &ts) {
+  const size_t t = VoteTimestampInner(ts);
+  return 1 + UvarintLen(t) + t;
+}
+inline uint8_t *PutVoteTimestamp(uint8_t *p, const Timestamp &ts) {
   *p++ = 0x2a;
-  p = PutUvarintP(p, t_len);
+  p = PutUvarintP(p, VoteTimestampInner(ts));
   if (ts.seconds != 0) { *p++ = 0x08; p = PutUvarintP(p, (uint64_t)ts.seconds); }
   if (ts.nanos != 0) { *p++ = 0x10; p = PutUvarintP(p, (uint64_t)(int64_t)ts.nanos); }
-  if (!chain_id.empty()) {
-    *p++ = 0x32;
-    p = PutUvarintP(p, chain_id.size());
-    std::memcpy(p, chain_id.data(), chain_id.size());
-    p += chain_id.size();
+  return p;
+}
+
+// Appends the encoding to `out` (no allocation when `out` has capacity).
+inline void AppendVoteSignBytes(Bytes &out, const std::string &chain_id, int32_t type, int64_t height,
+                                int32_t round, const BlockID *block_id, const Timestamp &ts) {
+  const size_t body = VoteHeadLen(type, height, round) + VoteBlockLen(block_id) + VoteTimestampLen(ts) +
+                      VoteChainLen(chain_id);
+  const size_t at = out.size();
+  out.resize(at + UvarintLen(body) + body);
+  uint8_t *p = PutUvarintP(out.data() + at, body);
+  p = PutVoteHead(p, type, height, round);
+  p = PutVoteBlock(p, block_id);
+  p = PutVoteTimestamp(p, ts);
+  PutVoteChain(p, chain_id);
+}
+
+// The three shared segments of tmv_verify_votes' template, back to back.
+struct VoteTemplate {
+  Bytes bytes;
+  uint32_t head_len = 0, block_len = 0, chain_len = 0;
+};
+inline VoteTemplate EncodeVoteTemplate(const std::string &chain_id, int32_t type, int64_t height, int32_t round,
+                                       const BlockID *block_id) {
+  VoteTemplate t;
+  t.head_len = (uint32_t)VoteHeadLen(type, height, round);
+  t.block_len = (uint32_t)VoteBlockLen(block_id);
+  t.chain_len = (uint32_t)VoteChainLen(chain_id);
+  t.bytes.resize((size_t)t.head_len + t.block_len + t.chain_len);
+  uint8_t *p = PutVoteHead(t.bytes.data(), type, height, round);
+  p = PutVoteBlock(p, block_id);
+  PutVoteChain(p, chain_id);
+  return t;
+}
+
+// One vote's sign-bytes from its commit's template (the host twin of
+// k_vote_signbytes).
+inline void AppendVoteFromTemplate(Bytes &out, const VoteTemplate &t, bool with_block, const Timestamp &ts) {
+  const size_t body = (size_t)t.head_len + (with_block ? t.block_len : 0) + VoteTimestampLen(ts) + t.chain_len;
+  const size_t at = out.size();
+  out.resize(at + UvarintLen(body) + body);
+  uint8_t *p = PutUvarintP(out.data() + at, body);
+  const uint8_t *b = t.bytes.data();
+  std::memcpy(p, b, t.head_len);
+  p += t.head_len;
+  if (with_block && t.block_len) {
+    std::memcpy(p, b + t.head_len, t.block_len);
+    p += t.block_len;
   }
+  p = PutVoteTimestamp(p, ts);
+  if (t.chain_len) std::memcpy(p, b + t.head_len + t.block_len, t.chain_len);
 }
 
 inline Bytes VoteSignBytes(const std::string &chain_id, int32_t type, int64_t height, int32_t round,
@@ -415,20 +479,16 @@ constexpr int kBatchVerifyThreshold = 2;  // types/validation.go:12
 
 // One signature to verify: status 1 valid, 0 invalid, -1 / -2 device-found
 // sr25519 Add errors (public key / signature encoding).
-// A view: the message lives in the plan's sign-bytes arena, the signature in
-// the commit (both outlive the backend call).
+// A view into the validator set and the commit (both outlive the check).
+// The message is not materialised on the host: it is the commit's vote
+// sign-bytes for the plan's chain_id at pl.sig_idx[i], built on the device
+// from the commit's template (tmv_verify_votes).
 struct SigEntry {
   KeyType kind;
   const Bytes *pk;
-  const uint8_t *msg;
-  uint32_t msg_len;
   uint32_t sig_len;
   const uint8_t *sig;
-  bool same_message(const SigEntry &o) const {
-    return msg_len == o.msg_len && (msg_len == 0 || std::memcmp(msg, o.msg, msg_len) == 0);
-  }
 };
-using SigBackend = std::function<std::vector<int8_t>(const std::vector<SigEntry> &)>;
 
 // A commit check up to the point where signature results are needed.
 // Plan (loop of verifyCommitBatch / verifyCommitSingle) -> the backend
@@ -439,16 +499,14 @@ struct CommitPlan {
   bool defer_add = false;            // sr25519 batch: device statuses -1/-2 are Add errors
   int64_t tallied = 0, needed = 0;
   std::vector<SigEntry> entries;     // in Add order
-  Bytes msg_arena;                   // sign-bytes of the entries, back to back
   std::vector<int> sig_idx;          // commit.Signatures index of each entry
   std::vector<std::string> deferred_sig;
   std::vector<uint8_t> crosses;      // single: this entry crosses the threshold (early ok)
   const Commit *commit = nullptr;
+  std::string chain_id;              // the messages are this commit's votes on chain_id
 };
 
 struct CommitVerifier {
-  SigBackend backend;
-
   static bool ShouldBatchVerify(const ValidatorSet &vals, const Commit &commit) {
     const Validator *p = vals.GetProposer();
     return commit.signatures.size() >= (size_t)kBatchVerifyThreshold && p && SupportsBatchVerifier(p->pub_key);
@@ -471,8 +529,6 @@ struct CommitVerifier {
       pl.defer_add = bkind == KeyType::Sr25519;
     }
     std::unordered_map<int32_t, int> seen;
-    std::vector<uint32_t> msg_at;
-    pl.msg_arena.reserve(commit.signatures.size() * 128);
     pl.entries.reserve(commit.signatures.size());
     for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
       const CommitSig &cs = commit.signatures[idx];
@@ -492,7 +548,7 @@ struct CommitVerifier {
         seen[vi] = (int)idx;
         val = v;
       }
-      SigEntry e{val->pub_key.type, &val->pub_key.bytes, nullptr, 0, 0, nullptr};
+      SigEntry e{val->pub_key.type, &val->pub_key.bytes, 0, nullptr};
       if (pl.batch) {
         AddCheck ac = CheckAdd(bkind, val->pub_key, cs.signature);
         if (ac.sync) {  // bv.Add error, returned verbatim (:211-213)
@@ -506,9 +562,6 @@ struct CommitVerifier {
         e.sig = cs.signature.data();
         e.sig_len = (uint32_t)cs.signature.size();
       }
-      msg_at.push_back((uint32_t)pl.msg_arena.size());
-      commit.AppendVoteSignBytes(pl.msg_arena, chain_id, (int32_t)idx);
-      e.msg_len = (uint32_t)(pl.msg_arena.size() - msg_at.back());
       pl.entries.push_back(e);
       pl.sig_idx.push_back((int)idx);
       if (count(cs)) pl.tallied += val->voting_power;
@@ -516,8 +569,6 @@ struct CommitVerifier {
       pl.crosses.push_back(cross ? 1 : 0);
       if (cross) break;
     }
-    // the arena no longer grows: point the entries at their messages
-    for (size_t i = 0; i < pl.entries.size(); i++) pl.entries[i].msg = pl.msg_arena.data() + msg_at[i];
   }
 
   // Signature results -> the reference's return value.
@@ -576,6 +627,7 @@ struct CommitVerifier {
                          int64_t height, const Commit *commit, int64_t num, int64_t den) {
     CommitPlan pl;
     pl.commit = commit;
+    pl.chain_id = chain_id;
     if (mode == kLightTrusting) {
       if (!vals) { pl.early = std::string("nil validator set"); return pl; }
       if (den == 0) { pl.early = std::string("trustLevel has zero Denominator"); return pl; }
@@ -597,43 +649,6 @@ struct CommitVerifier {
     if (mode == kFull) PlanLoop(pl, chain_id, *vals, *commit, IgnoreAbsent, CountCommit, true, true);
     else PlanLoop(pl, chain_id, *vals, *commit, IgnoreNotCommit, CountAll, false, true);
     return pl;
-  }
-
-  // Many commits, one backend call (cross-commit batching: blocksync
-  // look-ahead, light-client sequential headers).  Identical results to
-  // calling the single-commit functions one by one.
-  std::vector<Error> VerifyMany(std::vector<CommitPlan> &plans) const {
-    std::vector<SigEntry> all;
-    std::vector<size_t> start(plans.size());
-    for (size_t p = 0; p < plans.size(); p++) {
-      start[p] = all.size();
-      if (plans[p].early) continue;
-      for (auto &e : plans[p].entries) all.push_back(e);
-    }
-    std::vector<int8_t> st = all.empty() ? std::vector<int8_t>() : backend(all);
-    std::vector<Error> out(plans.size());
-    for (size_t p = 0; p < plans.size(); p++) out[p] = Finish(plans[p], st.data() + start[p]);
-    return out;
-  }
-
-  Error Run(Mode mode, const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id, int64_t height,
-            const Commit *commit, int64_t num = 0, int64_t den = 1) const {
-    std::vector<CommitPlan> plans;
-    plans.push_back(Plan(mode, chain_id, vals, block_id, height, commit, num, den));
-    return VerifyMany(plans)[0];
-  }
-
-  Error VerifyCommit(const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id, int64_t height,
-                     const Commit *commit) const {
-    return Run(kFull, chain_id, vals, block_id, height, commit);
-  }
-  Error VerifyCommitLight(const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id,
-                          int64_t height, const Commit *commit) const {
-    return Run(kLight, chain_id, vals, block_id, height, commit);
-  }
-  Error VerifyCommitLightTrusting(const std::string &chain_id, const ValidatorSet *vals, const Commit *commit,
-                                  int64_t num, int64_t den) const {
-    return Run(kLightTrusting, chain_id, vals, BlockID{}, 0, commit, num, den);
   }
 };
 

@@ -28,6 +28,7 @@
 #include "ed25519_core.h"
 #include "merlin_dev.h"
 #include "verify_kernels.h"
+#include "votes.h"
 
 namespace {
 
@@ -747,17 +748,28 @@ int tmv_num_devices(const tmv_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0
 
 enum class Scheme { Ed25519, Sr25519, Mixed, Ed25519Cached, Sr25519Cached };
 
+// Messages built on the device from vote templates (tmv_verify_votes):
+// the host sends the votes and the template table + blob; msg_off still
+// holds the host-computed offsets of the messages the device will write.
+struct VoteSrc {
+  const tmv_vote *votes;
+  const uint8_t *tab;  // n_tmpl VoteTab, then the template bytes
+  size_t tab_bytes, blob_at;
+};
+
 // Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
 // Layout: pk | sig | off | msg | kind (16-B aligned pieces).
 static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch, const uint8_t *kind,
                             const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                            uint32_t lo, uint32_t hi) {
+                            uint32_t lo, uint32_t hi, const VoteSrc *vs) {
   const uint32_t n = hi - lo;
   const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
   Layout L(n, mbytes);
   const bool cached = sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached;
   const size_t kind_at = L.total;
-  const size_t total = L.total + (sch == Scheme::Mixed ? align16(n) : 0) + (cached ? align16(4ull * n) : 0);
+  const size_t votes_at = L.total + (sch == Scheme::Mixed ? align16(n) : 0) + (cached ? align16(4ull * n) : 0);
+  const size_t tab_at = votes_at + (vs ? align16(sizeof(tmv_vote) * n) : 0);
+  const size_t total = tab_at + (vs ? align16(vs->tab_bytes) : 0);
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   if ((e = d.h_in.ensure(total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
@@ -771,7 +783,12 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
   uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
   const uint32_t base = msg_off[lo];
   for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
-  if (mbytes) par_memcpy(h + L.msg, msg + base, mbytes);
+  if (vs) {
+    par_memcpy(h + votes_at, vs->votes + lo, sizeof(tmv_vote) * n);
+    std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
+  } else if (mbytes) {
+    par_memcpy(h + L.msg, msg + base, mbytes);
+  }
   if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
   tm.mark("stage", n);
   if (cached) {
@@ -783,12 +800,25 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
     }
   }
   tm.mark("keys", n);
-  if ((e = hipMemcpyAsync(d.d_in.ptr, h, total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
+  uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
+  const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
+  if (vs) {  // everything but the message region, which the device writes
+    if ((e = hipMemcpyAsync(dd, h, L.msg, hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(dd + L.total, h + L.total, total - L.total, hipMemcpyHostToDevice, d.stream)) !=
+            hipSuccess) {
+      set_error("hipMemcpyAsync(H2D)", e);
+      return TMV_ERR_LAUNCH;
+    }
+    const tmv::VoteTab *tab = reinterpret_cast<const tmv::VoteTab *>(dd + tab_at);
+    if ((e = tmv::launch_vote_signbytes(reinterpret_cast<const tmv_vote *>(dd + votes_at), tab,
+                                        dd + tab_at + vs->blob_at, doff, n, dd + L.msg, d.stream)) != hipSuccess) {
+      set_error("k_vote_signbytes", e);
+      return TMV_ERR_LAUNCH;
+    }
+  } else if ((e = hipMemcpyAsync(d.d_in.ptr, h, total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
   }
-  uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
-  const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
   uint8_t *out = static_cast<uint8_t *>(d.d_out.ptr);
   const LaunchOpts o = (sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached) ? LaunchOpts{}
                                                                                          : make_opts(ctx, flags, n);
@@ -820,10 +850,12 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
 // Host-buffer batch: shard by contiguous index ranges over the context's
 // devices, stage, launch, gather.  out gets 1 byte per entry.
 static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
-                     const uint8_t *msg, const uint32_t *msg_off, uint32_t n, uint8_t *out, uint32_t flags = 0) {
+                     const uint8_t *msg, const uint32_t *msg_off, uint32_t n, uint8_t *out, uint32_t flags = 0,
+                     const VoteSrc *vs = nullptr) {
   if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
   if (n == 0) return TMV_NOT_ALL;
-  if (!pk || !sig || !msg_off || !out || (sch == Scheme::Mixed && !kind) || (!msg && msg_off[n] != msg_off[0])) {
+  if (!pk || !sig || !msg_off || !out || (sch == Scheme::Mixed && !kind) ||
+      (!msg && !vs && msg_off[n] != msg_off[0])) {
     set_error("null argument");
     return TMV_ERR_ARG;
   }
@@ -837,7 +869,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   int rc = 0;
   EngineTimer tm;
   for (uint32_t s = 0; s < shards && rc == 0; s++)
-    rc = stage_and_launch(ctx, flags, *ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1]);
+    rc = stage_and_launch(ctx, flags, *ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1], vs);
   tm.mark("launched", n);
   for (uint32_t s = 0; s < shards; s++) {
     Device &d = *ctx->devs[s];
@@ -852,6 +884,46 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   for (uint32_t i = 0; i < n; i++)
     if (out[i] != 1) return TMV_NOT_ALL;
   return TMV_ALL_VALID;
+}
+
+// Template table + blob for k_vote_signbytes, and the offsets of every
+// vote's message (host-side sizing with the device's own length functions).
+static int prepare_votes(const tmv_vote_template *tmpl, uint32_t n_tmpl, const tmv_vote *votes, uint32_t n,
+                         std::vector<uint8_t> &tab, size_t &blob_at, std::vector<uint32_t> &off) {
+  if ((!tmpl && n_tmpl) || (!votes && n)) { set_error("null argument"); return TMV_ERR_ARG; }
+  std::vector<tmv::VoteTab> vt(n_tmpl);
+  uint64_t blob = 0;
+  for (uint32_t t = 0; t < n_tmpl; t++) {
+    const tmv_vote_template &T = tmpl[t];
+    if ((T.head_len && !T.head) || (T.block_len && !T.block) || (T.chain_len && !T.chain)) {
+      set_error("null template segment");
+      return TMV_ERR_ARG;
+    }
+    vt[t] = tmv::VoteTab{(uint32_t)blob, T.head_len, (uint32_t)(blob + T.head_len), T.block_len,
+                         (uint32_t)(blob + T.head_len + T.block_len), T.chain_len};
+    blob += (uint64_t)T.head_len + T.block_len + T.chain_len;
+    if (blob > (1u << 30)) { set_error("vote templates too large"); return TMV_ERR_ARG; }
+  }
+  blob_at = align16(sizeof(tmv::VoteTab) * n_tmpl);
+  tab.resize(blob_at + blob);
+  if (n_tmpl) std::memcpy(tab.data(), vt.data(), sizeof(tmv::VoteTab) * n_tmpl);
+  for (uint32_t t = 0; t < n_tmpl; t++) {
+    uint8_t *b = tab.data() + blob_at + vt[t].head_at;
+    if (tmpl[t].head_len) std::memcpy(b, tmpl[t].head, tmpl[t].head_len);
+    if (tmpl[t].block_len) std::memcpy(b + tmpl[t].head_len, tmpl[t].block, tmpl[t].block_len);
+    if (tmpl[t].chain_len) std::memcpy(b + tmpl[t].head_len + tmpl[t].block_len, tmpl[t].chain, tmpl[t].chain_len);
+  }
+  off.resize((size_t)n + 1);
+  off[0] = 0;
+  uint64_t acc = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t t = votes[i].tmpl & ~TMV_VOTE_WITH_BLOCK;
+    if (t >= n_tmpl) { set_error("vote template index out of range"); return TMV_ERR_ARG; }
+    acc += tmv::vote_msg_len(vt[t], votes[i]);
+    if (acc > UINT32_MAX) { set_error("vote messages exceed 4 GiB"); return TMV_ERR_ARG; }
+    off[i + 1] = (uint32_t)acc;
+  }
+  return 0;
 }
 
 static Device *find_device(tmv_ctx *ctx, int device) {
@@ -893,6 +965,65 @@ int tmv_verify_mixed_batch_ex(tmv_ctx *ctx, uint32_t flags, const uint8_t *kind,
                               int8_t *status_out) {
   return run_batch(ctx, Scheme::Mixed, kind, pk, sig, msg, msg_off, n, reinterpret_cast<uint8_t *>(status_out),
                    flags);
+}
+
+int tmv_verify_votes(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const tmv_vote_template *tmpl,
+                     uint32_t n_tmpl, const tmv_vote *votes, const uint8_t *pk, const uint8_t *sig, uint32_t n,
+                     int8_t *status_out) {
+  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
+  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0 && !(flags & TMV_FLAG_BATCH_EQUATION);
+  Scheme sch;
+  if (key_kind == TMV_KIND_ED25519) sch = cache ? Scheme::Ed25519Cached : Scheme::Ed25519;
+  else if (key_kind == TMV_KIND_SR25519) sch = cache ? Scheme::Sr25519Cached : Scheme::Sr25519;
+  else { set_error("unsupported key kind"); return TMV_ERR_ARG; }
+  static thread_local std::vector<uint8_t> tab;
+  static thread_local std::vector<uint32_t> off;
+  size_t blob_at = 0;
+  EngineTimer tm;
+  const int pr = prepare_votes(tmpl, n_tmpl, votes, n, tab, blob_at, off);
+  if (pr < 0) return pr;
+  tm.mark("votes", n);
+  const VoteSrc vs{votes, tab.data(), tab.size(), blob_at};
+  return run_batch(ctx, sch, nullptr, pk, sig, nullptr, off.data(), n, reinterpret_cast<uint8_t *>(status_out),
+                   flags, &vs);
+}
+
+int64_t tmv_vote_sign_bytes_device(tmv_ctx *ctx, const tmv_vote_template *tmpl, uint32_t n_tmpl,
+                                   const tmv_vote *votes, uint32_t n, uint8_t *msg_out, size_t msg_cap,
+                                   uint32_t *msg_off_out) {
+  if (!ctx || !msg_off_out) { set_error("null argument"); return TMV_ERR_ARG; }
+  std::vector<uint8_t> tab;
+  std::vector<uint32_t> off;
+  size_t blob_at = 0;
+  const int pr = prepare_votes(tmpl, n_tmpl, votes, n, tab, blob_at, off);
+  if (pr < 0) return pr;
+  std::memcpy(msg_off_out, off.data(), sizeof(uint32_t) * ((size_t)n + 1));
+  const size_t total = off[n];
+  if (!msg_out || n == 0) return (int64_t)total;
+  if (msg_cap < total) { set_error("msg_cap too small"); return TMV_ERR_ARG; }
+  Device &d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  hipError_t e = hipSetDevice(d.id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  const size_t v_at = 0, t_at = align16(sizeof(tmv_vote) * n), o_at = t_at + align16(tab.size()),
+               m_at = o_at + align16(4ull * (n + 1)), bytes = m_at + std::max<size_t>(total, 1);
+  uint8_t *dev = nullptr;
+  if ((e = hipMalloc(&dev, bytes)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  int rc = 0;
+  if ((e = hipMemcpyAsync(dev + v_at, votes, sizeof(tmv_vote) * n, hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(dev + t_at, tab.data(), tab.size(), hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(dev + o_at, off.data(), 4ull * (n + 1), hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+      (e = tmv::launch_vote_signbytes(reinterpret_cast<const tmv_vote *>(dev + v_at),
+                                      reinterpret_cast<const tmv::VoteTab *>(dev + t_at), dev + t_at + blob_at,
+                                      reinterpret_cast<const uint32_t *>(dev + o_at), n, dev + m_at, d.stream)) !=
+          hipSuccess ||
+      (e = hipMemcpyAsync(msg_out, dev + m_at, total, hipMemcpyDeviceToHost, d.stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(d.stream)) != hipSuccess) {
+    set_error("tmv_vote_sign_bytes_device", e);
+    rc = TMV_ERR_LAUNCH;
+  }
+  (void)hipFree(dev);
+  return rc < 0 ? rc : (int64_t)total;
 }
 
 int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bits, const uint8_t *seed32,

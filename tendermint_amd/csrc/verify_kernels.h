@@ -4,6 +4,7 @@
 #include "curve25519.h"
 #include "merlin_dev.h"
 #include "msm.h"
+#include "../../include/tmverify.h"
 
 namespace tmv {
 
@@ -105,6 +106,11 @@ struct BatchRefs {
 hipError_t launch_gather(const BatchRefs &r, uint8_t *pk, uint8_t *sig, uint32_t *off, uint8_t *msg,
                          hipStream_t stream);
 hipError_t launch_scatter(const BatchRefs &r, const int8_t *status, hipStream_t stream);
+
+// Vote sign-bytes from templates (signbytes_kernels.hip, votes.h).
+struct VoteTab;
+hipError_t launch_vote_signbytes(const tmv_vote *votes, const VoteTab *tab, const uint8_t *blob,
+                                 const uint32_t *off, uint32_t n, uint8_t *msg, hipStream_t stream);
 
 hipError_t launch_ed25519_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                  const uint32_t *msg_off, uint32_t n, const ge_precomp *btable,

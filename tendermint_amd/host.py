@@ -194,6 +194,10 @@ def _setup(L):
     L.tmv_vote_sign_bytes.restype = ctypes.c_size_t
     L.tmv_vote_sign_bytes.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.POINTER(CBlockID), ctypes.c_int64, ctypes.c_int32, _u8p, ctypes.c_size_t]
+    L.tmv_vote_template_encode.restype = ctypes.c_size_t
+    L.tmv_vote_template_encode.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.POINTER(CBlockID), _u8p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_uint32)]
     L.tmv_verify_commit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(CValidator),
                                     ctypes.c_uint32, ctypes.c_int32, ctypes.POINTER(CBlockID), ctypes.c_int64,
                                     ctypes.POINTER(CCommit), ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p,
@@ -221,6 +225,22 @@ def vote_sign_bytes(chain_id: str, vote_type: int, height: int, round_: int, blo
     n = L.tmv_vote_sign_bytes(chain_id.encode(), vote_type, height, round_, bid, timestamp[0], timestamp[1],
                               ctypes.cast(out, _u8p), 512)
     return bytes(out[:n])
+
+
+def vote_template(chain_id: str, vote_type: int, height: int, round_: int, block_id: Optional[BlockID],
+                  lib=None) -> Tuple[bytes, bytes, bytes]:
+    """The (head, block, chain) segments of tmv_verify_votes' template through
+    the C++ encoder (tmv_vote_template_encode)."""
+    L = _setup(lib or _native.lib())
+    k = _Keep()
+    bid = ctypes.byref(_c_block_id(k, block_id)) if block_id is not None else None
+    out = (ctypes.c_uint8 * 1024)()
+    lens = (ctypes.c_uint32 * 3)()
+    n = L.tmv_vote_template_encode(chain_id.encode(), vote_type, height, round_, bid, ctypes.cast(out, _u8p), 1024,
+                                   lens)
+    b = bytes(out[:n])
+    h, k2 = lens[0], lens[0] + lens[1]
+    return b[:h], b[h:k2], b[k2:]
 
 
 def _commit_call(fn, ctx_handle, mode, chain_id, vals: Optional[ValidatorSet], block_id: Optional[BlockID],

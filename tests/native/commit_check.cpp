@@ -71,6 +71,47 @@ int tmv_verify_batch_ex(tmv_ctx *, uint8_t key_kind, uint32_t, const uint8_t *pk
   return all ? TMV_ALL_VALID : TMV_NOT_ALL;
 }
 
+// The message the device builds for a vote (include/tmverify.h,
+// tmv_verify_votes), assembled here independently of the product's encoder
+// so that the CPU suite checks the template split against the reference's
+// sign-bytes (tests compare with oracle-encoded messages).
+static void put_uvarint(Bytes &out, uint64_t x) {
+  while (x >= 0x80) { out.push_back((uint8_t)(x | 0x80)); x >>= 7; }
+  out.push_back((uint8_t)x);
+}
+static Bytes vote_message(const tmv_vote_template &t, const tmv_vote &v) {
+  Bytes ts;
+  if (v.ts_seconds != 0) { ts.push_back(0x08); put_uvarint(ts, (uint64_t)v.ts_seconds); }
+  if (v.ts_nanos != 0) { ts.push_back(0x10); put_uvarint(ts, (uint64_t)(int64_t)v.ts_nanos); }
+  Bytes body(t.head, t.head + t.head_len);
+  if (v.tmpl & TMV_VOTE_WITH_BLOCK) body.insert(body.end(), t.block, t.block + t.block_len);
+  body.push_back(0x2a);
+  put_uvarint(body, ts.size());
+  body.insert(body.end(), ts.begin(), ts.end());
+  body.insert(body.end(), t.chain, t.chain + t.chain_len);
+  Bytes msg;
+  put_uvarint(msg, body.size());
+  msg.insert(msg.end(), body.begin(), body.end());
+  return msg;
+}
+
+int tmv_verify_votes(tmv_ctx *, uint8_t key_kind, uint32_t, const tmv_vote_template *tmpl, uint32_t n_tmpl,
+                     const tmv_vote *votes, const uint8_t *pk, const uint8_t *sig, uint32_t n, int8_t *status_out) {
+  commitcheck_backend_calls++;
+  commitcheck_entries_verified += (int)n;
+  bool all = n > 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t t = votes[i].tmpl & ~TMV_VOTE_WITH_BLOCK;
+    if (t >= n_tmpl) return TMV_ERR_ARG;
+    const Bytes key(pk + 32 * i, pk + 32 * i + 32);
+    status_out[i] = g_skip_hash ? 1
+                                : fake_status(key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, key,
+                                              vote_message(tmpl[t], votes[i]), Bytes(sig + 64 * i, sig + 64 * i + 64));
+    all = all && status_out[i] == 1;
+  }
+  return all ? TMV_ALL_VALID : TMV_NOT_ALL;
+}
+
 static tmv_ctx g_ctx;
 
 // Same contract as tmv_verify_commits (include/tmhost.h), fake signatures.
