@@ -1,0 +1,26 @@
+// A process-wide pool of host worker threads for the engine's parallel
+// loops (packing, planning, key lookups, staging copies).  Spawning and
+// joining 15 threads costs ~0.2-0.5 ms, several times per commit window;
+// the pool's workers sleep on a condition variable between jobs instead.
+// One job runs at a time; a caller that finds the pool busy (another thread
+// inside the engine, or a loop nested in a pool job) runs its loop itself.
+#pragma once
+#include <cstddef>
+#include <type_traits>
+
+namespace tmh {
+
+// Calls fn(ctx, i) for every i in [0, n) on up to max_threads threads
+// (the caller included).  Returns when all calls have finished.
+void pool_for(size_t n, size_t max_threads, void (*fn)(void *, size_t), void *ctx);
+
+// Threads the pool may use: min(16, hardware threads), or TMV_HOST_THREADS.
+size_t pool_threads();
+
+template <class F>
+void parallel_for_n(size_t n, size_t max_threads, F &&fn) {
+  using Fn = std::remove_reference_t<F>;
+  pool_for(n, max_threads, [](void *c, size_t i) { (*static_cast<Fn *>(c))(i); }, const_cast<void *>(static_cast<const void *>(&fn)));
+}
+
+}  // namespace tmh

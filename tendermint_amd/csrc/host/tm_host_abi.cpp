@@ -17,6 +17,7 @@
 
 #include "../../../include/tmhost.h"
 #include "../../../include/tmverify.h"
+#include "pool.h"
 #include "tm_types.h"
 
 namespace {
@@ -193,27 +194,10 @@ size_t tmv_vote_template_encode(const char *chain_id, int32_t vote_type, int64_t
 
 namespace {
 
-// Run fn(i) for i in [0, n) on up to 16 host threads (serial when small).
+// Run fn(i) for i in [0, n) on the host worker pool (serial when small).
 template <class F>
 void parallel_for(size_t n, size_t min_per_thread, F fn) {
-  static const size_t hw = [] {
-    const char *e = std::getenv("TMV_HOST_THREADS");
-    const long v = e ? std::atol(e) : 0;
-    return v > 0 ? (size_t)v : (size_t)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  }();
-  const size_t nt = std::min(hw, n / std::max<size_t>(1, min_per_thread));
-  if (nt <= 1) {
-    for (size_t i = 0; i < n; i++) fn(i);
-    return;
-  }
-  std::atomic<size_t> next{0};
-  auto worker = [&] {
-    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
-  };
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nt; t++) th.emplace_back(worker);
-  worker();
-  for (auto &t : th) t.join();
+  tmh::parallel_for_n(n, n / std::max<size_t>(1, min_per_thread), fn);
 }
 
 // Signature backend over the device: entries split by key kind, each kind one
@@ -260,24 +244,30 @@ struct GpuBackend {
     std::unordered_map<const tmh::CommitPlan *, uint32_t> plan_tmpl;
     std::unordered_map<const tmh::Commit *, std::vector<std::pair<const std::string *, uint32_t>>> by_commit;
     std::vector<uint32_t> ent_tmpl(es.size());
+    const tmh::CommitPlan *last = nullptr;  // entries come plan by plan
+    uint32_t last_t = 0;
     for (size_t i = 0; i < es.size(); i++) {
       const tmh::CommitPlan *pl = es[i].pl;
-      auto [it, fresh] = plan_tmpl.emplace(pl, 0);
-      if (fresh) {
-        auto &chains = by_commit[pl->commit];
-        uint32_t t = UINT32_MAX;
-        for (auto &c : chains)
-          if (*c.first == pl->chain_id) t = c.second;
-        if (t == UINT32_MAX) {
-          t = (uint32_t)tmpls.size();
-          const tmh::Commit &cm = *pl->commit;
-          tmpls.push_back(tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round,
-                                                  &cm.block_id));
-          chains.emplace_back(&pl->chain_id, t);
+      if (pl != last) {
+        auto [it, fresh] = plan_tmpl.emplace(pl, 0);
+        if (fresh) {
+          auto &chains = by_commit[pl->commit];
+          uint32_t t = UINT32_MAX;
+          for (auto &c : chains)
+            if (*c.first == pl->chain_id) t = c.second;
+          if (t == UINT32_MAX) {
+            t = (uint32_t)tmpls.size();
+            const tmh::Commit &cm = *pl->commit;
+            tmpls.push_back(tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round,
+                                                    &cm.block_id));
+            chains.emplace_back(&pl->chain_id, t);
+          }
+          it->second = t;
         }
-        it->second = t;
+        last = pl;
+        last_t = it->second;
       }
-      ent_tmpl[i] = it->second;
+      ent_tmpl[i] = last_t;
     }
     std::vector<tmv_vote_template> tv(tmpls.size());
     for (size_t t = 0; t < tmpls.size(); t++) {

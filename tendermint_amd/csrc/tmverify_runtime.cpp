@@ -27,6 +27,7 @@
 #include "../../include/tmverify.h"
 #include "ed25519_core.h"
 #include "merlin_dev.h"
+#include "host/pool.h"
 #include "verify_kernels.h"
 #include "votes.h"
 
@@ -44,18 +45,13 @@ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 // Large staging copies into pinned memory use several host threads (one
 // thread moves ~10 GB/s; a 1M-signature batch is ~220 MB).
 void par_memcpy(void *dst, const void *src, size_t n) {
-  const size_t kChunk = size_t(4) << 20;
+  const size_t kChunk = size_t(2) << 20;
   if (n < 2 * kChunk) { std::memcpy(dst, src, n); return; }
-  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  const unsigned nt = (unsigned)std::min<size_t>(hw, n / kChunk);
-  std::vector<std::thread> th;
-  const size_t per = (n + nt - 1) / nt;
-  for (unsigned t = 1; t < nt; t++) {
-    const size_t lo = t * per, len = std::min(n, lo + per) - lo;
-    th.emplace_back([=] { std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len); });
-  }
-  std::memcpy(dst, src, std::min(n, per));
-  for (auto &x : th) x.join();
+  const size_t chunks = (n + kChunk - 1) / kChunk;
+  tmh::parallel_for_n(chunks, 8, [&](size_t c) {
+    const size_t lo = c * kChunk, len = std::min(n, lo + kChunk) - lo;
+    std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len);
+  });
 }
 
 struct DeviceBuf {
@@ -453,12 +449,11 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
       last_pk = p;
     }
   };
-  const uint32_t nth = n >= 16384 ? std::max(1u, std::min(8u, std::thread::hardware_concurrency())) : 1;
-  if (nth > 1) {
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < nth; t++) th.emplace_back(lookup, (uint32_t)((uint64_t)n * t / nth), (uint32_t)((uint64_t)n * (t + 1) / nth));
-    lookup(0, (uint32_t)((uint64_t)n / nth));
-    for (auto &x : th) x.join();
+  if (n >= 16384) {
+    const uint32_t parts = 16;
+    tmh::parallel_for_n(parts, 8, [&](size_t t) {
+      lookup((uint32_t)((uint64_t)n * t / parts), (uint32_t)((uint64_t)n * (t + 1) / parts));
+    });
   } else {
     lookup(0, n);
   }
