@@ -25,6 +25,20 @@
 //                window sum S_w = sum_j (j+1) bucket_j
 //   k_msm_horner one quad per group: T_g = sum_w 2^(c w) S_w (Horner, quad-lane
 //                arithmetic) and the group verdict
+//
+// Key-merged form (batches whose keys sit in the
+// device key cache, e.g. commits of one validator set): entries are ordered
+// by key, so a group holds few distinct keys, and the A terms collapse to
+// one scalar per (group, key):  sum_i [z_i k_i](-A_i) = sum_key [W_key](-A_key)
+// with W_key = sum z_i k_i mod l.  The MSM then covers only the m R points
+// (ceil(129/c) windows of the 128-bit z_i: Horner needs ~129 doublings, not
+// ~253), and each key term and the B term are comb sums over the cached
+// tables (64 and 32 additions, no doublings):
+//   k_msm_sort<KM>  z_i digits only; w_i = z_i k_i and the B scalar to HBM
+//   k_msm_items     one quad per run of one key inside a group (W_key, key
+//                   comb) and per group (B scalar, base comb)
+//   k_msm_horner<KM> Horner over the R windows + the group's item points
+// The per-entry fallback of failing groups is the key-cached comb kernel.
 #pragma once
 #include <stdint.h>
 #include "curve25519.h"
@@ -51,25 +65,27 @@ struct MsmParams {
   uint32_t groups;   // groups allocated = ceil(n / m)
   uint32_t P;        // lanes per window in k_msm_wpart (power of two <= H)
   uint32_t L;        // sorted entries per k_msm_accum lane (8, 16 or 32)
+  uint32_t merged;   // key-merged form: R points only, W = WR
 
   TMV_HD uint32_t m() const { return 1u << m_log2; }
   TMV_HD uint32_t buckets_per_group() const { return W * H; }
   TMV_HD uint32_t chunks_per_group() const { return cap / L; }
 
-  static MsmParams make(uint32_t n, uint32_t m_log2, uint32_t c) {
+  static MsmParams make(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false) {
     MsmParams p;
     p.m_log2 = m_log2;
     p.c = c;
-    p.W = (254 + c - 1) / c;
+    p.merged = merged ? 1 : 0;
     p.WR = (129 + c - 1) / c;
+    p.W = merged ? p.WR : (254 + c - 1) / c;
     p.H = 1u << (c - 1);
     const uint32_t m = 1u << m_log2;
-    const uint32_t slots = (2 * m + 1) * p.W;
+    const uint32_t slots = merged ? m * p.WR : (2 * m + 1) * p.W;
     p.cap = (slots + kMsmChunkMax - 1) / kMsmChunkMax * kMsmChunkMax;
     // chunk length at least the mean bucket size of the low windows (2m / H
     // entries) so buckets rarely span chunks (few partials to merge);
     // measured: 16 beats 8 at m = 64 (C2) and 32 at m = 1024 (1M honest)
-    const uint32_t mean = 2 * m / p.H;
+    const uint32_t mean = (merged ? m : 2 * m) / p.H;
     p.L = mean <= 16 ? 16 : 32;
     p.groups = (n + m - 1) >> m_log2;
     // P minimises the latency chain: 2 H/P running-sum additions per part,
@@ -99,12 +115,21 @@ struct MsmWork {
   ge_p3 *wsum;         // groups x W: window sums
   uint8_t *group_ok;   // groups
   uint32_t n_pts;      // index of B (= 2n)
+  // key-merged form only (null otherwise)
+  uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
+  uint32_t *bscal;     // groups x 8 words: B scalar of the group
+  fe *item_pt;         // (runs + groups) x 4 fe, P3Q: key-run and B-term points
+
+  // item capacity of the key-merged form: runs (<= n + groups) + groups
+  static size_t max_items(uint32_t n, const MsmParams &p) { return (size_t)n + 2ull * p.groups; }
 
   static size_t bytes(uint32_t n, const MsmParams &p) {
     const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
     const size_t chunks = ent / p.L;
-    return (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
-           2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 16 * 12;
+    size_t b = (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
+               2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 16 * 16;
+    if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
+    return b;
   }
   static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
     auto up = [](size_t x) { return (x + 15) & ~size_t(15); };
@@ -123,8 +148,15 @@ struct MsmWork {
     w.part_last = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.P * sizeof(ge_p3));
     w.wsum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * sizeof(ge_p3));
-    w.group_ok = b + o;
+    w.group_ok = b + o; o = up(o + G);
     w.n_pts = 2 * n;
+    w.wscal = w.bscal = nullptr;
+    w.item_pt = nullptr;
+    if (p.merged) {
+      w.wscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32ull * n);
+      w.bscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32 * G);
+      w.item_pt = reinterpret_cast<fe *>(b + o);
+    }
     return w;
   }
 };

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include "ed25519_core.h"
 #include "kernel_util.h"
+#include "comb.h"
 #include "quad.h"
 #include "verify_kernels.h"
 
@@ -87,17 +88,21 @@ __device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &o
 
 // One workgroup per group of m entries: z_e, z_e k_e mod l, sum z_e s_e mod l
 // (the B scalar), then a counting sort of the (window, |digit|) bucket entries
-// of the 2m+1 points into the group's slots of ent_pt/ent_bk.
-template <bool SR>
+// of the 2m+1 points into the group's slots of ent_pt/ent_bk.  KM (key-merged
+// form): only the m R points are sorted; z_e k_e and the B scalar go to
+// mw.wscal / mw.bscal for k_msm_items, and the key's decode status comes from
+// the key cache.
+template <bool SR, bool KM>
 __global__ void __launch_bounds__(kMsmSortBlock)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
-           Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned) {
+           Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned,
+           const uint32_t *__restrict__ key_slot, const uint8_t *__restrict__ key_ok) {
   extern __shared__ uint32_t smem[];
   const uint32_t cnt = entry_count(count_ptr, n);
   const uint32_t g = blockIdx.x;
   const uint32_t tid = threadIdx.x;
   const uint32_t e0 = g << p.m_log2;
-  if (g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
+  if (!KM && g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
     niels_pt bp;
     bp.ymx = btab_q[0];
     bp.ypx = btab_q[1];
@@ -140,7 +145,14 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       for (int t = 0; t < 8; t++) s[t] = s_raw[t];
       s_ok = sc_is_canonical(s);
     }
-    if (!(s_ok && w.flags[4 * e] && w.flags[4 * e + 1])) continue;  // left out of the sums
+    const bool a_ok = KM ? key_ok[key_slot[e]] != 0 : w.flags[4 * e] != 0;
+    if (!(s_ok && a_ok && w.flags[4 * e + 1])) {  // left out of the sums
+      if (KM) {
+        uint4 *wd = reinterpret_cast<uint4 *>(mw.wscal + 8ull * e);
+        wd[0] = wd[1] = make_uint4(0, 0, 0, 0);
+      }
+      continue;
+    }
     live[r] = true;
     uint32_t blk[16];
     chacha20_block(blk, seed.key, e, seed.nonce);
@@ -152,6 +164,11 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w;
     k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
     sc_mul_mod(wv[r], z[r], 4, k);
+    if (KM) {
+      uint4 *wd = reinterpret_cast<uint4 *>(mw.wscal + 8ull * e);
+      wd[0] = make_uint4(wv[r][0], wv[r][1], wv[r][2], wv[r][3]);
+      wd[1] = make_uint4(wv[r][4], wv[r][5], wv[r][6], wv[r][7]);
+    }
     uint32_t u[8];
     sc_mul_mod(u, z[r], 4, s);
     uint64_t c = 0;
@@ -183,6 +200,8 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     for (int t = 0; t < 16; t++) x[t] = t < 9 ? red[t] : 0;
     sc_reduce512(b, x);
     for (int t = 0; t < 8; t++) red[t] = b[t];
+    if (KM)
+      for (int t = 0; t < 8; t++) mw.bscal[8ull * g + t] = b[t];
   }
   for (uint32_t t = tid; t < WH; t += kMsmSortBlock) hist[t] = 0;
   __syncthreads();
@@ -195,9 +214,9 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   for (int r = 0; r < R; r++) {
     if (!live[r]) continue;
     for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
-    for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
+    if (!KM) for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
   }
-  if (tid == 0) for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
+  if (!KM && tid == 0) for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
   __syncthreads();
 
   // exclusive scan: contiguous segments per thread, thread 0 scans the totals
@@ -240,16 +259,16 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     const uint32_t e = e0 + tid + r * kMsmSortBlock;
     for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      ent_pt[pos] = ((2 * e) << 1) | (neg ? 1u : 0u);
+      ent_pt[pos] = ((KM ? e : 2 * e) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
-    for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool neg) {
+    if (!KM) for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
       ent_pt[pos] = ((2 * e + 1) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
   }
-  if (tid == 0) {
+  if (!KM && tid == 0) {
     for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
       ent_pt[pos] = (mw.n_pts << 1) | (neg ? 1u : 0u);
@@ -379,9 +398,10 @@ k_msm_wsum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 // Group verdicts: one quad per group (lane c holds coordinate c), 16 groups
 // per wave; T_g = sum_w 2^(c w) S_w by Horner, then
 //   ed25519: [8] T_g == O;  sr25519: T_g is the Ristretto identity.
-template <bool SR>
+template <bool SR, bool KM>
 __global__ void __launch_bounds__(64)
-k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, const uint32_t *__restrict__ group_run0,
+             uint32_t n_runs) {
   const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
   if (blockIdx.x * 16 >= live_groups) return;  // block-uniform
   const uint32_t raw = blockIdx.x * 16 + (threadIdx.x >> 2);
@@ -401,6 +421,15 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     quad::add(r, acc, qc);
     quad::p1p1_to_p3(acc, r);
   }
+  if (KM) {  // + the group's key-run points and its B-term point (k_msm_items)
+    const uint32_t r0 = group_run0[g], r1 = group_run0[g + 1];
+    for (uint32_t it = r0; it <= r1; it++) {
+      q = mw.item_pt[4ull * (it < r1 ? it : n_runs + g) + c];
+      quad::to_cached(qc, q);
+      quad::add(r, acc, qc);
+      quad::p1p1_to_p3(acc, r);
+    }
+  }
   bool ok;
   if (SR) {
     fe id;
@@ -410,6 +439,27 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     ok = quad::is_identity_times8(acc);
   }
   if (live && c == 0) mw.group_ok[g] = ok ? 1 : 0;
+}
+
+// Bucket sums, window parts and window sums (shared by both forms).
+static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork mw, const MsmParams &p,
+                                 hipStream_t stream) {
+  const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
+  const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
+  if (p.L == 8)
+    hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+  else if (p.L == 16)
+    hipLaunchKernelGGL(k_msm_accum<16>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+  else
+    hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+  hipError_t e;
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
+  hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint64_t rows = (uint64_t)p.groups * p.W;
+  hipLaunchKernelGGL(k_msm_wsum, dim3((uint32_t)((rows + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  return hipGetLastError();
 }
 
 template <bool SR>
@@ -423,27 +473,112 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
   const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_msm_sort<SR>, dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx, count_ptr, n, w,
-                     mw, p, seed, btab_q, aligned);
+  hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx, count_ptr, n,
+                     w, mw, p, seed, btab_q, aligned, nullptr, nullptr);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
-  const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
-  if (p.L == 8)
-    hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
-  else if (p.L == 16)
-    hipLaunchKernelGGL(k_msm_accum<16>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
-  else
-    hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
-  hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  const uint64_t rows = (uint64_t)p.groups * p.W;
-  hipLaunchKernelGGL(k_msm_wsum, dim3((uint32_t)((rows + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_msm_horner<SR>, dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p);
+  if ((e = launch_buckets(count_ptr, n, mw, p, stream)) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
+                     nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream);
+}
+
+// Key-merged form: one quad per item.  Items [0, n_runs) are runs of one key
+// inside a group: W = sum of z_e k_e over the run (mod l), then [W](-A) from
+// the key's comb (64 additions).  Item n_runs + g is group g's B term:
+// [sum z_e s_e]B from the base comb (32 additions).  Lane 0 of the quad
+// forms the scalar and its digits; all four lanes add (quad arithmetic).
+__global__ void __launch_bounds__(kQuadBlock)
+k_msm_items(KeyRuns runs, uint32_t n_items, MsmWork mw, KeyTable kt, const fe *__restrict__ bcomb) {
+  constexpr int kItems = kQuadBlock / 4;
+  __shared__ int8_t dig[kItems][64];
+  if (blockIdx.x * kItems >= n_items) return;  // block-uniform
+  const int c = threadIdx.x & 3;
+  const int q = threadIdx.x >> 2;
+  const uint32_t raw = blockIdx.x * kItems + q;
+  const bool live = raw < n_items;
+  const uint32_t it = live ? raw : n_items - 1;
+  const bool key = it < runs.n_runs;  // quad-uniform; runs precede B terms
+  if (c == 0) {
+    uint32_t sc[8];
+    if (key) {
+      uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t e = runs.lo[it]; e < runs.lo[it + 1]; e++) {
+        const uint4 *wp = reinterpret_cast<const uint4 *>(mw.wscal + 8ull * e);
+        const uint4 a = wp[0], b = wp[1];
+        const uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint64_t cy = 0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          cy += (uint64_t)acc[t] + v[t];
+          acc[t] = (uint32_t)cy;
+          cy >>= 32;
+        }
+        acc[8] += (uint32_t)cy;
+      }
+      uint32_t x[16];
+#pragma unroll
+      for (int t = 0; t < 16; t++) x[t] = t < 9 ? acc[t] : 0;
+      sc_reduce512(sc, x);
+      recode16_store(&dig[q][0], sc, true);
+    } else {
+      const uint32_t *bs = mw.bscal + 8ull * (it - runs.n_runs);
+#pragma unroll
+      for (int t = 0; t < 8; t++) sc[t] = bs[t];
+      recode256_store(&dig[q][0], sc);
+    }
+  }
+  __syncthreads();  // one wave per block
+  fe acc, idq;
+  quad::p3_identity(acc);
+  quad::cached_identity(idq);
+  if (key) {
+    const fe *krow = kt.tab + (size_t)runs.slot[it] * kKeyRowsEntries * 4;
+    comb_accumulate<64>(acc, idq, [&](int t, int &dsg) -> const fe * {
+      dsg = dig[q][t];
+      const int a = dsg < 0 ? -dsg : dsg;
+      return krow + ((t * 8) + (a ? a - 1 : 0)) * 4 + c;
+    });
+  } else {
+    comb_accumulate<32>(acc, idq, [&](int t, int &dsg) -> const fe * {
+      dsg = dig[q][t];
+      const int a = dsg < 0 ? -dsg : dsg;
+      return bcomb + ((t * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
+    });
+  }
+  if (live) mw.item_pt[4ull * it + c] = acc;
+}
+
+template <bool SR>
+static hipError_t launch_km(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                            const uint32_t *key_slot, KeyRuns runs, uint32_t n, KeyTable kt, const fe *bcomb,
+                            const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                            const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  w.niels = mw.pts;
+  hipError_t e = launch_prep_cached<SR>(pk, sig, msg, msg_off, n, prefix, w, aligned, stream);
+  if (e != hipSuccess) return e;
+  const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+  hipLaunchKernelGGL((k_msm_sort<SR, true>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, nullptr, nullptr, n,
+                     w, mw, p, seed, nullptr, aligned, key_slot, kt.ok);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = launch_buckets(nullptr, n, mw, p, stream)) != hipSuccess) return e;
+  const uint32_t n_items = runs.n_runs + p.groups;
+  hipLaunchKernelGGL(k_msm_items, dim3((n_items + 15) / 16), dim3(kQuadBlock), 0, stream, runs, n_items, mw, kt, bcomb);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_msm_horner<SR, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, nullptr, n, mw, p,
+                     runs.group_run0, runs.n_runs);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_comb_fallback<SR>(sig, key_slot, n, w, kt, bcomb, out, aligned, mw.group_ok, p.m_log2, stream);
+}
+
+hipError_t launch_key_merged_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                   const uint32_t *msg_off, const uint32_t *key_slot, KeyRuns runs, uint32_t n,
+                                   KeyTable kt, const fe *bcomb, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                                   const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (sr) return launch_km<true>(pk, sig, msg, msg_off, key_slot, runs, n, kt, bcomb, prefix, w, mw, p, seed, out, stream);
+  return launch_km<false>(pk, sig, msg, msg_off, key_slot, runs, n, kt, bcomb, prefix, w, mw, p, seed, out, stream);
 }
 
 hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,

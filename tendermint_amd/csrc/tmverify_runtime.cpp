@@ -167,6 +167,10 @@ struct Device {
   std::vector<uint64_t> kslot_epoch;
   uint64_t kepoch = 0, khits = 0, kmisses = 0;
   DeviceBuf d_kbuild, h_kbuild;
+  // host-buffer launches: key slots of the shard, and for the key-merged
+  // form the key order it was staged in (statuses come back in that order)
+  std::vector<uint32_t> slots, perm, key_count;
+  bool permuted = false;
   std::mutex mu;
 };
 
@@ -208,20 +212,23 @@ void read_env() {
 // invalid yet decode; 64 keeps the per-entry fallback near 10% of a batch
 // with 0.2% such entries, as in BASELINE configs[1]).  Window: minimises
 // bucket additions + per-window running sums for that m (c in [4, 9]).
-tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c) {
-  if (m_log2 == 0) m_log2 = 6;
+// The key-merged form (merged = true; keyed batches are commit traffic,
+// nearly always valid) defaults to groups of 256: its MSM has only the R
+// points and its fallback is the cheaper key-cached comb.
+tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false) {
+  if (m_log2 == 0) m_log2 = merged ? 8 : 6;
   m_log2 = std::max<uint32_t>(5, std::min<uint32_t>(10, m_log2));
   if (c == 0) {
     const double m = double(1u << m_log2);
     double best = 1e30;
     for (uint32_t cc = 4; cc <= 9; cc++) {
       const double W = (254 + cc - 1) / cc, WR = (129 + cc - 1) / cc, H = double(1u << (cc - 1));
-      const double cost = m * (W + WR) + 2.2 * W * H;
+      const double cost = merged ? m * WR + 2.2 * WR * H : m * (W + WR) + 2.2 * W * H;
       if (cost < best) { best = cost; c = cc; }
     }
   }
   c = std::max<uint32_t>(4, std::min<uint32_t>(9, c));
-  tmv::MsmParams p = tmv::MsmParams::make(n, m_log2, c);
+  tmv::MsmParams p = tmv::MsmParams::make(n, m_log2, c, merged);
   if (g_msm_chunk == 8 || g_msm_chunk == 16 || g_msm_chunk == 32) p.L = g_msm_chunk;
   return p;
 }
@@ -275,7 +282,7 @@ struct tmv_ctx {
 
 // Options of one launch of n entries: per-entry or batch equation (flags,
 // else TMV_MSM_MIN), parameters and fresh randomness.
-static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n) {
+static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merged = false) {
   read_env();
   LaunchOpts o;
   if (flags & TMV_FLAG_PER_ENTRY) o.batch_eq = false;
@@ -285,7 +292,7 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n) {
   uint8_t key[32];
   {
     std::lock_guard<std::mutex> lk(ctx->opt_mu);
-    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c);
+    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged);
     if (ctx->fixed_seed) std::memcpy(key, ctx->seed, 32);
   }
   if (!ctx->fixed_seed) {
@@ -652,6 +659,27 @@ static int launch_cached(Device &d, bool sr, const uint8_t *pk, const uint8_t *s
   return 0;
 }
 
+// Key-merged batch equation over a key-ordered batch (msm.h).
+static int launch_key_merged(Device &d, const LaunchOpts &o, bool sr, const uint8_t *pk, const uint8_t *sig,
+                             const uint8_t *msg, const uint32_t *off, const uint32_t *slots, tmv::KeyRuns runs,
+                             uint32_t n, uint8_t *out, hipStream_t s) {
+  int rc;
+  Workspace *ws = reserve_work(d, n, false, s, &rc, &o.p);
+  if (!ws) return rc;
+  tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
+  tmv::MsmWork mw = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
+  hipError_t e = tmv::launch_key_merged_check(sr, pk, sig, msg, off, slots, runs, n, d.kt, d.d_bcomb, d.d_prefix, w,
+                                              mw, o.p, o.seed[sr ? 1 : 0], out, s);
+  if (e != hipSuccess) { set_error("key-merged check launch", e); return TMV_ERR_LAUNCH; }
+  ws->group_ok[0] = mw.group_ok;
+  ws->group_ok[1] = nullptr;
+  ws->groups = o.p.groups;
+  ws->m_log2 = o.p.m_log2;
+  ws->counts = nullptr;
+  (void)hipEventRecord(ws->done, s);
+  return 0;
+}
+
 // Enqueue ed25519 verification of n device-resident entries on stream s.
 // Caller holds d.mu.  Chooses the quad or single-lane kernel.
 static int launch_ed25519(Device &d, const LaunchOpts &o, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
@@ -753,48 +781,114 @@ struct VoteSrc {
 };
 
 // Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
-// Layout: pk | sig | off | msg | kind (16-B aligned pieces).
+// Layout: pk | sig | off | msg | kind or key slots | votes | templates | key
+// runs (16-B aligned pieces).  Key-cached batches resolve their slots first;
+// when they take the key-merged batch equation the shard is staged in key
+// order (d.perm) and run_batch puts the statuses back.
 static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch, const uint8_t *kind,
                             const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                             uint32_t lo, uint32_t hi, const VoteSrc *vs) {
   const uint32_t n = hi - lo;
   const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
   Layout L(n, mbytes);
-  const bool cached = sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached;
+  bool cached = sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached;
+  const bool sr = sch == Scheme::Sr25519Cached || sch == Scheme::Sr25519;
+  hipError_t e = hipSetDevice(d.id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  EngineTimer tm;
+  d.permuted = false;
+  if (cached) {
+    d.slots.resize(n);
+    const int kr = resolve_keys(d, sr, pk + 32ull * lo, n, d.slots.data(), d.stream);
+    if (kr < 0) return kr;
+    if (kr == 1) {  // more distinct keys than the cache holds: uncached path
+      sch = sr ? Scheme::Sr25519 : Scheme::Ed25519;
+      cached = false;
+    }
+  }
+  tm.mark("keys", n);
+  LaunchOpts o = make_opts(ctx, flags, n, cached);
+  // key-merged form: worth it while a group holds few keys (runs <= n / 2)
+  bool merged = cached && o.batch_eq;
+  if (merged) {
+    d.key_count.assign((size_t)d.kcap + 1, 0);
+    for (uint32_t i = 0; i < n; i++) d.key_count[d.slots[i] + 1]++;
+    uint32_t distinct = 0;
+    for (uint32_t k = 1; k <= d.kcap; k++) distinct += d.key_count[k] != 0;
+    if ((uint64_t)distinct + o.p.groups > n / 2) merged = false;
+  }
+  if (cached && !merged) o.batch_eq = false;  // key-cached per-entry path
+  const uint32_t G = merged ? o.p.groups : 0;
   const size_t kind_at = L.total;
   const size_t votes_at = L.total + (sch == Scheme::Mixed ? align16(n) : 0) + (cached ? align16(4ull * n) : 0);
   const size_t tab_at = votes_at + (vs ? align16(sizeof(tmv_vote) * n) : 0);
-  const size_t total = tab_at + (vs ? align16(vs->tab_bytes) : 0);
-  hipError_t e = hipSetDevice(d.id);
-  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  const size_t runs_at = tab_at + (vs ? align16(vs->tab_bytes) : 0);
+  const size_t run_cap = (size_t)n + G;  // runs never exceed entries + group cuts
+  const size_t total = runs_at + (merged ? align16(4ull * (2 * run_cap + 1 + G + 1)) : 0);
   if ((e = d.h_in.ensure(total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_in.ensure(total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
-  EngineTimer tm;
   uint8_t *h = static_cast<uint8_t *>(d.h_in.ptr);
-  par_memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
-  par_memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
   uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
+  uint32_t *hslots = reinterpret_cast<uint32_t *>(h + kind_at);
   const uint32_t base = msg_off[lo];
-  for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
-  if (vs) {
-    par_memcpy(h + votes_at, vs->votes + lo, sizeof(tmv_vote) * n);
-    std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
-  } else if (mbytes) {
-    par_memcpy(h + L.msg, msg + base, mbytes);
-  }
-  if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
-  tm.mark("stage", n);
-  if (cached) {
-    const int kr = resolve_keys(d, sch == Scheme::Sr25519Cached, pk + 32ull * lo, n,
-                                reinterpret_cast<uint32_t *>(h + kind_at), d.stream);
-    if (kr < 0) return kr;
-    if (kr == 1) {  // more distinct keys than the cache holds: uncached path
-      sch = sch == Scheme::Sr25519Cached ? Scheme::Sr25519 : Scheme::Ed25519;
+  uint32_t n_runs = 0;
+  if (merged) {
+    // stable counting sort by key slot
+    for (uint32_t k = 1; k <= d.kcap; k++) d.key_count[k] += d.key_count[k - 1];
+    d.perm.resize(n);
+    for (uint32_t i = 0; i < n; i++) d.perm[d.key_count[d.slots[i]]++] = i;
+    off[0] = 0;
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t i = lo + d.perm[j];
+      off[j + 1] = off[j] + (msg_off[i + 1] - msg_off[i]);
     }
+    const uint32_t *perm = d.perm.data();
+    const uint32_t *slots = d.slots.data();
+    tmh::parallel_for_n((n + 4095) / 4096, 16, [&](size_t c) {
+      const uint32_t j1 = std::min<uint32_t>(n, (uint32_t)(c + 1) * 4096);
+      for (uint32_t j = (uint32_t)c * 4096; j < j1; j++) {
+        const uint32_t i = perm[j];
+        std::memcpy(h + L.pk + 32ull * j, pk + 32ull * (lo + i), 32);
+        std::memcpy(h + L.sig + 64ull * j, sig + 64ull * (lo + i), 64);
+        hslots[j] = slots[i];
+        if (vs) std::memcpy(h + votes_at + sizeof(tmv_vote) * j, vs->votes + lo + i, sizeof(tmv_vote));
+        else if (mbytes) std::memcpy(h + L.msg + off[j], msg + msg_off[lo + i], off[j + 1] - off[j]);
+      }
+    });
+    if (vs) std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
+    // runs of one key inside a group
+    uint32_t *rlo = reinterpret_cast<uint32_t *>(h + runs_at);
+    uint32_t *rslot = rlo + run_cap + 1;
+    uint32_t *rg0 = rslot + run_cap;
+    const uint32_t m = o.p.m();
+    for (uint32_t j = 0; j < n; j++) {
+      const bool cut = (j & (m - 1)) == 0;
+      if (cut) rg0[j >> o.p.m_log2] = n_runs;
+      if (cut || hslots[j] != hslots[j - 1]) {
+        rlo[n_runs] = j;
+        rslot[n_runs] = hslots[j];
+        n_runs++;
+      }
+    }
+    rlo[n_runs] = n;
+    rg0[G] = n_runs;
+    d.permuted = true;
+  } else {
+    par_memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
+    par_memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
+    for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
+    if (vs) {
+      par_memcpy(h + votes_at, vs->votes + lo, sizeof(tmv_vote) * n);
+      std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
+    } else if (mbytes) {
+      par_memcpy(h + L.msg, msg + base, mbytes);
+    }
+    if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
+    if (cached) std::memcpy(hslots, d.slots.data(), 4ull * n);
   }
-  tm.mark("keys", n);
+  tm.mark("stage", n);
   uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
   const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
   if (vs) {  // everything but the message region, which the device writes
@@ -815,8 +909,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
     return TMV_ERR_LAUNCH;
   }
   uint8_t *out = static_cast<uint8_t *>(d.d_out.ptr);
-  const LaunchOpts o = (sch == Scheme::Ed25519Cached || sch == Scheme::Sr25519Cached) ? LaunchOpts{}
-                                                                                         : make_opts(ctx, flags, n);
+  const uint32_t *dslots = reinterpret_cast<const uint32_t *>(dd + kind_at);
   int rc;
   switch (sch) {
     case Scheme::Ed25519:
@@ -827,8 +920,13 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
       break;
     case Scheme::Ed25519Cached:
     case Scheme::Sr25519Cached:
-      rc = launch_cached(d, sch == Scheme::Sr25519Cached, dd + L.pk, dd + L.sig, dd + L.msg, doff,
-                         reinterpret_cast<uint32_t *>(dd + kind_at), n, out, d.stream);
+      if (merged) {
+        const uint32_t *rlo = reinterpret_cast<const uint32_t *>(dd + runs_at);
+        const tmv::KeyRuns runs{rlo, rlo + run_cap + 1, rlo + 2 * run_cap + 1, n_runs};
+        rc = launch_key_merged(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, doff, dslots, runs, n, out, d.stream);
+      } else {
+        rc = launch_cached(d, sr, dd + L.pk, dd + L.sig, dd + L.msg, doff, dslots, n, out, d.stream);
+      }
       break;
     default:
       rc = launch_mixed(d, o, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out),
@@ -871,7 +969,12 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     (void)hipSetDevice(d.id);
     hipError_t e = hipStreamSynchronize(d.stream);
     if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
-    if (rc == 0) std::memcpy(out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
+    if (rc == 0 && d.permuted) {  // key-merged form: statuses in key order
+      const uint8_t *src = static_cast<const uint8_t *>(d.h_out.ptr);
+      for (uint32_t j = 0; j < bounds[s + 1] - bounds[s]; j++) out[bounds[s] + d.perm[j]] = src[j];
+    } else if (rc == 0) {
+      std::memcpy(out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
+    }
     if (rc == 0 && ctx->stats) collect_stats(ctx, d, d.stream);
   }
   tm.mark("synced", n);
@@ -947,7 +1050,7 @@ int tmv_verify_mixed_batch(tmv_ctx *ctx, const uint8_t *kind, const uint8_t *pk,
 
 int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
-  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0 && !(flags & TMV_FLAG_BATCH_EQUATION);
+  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0;
   Scheme sch;
   if (key_kind == TMV_KIND_ED25519) sch = cache ? Scheme::Ed25519Cached : Scheme::Ed25519;
   else if (key_kind == TMV_KIND_SR25519) sch = cache ? Scheme::Sr25519Cached : Scheme::Sr25519;
@@ -966,7 +1069,7 @@ int tmv_verify_votes(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const tmv_v
                      uint32_t n_tmpl, const tmv_vote *votes, const uint8_t *pk, const uint8_t *sig, uint32_t n,
                      int8_t *status_out) {
   if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
-  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0 && !(flags & TMV_FLAG_BATCH_EQUATION);
+  const bool cache = (flags & TMV_FLAG_KEY_CACHE) != 0;
   Scheme sch;
   if (key_kind == TMV_KIND_ED25519) sch = cache ? Scheme::Ed25519Cached : Scheme::Ed25519;
   else if (key_kind == TMV_KIND_SR25519) sch = cache ? Scheme::Sr25519Cached : Scheme::Sr25519;

@@ -107,6 +107,30 @@ hipError_t launch_gather(const BatchRefs &r, uint8_t *pk, uint8_t *sig, uint32_t
                          hipStream_t stream);
 hipError_t launch_scatter(const BatchRefs &r, const int8_t *status, hipStream_t stream);
 
+// Key-merged batch equation (msm.h): R decode + challenge with Niels(-R) in
+// w.niels, and the key-cached comb verification of the entries of failing
+// groups (passing groups' entries take their pre-check status).
+template <bool SR>
+hipError_t launch_prep_cached(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                              uint32_t n, const strobe_t *prefix, Ed25519Work w, int aligned, hipStream_t stream);
+template <bool SR>
+hipError_t launch_comb_fallback(const uint8_t *sig, const uint32_t *key_slot, uint32_t n, Ed25519Work w, KeyTable kt,
+                                const fe *bcomb, uint8_t *out, int aligned, const uint8_t *group_ok,
+                                uint32_t group_log2, hipStream_t stream);
+// Runs of one key inside a group, in key order: run r covers entries
+// [lo[r], lo[r + 1]) of key slot slot[r]; group g's runs are
+// [group_run0[g], group_run0[g + 1]).
+struct KeyRuns {
+  const uint32_t *lo;
+  const uint32_t *slot;
+  const uint32_t *group_run0;
+  uint32_t n_runs;
+};
+hipError_t launch_key_merged_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                   const uint32_t *msg_off, const uint32_t *key_slot, KeyRuns runs, uint32_t n,
+                                   KeyTable kt, const fe *bcomb, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                                   const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream);
+
 // Vote sign-bytes from templates (signbytes_kernels.hip, votes.h).
 struct VoteTab;
 hipError_t launch_vote_signbytes(const tmv_vote *votes, const VoteTab *tab, const uint8_t *blob,

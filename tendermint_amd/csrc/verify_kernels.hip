@@ -12,6 +12,7 @@
 #include "sr25519_core.h"
 #include "verify_kernels.h"
 #include "kernel_util.h"
+#include "comb.h"
 
 namespace tmv {
 
@@ -133,35 +134,6 @@ k_prep_hash(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, con
   uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
   kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
   kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
-}
-
-// Signed radix-16 recoding written straight to LDS (lanes with c >= 2 skip).
-__device__ __forceinline__ void recode16_store(int8_t *dst, const uint32_t s[8], bool store) {
-  int carry = 0;
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-    int e = (int)((s[i >> 3] >> (4 * (i & 7))) & 15) + carry;
-    if (i < 63) {
-      carry = (e + 8) >> 4;
-      e -= carry * 16;
-    }
-    if (store) dst[i] = (int8_t)e;
-  }
-}
-
-// Signed radix-256 recoding (32 digits in [-128, 127], top digit absorbs the
-// carry) for the fixed base B, written to LDS.
-__device__ __forceinline__ void recode256_store(int8_t *dst, const uint32_t s[8]) {
-  int carry = 0;
-#pragma unroll
-  for (int i = 0; i < 32; i++) {
-    int e = (int)((s[i >> 2] >> (8 * (i & 3))) & 255) + carry;
-    if (i < 31) {
-      carry = (e + 128) >> 8;
-      e -= carry * 256;
-    }
-    dst[i] = (int8_t)e;
-  }
 }
 
 constexpr int kQuadSigs = kQuadBlock / 4;
@@ -403,6 +375,15 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
   bool ok = SR ? ristretto_decode(P, r_w) : ge_decode_zip215(P, r_w);
   if (!ok) ge_p3_identity(P);
   w.flags[4 * i + 1] = ok ? 1 : 0;
+  if (w.niels) {  // -R in affine Niels form for the key-merged batch equation (point index i)
+    niels_pt np;
+    fe t;
+    fe_sub(t, P.Y, P.X); fe_carry(np.ypx, t);
+    fe_add(t, P.Y, P.X); fe_carry(np.ymx, t);
+    fe_mul(t, P.T, consts::d2()); fe_neg(np.xy2d, t);
+    np.pad[0] = np.pad[1] = 0;
+    w.niels[i] = np;
+  }
   fe *dst = w.Rc + 4ull * i;
   if (SR) {
     dst[0] = P.X; dst[1] = P.Y;
@@ -419,40 +400,13 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
   }
 }
 
-// The 96 table additions of the key-cached path with kCombAhead entries in
-// flight: the tables live in HBM / the Infinity Cache (a key is 80 KB), so
-// one entry of prefetch left the loop waiting on memory latency.
-constexpr int kCombAhead = 8;
-
-template <class EntryAt>
-__device__ __forceinline__ void comb_accumulate(fe &acc, const fe &idq, EntryAt entry_at) {
-  // named registers, not an array, so the ring stays out of scratch
-  fe b0, b1, b2, b3, b4, b5, b6, b7;
-  int d0, d1, d2, d3, d4, d5, d6, d7;
-  b0 = *entry_at(0, d0); b1 = *entry_at(1, d1); b2 = *entry_at(2, d2); b3 = *entry_at(3, d3);
-  b4 = *entry_at(4, d4); b5 = *entry_at(5, d5); b6 = *entry_at(6, d6); b7 = *entry_at(7, d7);
-  fe r;
-  auto step = [&](fe &b, int &d, int next) {
-    fe ent = b;
-    const int dd = d;
-    if (next < 96) b = *entry_at(next, d);
-    fe_cmov(ent, idq, dd == 0);
-    quad::cached_cneg(ent, dd < 0);
-    quad::add(r, acc, ent);
-    quad::p1p1_to_p3(acc, r);
-  };
-  for (int t0 = 0; t0 < 96; t0 += kCombAhead) {
-    step(b0, d0, t0 + 8); step(b1, d1, t0 + 9); step(b2, d2, t0 + 10); step(b3, d3, t0 + 11);
-    step(b4, d4, t0 + 12); step(b5, d5, t0 + 13); step(b6, d6, t0 + 14); step(b7, d7, t0 + 15);
-  }
-}
-
 // acc = sum_i e_i(k) 16^i(-A) [key comb] + sum_j d_j(s) 256^j B [base comb];
 // no doublings.  Table entries are prefetched kCombAhead additions ahead.
 template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_slot, uint32_t n, Ed25519Work w,
-              KeyTable kt, const fe *__restrict__ bcomb, uint8_t *__restrict__ out, int aligned) {
+              KeyTable kt, const fe *__restrict__ bcomb, uint8_t *__restrict__ out, int aligned,
+              const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
   __shared__ int8_t dig[kQuadSigs][2][64];
   if (blockIdx.x * kQuadSigs >= n) return;
   const int c = threadIdx.x & 3;
@@ -470,6 +424,16 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
 #pragma unroll
     for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
     s_ok = sc_is_canonical(s_w);
+  }
+  // key-merged batch equation held for this block's group (groups are >= 32
+  // entries: block-uniform): the pre-checks decide every entry
+  if (group_ok && group_ok[(blockIdx.x * kQuadSigs) >> group_log2]) {
+    if (!live || c != 0) return;
+    const bool a_ok = kt.ok[key_slot[i]] != 0;
+    const bool r_ok = w.flags[4 * i + 1] != 0;
+    const int status = SR ? (!a_ok ? -1 : (!s_ok ? -2 : (r_ok ? 1 : 0))) : ((a_ok && r_ok && s_ok) ? 1 : 0);
+    out[i] = (uint8_t)(int8_t)status;
+    return;
   }
   if (!s_ok) s_w[7] &= 0x0fffffffu;
   {
@@ -500,7 +464,7 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
     const int a = dsg < 0 ? -dsg : dsg;
     return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
   };
-  comb_accumulate(acc, idq, entry_at);
+  comb_accumulate<96>(acc, idq, entry_at);
   int status;
   if (SR) {
     const fe Rq = w.Rc[4ull * i + c];
@@ -621,7 +585,7 @@ k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict_
     const int a = dsg < 0 ? -dsg : dsg;
     return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
   };
-  comb_accumulate(acc, idq, entry_at);
+  comb_accumulate<96>(acc, idq, entry_at);
   __syncthreads();  // R decoded by wave 1
   const bool r_ok = rok[q] != 0;
   int status;
@@ -662,16 +626,46 @@ hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, 
                             msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
     return hipGetLastError();
   }
+  w.niels = nullptr;
   const uint32_t pblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
   if (sr) hipLaunchKernelGGL(k_prep_cached<true>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
   else hipLaunchKernelGGL(k_prep_cached<false>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  if (sr) hipLaunchKernelGGL(k_verify_comb<true>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned);
-  else hipLaunchKernelGGL(k_verify_comb<false>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned);
+  if (sr) hipLaunchKernelGGL(k_verify_comb<true>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned,
+                             nullptr, 0u);
+  else hipLaunchKernelGGL(k_verify_comb<false>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned,
+                          nullptr, 0u);
   return hipGetLastError();
 }
+
+template <bool SR>
+hipError_t launch_prep_cached(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                              uint32_t n, const strobe_t *prefix, Ed25519Work w, int aligned, hipStream_t stream) {
+  const uint32_t pblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
+  hipLaunchKernelGGL(k_prep_cached<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix,
+                     aligned);
+  return hipGetLastError();
+}
+template hipError_t launch_prep_cached<false>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
+                                              uint32_t, const strobe_t *, Ed25519Work, int, hipStream_t);
+template hipError_t launch_prep_cached<true>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
+                                             uint32_t, const strobe_t *, Ed25519Work, int, hipStream_t);
+
+template <bool SR>
+hipError_t launch_comb_fallback(const uint8_t *sig, const uint32_t *key_slot, uint32_t n, Ed25519Work w, KeyTable kt,
+                                const fe *bcomb, uint8_t *out, int aligned, const uint8_t *group_ok,
+                                uint32_t group_log2, hipStream_t stream) {
+  const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
+  hipLaunchKernelGGL(k_verify_comb<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out,
+                     aligned, group_ok, group_log2);
+  return hipGetLastError();
+}
+template hipError_t launch_comb_fallback<false>(const uint8_t *, const uint32_t *, uint32_t, Ed25519Work, KeyTable,
+                                                const fe *, uint8_t *, int, const uint8_t *, uint32_t, hipStream_t);
+template hipError_t launch_comb_fallback<true>(const uint8_t *, const uint32_t *, uint32_t, Ed25519Work, KeyTable,
+                                               const fe *, uint8_t *, int, const uint8_t *, uint32_t, hipStream_t);
 
 static int is_aligned(const void *a, const void *b) {
   return ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
