@@ -145,7 +145,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       for (int t = 0; t < 8; t++) s[t] = s_raw[t];
       s_ok = sc_is_canonical(s);
     }
-    const bool a_ok = KM ? key_ok[key_slot[e]] != 0 : w.flags[4 * e] != 0;
+    const bool a_ok = KM ? key_ok[key_slot[i]] != 0 : w.flags[4 * e] != 0;
     if (!(s_ok && a_ok && w.flags[4 * e + 1])) {  // left out of the sums
       if (KM) {
         uint4 *wd = reinterpret_cast<uint4 *>(mw.wscal + 8ull * e);
@@ -557,11 +557,11 @@ static hipError_t launch_km(const uint8_t *pk, const uint8_t *sig, const uint8_t
   if (n == 0) return hipSuccess;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
   w.niels = mw.pts;
-  hipError_t e = launch_prep_cached<SR>(pk, sig, msg, msg_off, n, prefix, w, aligned, stream);
+  hipError_t e = launch_prep_cached<SR>(pk, sig, msg, msg_off, runs.order, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
   const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
-  hipLaunchKernelGGL((k_msm_sort<SR, true>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, nullptr, nullptr, n,
-                     w, mw, p, seed, nullptr, aligned, key_slot, kt.ok);
+  hipLaunchKernelGGL((k_msm_sort<SR, true>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, runs.order, nullptr,
+                     n, w, mw, p, seed, nullptr, aligned, key_slot, kt.ok);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = launch_buckets(nullptr, n, mw, p, stream)) != hipSuccess) return e;
   const uint32_t n_items = runs.n_runs + p.groups;
@@ -570,7 +570,8 @@ static hipError_t launch_km(const uint8_t *pk, const uint8_t *sig, const uint8_t
   hipLaunchKernelGGL((k_msm_horner<SR, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, nullptr, n, mw, p,
                      runs.group_run0, runs.n_runs);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_comb_fallback<SR>(sig, key_slot, n, w, kt, bcomb, out, aligned, mw.group_ok, p.m_log2, stream);
+  return launch_comb_fallback<SR>(sig, key_slot, runs.order, n, w, kt, bcomb, out, aligned, mw.group_ok, p.m_log2,
+                                  stream);
 }
 
 hipError_t launch_key_merged_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,

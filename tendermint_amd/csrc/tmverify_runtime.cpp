@@ -144,13 +144,24 @@ struct Workspace {
   const uint32_t *counts = nullptr;  // mixed launches: per-kind entry counts on the device
 };
 
+// One lane of the host-buffer pipeline: a stream with its own pinned and
+// device staging.  Large host batches are cut into chunks that alternate
+// between two lanes, so chunk k+1's staging and H2D copy overlap chunk k's
+// kernels (the reference's "double-buffered hipMemcpyAsync on side streams").
+struct HostLane {
+  hipStream_t stream = nullptr;
+  DeviceBuf h_in, d_in, h_out, d_out;
+  uint32_t lo = 0, n = 0;  // chunk in flight (n == 0: idle)
+};
+constexpr int kLanes = 2;
+
 struct Device {
   int id = -1;
   hipStream_t stream = nullptr;
+  HostLane lane[kLanes];  // lane[0].stream == stream
   tmv::ge_precomp *d_btable = nullptr;   // 32x8 comb (single-lane kernel)
   tmv::fe *d_btab_q = nullptr;           // 8 x CachedQ multiples of B (quad kernel)
   tmv::strobe_t *d_prefix = nullptr;     // sr25519 transcript prefix (empty context)
-  DeviceBuf d_in, d_out, h_in, h_out;
   // one workspace per launch stream, so device-resident batches issued on
   // different caller streams run concurrently (the context's own stream is
   // one of them)
@@ -165,12 +176,12 @@ struct Device {
   std::vector<std::list<uint32_t>::iterator> kpos;
   std::vector<std::array<uint8_t, 33>> kslot_key;
   std::vector<uint64_t> kslot_epoch;
+  std::vector<uint8_t> kseen;  // resolve_keys: slots found, per lookup part
   uint64_t kepoch = 0, khits = 0, kmisses = 0;
   DeviceBuf d_kbuild, h_kbuild;
-  // host-buffer launches: key slots of the shard, and for the key-merged
-  // form the key order it was staged in (statuses come back in that order)
-  std::vector<uint32_t> slots, perm, key_count;
-  bool permuted = false;
+  // host-buffer launches: key slots of the shard and the per-chunk key
+  // histograms of the key-merged form's counting sort
+  std::vector<uint32_t> slots, key_count;
   std::mutex mu;
 };
 
@@ -189,6 +200,10 @@ uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk len
 // Key-cached batches up to this size run as one fused latency kernel
 // (TMV_CACHED_FUSED_MAX; commit-sized calls such as VerifyCommit).
 uint32_t g_cached_fused_max = 4096;
+// Host-buffer batches of at least this many entries per device are
+// pipelined in chunks (of half to one of these) over two lanes
+// (TMV_HOST_CHUNK).
+uint32_t g_host_chunk = 262144;
 
 void read_env() {
   static std::once_flag once;
@@ -202,6 +217,8 @@ void read_env() {
     if (mm) g_msm_min = (uint32_t)strtoul(mm, nullptr, 10);
     const char *cf = getenv("TMV_CACHED_FUSED_MAX");
     if (cf) g_cached_fused_max = (uint32_t)strtoul(cf, nullptr, 10);
+    const char *hc = getenv("TMV_HOST_CHUNK");
+    if (hc) g_host_chunk = (uint32_t)strtoul(hc, nullptr, 10);
     const char *mc = getenv("TMV_MSM_CHUNK");
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
   });
@@ -343,6 +360,11 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
   if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
+  d.lane[0].stream = d.stream;
+  for (int l = 1; l < kLanes; l++) {
+    e = hipStreamCreateWithFlags(&d.lane[l].stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
+  }
   std::vector<tmv::ge_precomp> table(tmv::kBaseTableRows * tmv::kBaseTableCols);
   tmv::build_base_table(table.data());
   const size_t bytes = table.size() * sizeof(tmv::ge_precomp);
@@ -442,38 +464,53 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   std::vector<uint32_t> miss_idx;
   std::vector<uint32_t> miss_slot;
   // 1) read-only lookups, in parallel for large batches (runs of one key
-  //    reuse the previous answer)
-  auto lookup = [&](uint32_t lo, uint32_t hi) {
+  //    reuse the previous answer); each part marks the slots it found and
+  //    counts its misses
+  constexpr uint32_t kParts = 16;
+  const uint32_t parts = n >= 16384 ? kParts : 1;
+  d.kseen.assign((size_t)parts * d.kcap, 0);
+  uint32_t misses[kParts] = {0};
+  auto lookup = [&](uint32_t part) {
+    const uint32_t lo = (uint32_t)((uint64_t)n * part / parts), hi = (uint32_t)((uint64_t)n * (part + 1) / parts);
+    uint8_t *seen = d.kseen.data() + (size_t)part * d.kcap;
     uint8_t key[33];
     key[0] = sr ? 1 : 0;
     const uint8_t *last_pk = nullptr;
-    uint32_t last_slot = UINT32_MAX;
+    uint32_t last_slot = UINT32_MAX, miss = 0;
     for (uint32_t i = lo; i < hi; i++) {
       const uint8_t *p = pk + 32ull * i;
-      if (last_pk && std::memcmp(p, last_pk, 32) == 0) { slots_out[i] = last_slot; continue; }
+      if (last_pk && std::memcmp(p, last_pk, 32) == 0) {
+        slots_out[i] = last_slot;
+        miss += last_slot == UINT32_MAX;
+        continue;
+      }
       std::memcpy(key + 1, p, 32);
       last_slot = slots_out[i] = d.kindex.find(key);
       last_pk = p;
+      if (last_slot == UINT32_MAX) miss++;
+      else seen[last_slot] = 1;
     }
+    misses[part] = miss;
   };
-  if (n >= 16384) {
-    const uint32_t parts = 16;
-    tmh::parallel_for_n(parts, 8, [&](size_t t) {
-      lookup((uint32_t)((uint64_t)n * t / parts), (uint32_t)((uint64_t)n * (t + 1) / parts));
-    });
-  } else {
-    lookup(0, n);
-  }
+  if (parts > 1) tmh::parallel_for_n(parts, kParts, lookup);
+  else lookup(0);
+  uint32_t n_miss = 0;
+  for (uint32_t t = 0; t < parts; t++) n_miss += misses[t];
   // 2) pin every key found to this batch (epoch) before any miss may evict
   uint32_t distinct = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    const uint32_t slot = slots_out[i];
-    if (slot == UINT32_MAX || d.kslot_epoch[slot] == epoch) continue;
+  for (uint32_t slot = 0; slot < d.kcap; slot++) {
+    bool hit = false;
+    for (uint32_t t = 0; t < parts && !hit; t++) hit = d.kseen[(size_t)t * d.kcap + slot] != 0;
+    if (!hit) continue;
     d.kslot_epoch[slot] = epoch;
     distinct++;
     d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
     d.khits++;
   }
+  if (n_miss == 0) return 0;
+  // new keys may evict slots: let chunks still in flight on other lanes finish
+  for (HostLane &l : d.lane)
+    if (l.n && l.stream != s) (void)hipStreamSynchronize(l.stream);
   // 3) misses.  First decide, before touching the index, whether the batch
   //    fits: bailing out after inserting keys whose tables were never built
   //    would leave stale entries behind.
@@ -735,9 +772,13 @@ void tmv_close(tmv_ctx *ctx) {
   if (!ctx) return;
   for (auto &d : ctx->devs) {
     (void)hipSetDevice(d->id);
-    if (d->stream) (void)hipStreamSynchronize(d->stream);
-    d->d_in.release();
-    d->d_out.release();
+    for (HostLane &l : d->lane) {
+      if (l.stream) (void)hipStreamSynchronize(l.stream);
+      l.d_in.release();
+      l.d_out.release();
+      l.h_in.release();
+      l.h_out.release();
+    }
     for (auto &kv : d->ws) {
       if (kv.second->done) (void)hipEventSynchronize(kv.second->done);
       kv.second->work.release();
@@ -757,9 +798,9 @@ void tmv_close(tmv_ctx *ctx) {
     if (d->d_prefix) (void)hipFree(d->d_prefix);
     if (d->d_btab_q) (void)hipFree(d->d_btab_q);
     if (d->work_done) (void)hipEventDestroy(d->work_done);
-    d->h_in.release();
-    d->h_out.release();
     if (d->d_btable) (void)hipFree(d->d_btable);
+    for (int l = 1; l < kLanes; l++)
+      if (d->lane[l].stream) (void)hipStreamDestroy(d->lane[l].stream);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
@@ -782,10 +823,11 @@ struct VoteSrc {
 
 // Stage one contiguous shard [lo, hi) to device d and launch; does not sync.
 // Layout: pk | sig | off | msg | kind or key slots | votes | templates | key
-// runs (16-B aligned pieces).  Key-cached batches resolve their slots first;
-// when they take the key-merged batch equation the shard is staged in key
-// order (d.perm) and run_batch puts the statuses back.
-static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch, const uint8_t *kind,
+// runs | key order (16-B aligned pieces).  Key-cached batches resolve their
+// slots first; the key-merged batch equation gets the key order of the
+// entries (a counting sort by slot) and the runs of one key inside a group,
+// and its kernels read the entries through that order.
+static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &ln, Scheme sch, const uint8_t *kind,
                             const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                             uint32_t lo, uint32_t hi, const VoteSrc *vs) {
   const uint32_t n = hi - lo;
@@ -796,10 +838,9 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   EngineTimer tm;
-  d.permuted = false;
   if (cached) {
     d.slots.resize(n);
-    const int kr = resolve_keys(d, sr, pk + 32ull * lo, n, d.slots.data(), d.stream);
+    const int kr = resolve_keys(d, sr, pk + 32ull * lo, n, d.slots.data(), ln.stream);
     if (kr < 0) return kr;
     if (kr == 1) {  // more distinct keys than the cache holds: uncached path
       sch = sr ? Scheme::Sr25519 : Scheme::Ed25519;
@@ -810,11 +851,23 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
   LaunchOpts o = make_opts(ctx, flags, n, cached);
   // key-merged form: worth it while a group holds few keys (runs <= n / 2)
   bool merged = cached && o.batch_eq;
-  if (merged) {
-    d.key_count.assign((size_t)d.kcap + 1, 0);
-    for (uint32_t i = 0; i < n; i++) d.key_count[d.slots[i] + 1]++;
-    uint32_t distinct = 0;
-    for (uint32_t k = 1; k <= d.kcap; k++) distinct += d.key_count[k] != 0;
+  uint32_t distinct = 0;
+  const uint32_t kc = d.kcap;
+  constexpr uint32_t kSortChunks = 16;
+  if (merged) {  // per-chunk key histograms (parallel), for a stable counting sort
+    d.key_count.assign((size_t)kSortChunks * kc, 0);
+    const uint32_t *sl = d.slots.data();
+    uint32_t *hist = d.key_count.data();
+    tmh::parallel_for_n(kSortChunks, kSortChunks, [&](size_t c) {
+      const uint32_t j0 = (uint32_t)((uint64_t)n * c / kSortChunks), j1 = (uint32_t)((uint64_t)n * (c + 1) / kSortChunks);
+      uint32_t *hc = hist + c * kc;
+      for (uint32_t j = j0; j < j1; j++) hc[sl[j]]++;
+    });
+    for (uint32_t k = 0; k < kc; k++) {
+      uint32_t t = 0;
+      for (uint32_t c = 0; c < kSortChunks; c++) t += hist[(size_t)c * kc + k];
+      distinct += t != 0;
+    }
     if ((uint64_t)distinct + o.p.groups > n / 2) merged = false;
   }
   if (cached && !merged) o.batch_eq = false;  // key-cached per-entry path
@@ -823,117 +876,117 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, Scheme sch,
   const size_t votes_at = L.total + (sch == Scheme::Mixed ? align16(n) : 0) + (cached ? align16(4ull * n) : 0);
   const size_t tab_at = votes_at + (vs ? align16(sizeof(tmv_vote) * n) : 0);
   const size_t runs_at = tab_at + (vs ? align16(vs->tab_bytes) : 0);
-  const size_t run_cap = (size_t)n + G;  // runs never exceed entries + group cuts
-  const size_t total = runs_at + (merged ? align16(4ull * (2 * run_cap + 1 + G + 1)) : 0);
-  if ((e = d.h_in.ensure(total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
-  if ((e = d.d_in.ensure(total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
-  if ((e = d.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
-  if ((e = d.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
-  uint8_t *h = static_cast<uint8_t *>(d.h_in.ptr);
+  const size_t run_cap = (size_t)distinct + G;  // key segments cut at group edges
+  const size_t order_at = runs_at + align16(4ull * (2 * run_cap + 1 + G + 1));
+  const size_t total = merged ? order_at + align16(4ull * n) : runs_at;
+  if ((e = ln.h_in.ensure(total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = ln.d_in.ensure(total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = ln.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = ln.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  uint8_t *h = static_cast<uint8_t *>(ln.h_in.ptr);
   uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
-  uint32_t *hslots = reinterpret_cast<uint32_t *>(h + kind_at);
   const uint32_t base = msg_off[lo];
+  par_memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
+  par_memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
+  for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
+  if (vs) {
+    par_memcpy(h + votes_at, vs->votes + lo, sizeof(tmv_vote) * n);
+    std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
+  } else if (mbytes) {
+    par_memcpy(h + L.msg, msg + base, mbytes);
+  }
+  if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
+  if (cached) std::memcpy(h + kind_at, d.slots.data(), 4ull * n);
   uint32_t n_runs = 0;
   if (merged) {
-    // stable counting sort by key slot
-    for (uint32_t k = 1; k <= d.kcap; k++) d.key_count[k] += d.key_count[k - 1];
-    d.perm.resize(n);
-    for (uint32_t i = 0; i < n; i++) d.perm[d.key_count[d.slots[i]]++] = i;
-    off[0] = 0;
-    for (uint32_t j = 0; j < n; j++) {
-      const uint32_t i = lo + d.perm[j];
-      off[j + 1] = off[j] + (msg_off[i + 1] - msg_off[i]);
-    }
-    const uint32_t *perm = d.perm.data();
-    const uint32_t *slots = d.slots.data();
-    tmh::parallel_for_n((n + 4095) / 4096, 16, [&](size_t c) {
-      const uint32_t j1 = std::min<uint32_t>(n, (uint32_t)(c + 1) * 4096);
-      for (uint32_t j = (uint32_t)c * 4096; j < j1; j++) {
-        const uint32_t i = perm[j];
-        std::memcpy(h + L.pk + 32ull * j, pk + 32ull * (lo + i), 32);
-        std::memcpy(h + L.sig + 64ull * j, sig + 64ull * (lo + i), 64);
-        hslots[j] = slots[i];
-        if (vs) std::memcpy(h + votes_at + sizeof(tmv_vote) * j, vs->votes + lo + i, sizeof(tmv_vote));
-        else if (mbytes) std::memcpy(h + L.msg + off[j], msg + msg_off[lo + i], off[j + 1] - off[j]);
+    // key order of the work slots: stable counting sort, chunks scattered in parallel
+    uint32_t *hist = d.key_count.data();
+    std::vector<uint32_t> key_start(kc + 1);
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < kc; k++) {
+      key_start[k] = run;
+      for (uint32_t c = 0; c < kSortChunks; c++) {
+        const uint32_t v = hist[(size_t)c * kc + k];
+        hist[(size_t)c * kc + k] = run;
+        run += v;
       }
+    }
+    key_start[kc] = run;
+    uint32_t *order = reinterpret_cast<uint32_t *>(h + order_at);
+    const uint32_t *sl = d.slots.data();
+    tmh::parallel_for_n(kSortChunks, kSortChunks, [&](size_t c) {
+      const uint32_t j0 = (uint32_t)((uint64_t)n * c / kSortChunks), j1 = (uint32_t)((uint64_t)n * (c + 1) / kSortChunks);
+      uint32_t *cur = hist + c * kc;
+      for (uint32_t j = j0; j < j1; j++) order[cur[sl[j]]++] = j;
     });
-    if (vs) std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
-    // runs of one key inside a group
+    // runs: key segments [key_start[k], key_start[k+1]) cut at group edges
     uint32_t *rlo = reinterpret_cast<uint32_t *>(h + runs_at);
     uint32_t *rslot = rlo + run_cap + 1;
     uint32_t *rg0 = rslot + run_cap;
     const uint32_t m = o.p.m();
-    for (uint32_t j = 0; j < n; j++) {
-      const bool cut = (j & (m - 1)) == 0;
-      if (cut) rg0[j >> o.p.m_log2] = n_runs;
-      if (cut || hslots[j] != hslots[j - 1]) {
-        rlo[n_runs] = j;
-        rslot[n_runs] = hslots[j];
+    uint32_t g = 0;
+    for (uint32_t k = 0; k < kc; k++) {
+      uint32_t a0 = key_start[k];
+      const uint32_t a1 = key_start[k + 1];
+      while (a0 < a1) {
+        while (g < G && (g << o.p.m_log2) <= a0) rg0[g++] = n_runs;
+        rlo[n_runs] = a0;
+        rslot[n_runs] = k;
         n_runs++;
+        a0 = std::min(a1, (a0 / m + 1) * m);
       }
     }
+    while (g < G) rg0[g++] = n_runs;
     rlo[n_runs] = n;
     rg0[G] = n_runs;
-    d.permuted = true;
-  } else {
-    par_memcpy(h + L.pk, pk + 32ull * lo, 32ull * n);
-    par_memcpy(h + L.sig, sig + 64ull * lo, 64ull * n);
-    for (uint32_t i = 0; i <= n; i++) off[i] = msg_off[lo + i] - base;
-    if (vs) {
-      par_memcpy(h + votes_at, vs->votes + lo, sizeof(tmv_vote) * n);
-      std::memcpy(h + tab_at, vs->tab, vs->tab_bytes);
-    } else if (mbytes) {
-      par_memcpy(h + L.msg, msg + base, mbytes);
-    }
-    if (sch == Scheme::Mixed) std::memcpy(h + kind_at, kind + lo, n);
-    if (cached) std::memcpy(hslots, d.slots.data(), 4ull * n);
   }
   tm.mark("stage", n);
-  uint8_t *dd = static_cast<uint8_t *>(d.d_in.ptr);
+  uint8_t *dd = static_cast<uint8_t *>(ln.d_in.ptr);
   const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
   if (vs) {  // everything but the message region, which the device writes
-    if ((e = hipMemcpyAsync(dd, h, L.msg, hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(dd + L.total, h + L.total, total - L.total, hipMemcpyHostToDevice, d.stream)) !=
+    if ((e = hipMemcpyAsync(dd, h, L.msg, hipMemcpyHostToDevice, ln.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(dd + L.total, h + L.total, total - L.total, hipMemcpyHostToDevice, ln.stream)) !=
             hipSuccess) {
       set_error("hipMemcpyAsync(H2D)", e);
       return TMV_ERR_LAUNCH;
     }
     const tmv::VoteTab *tab = reinterpret_cast<const tmv::VoteTab *>(dd + tab_at);
     if ((e = tmv::launch_vote_signbytes(reinterpret_cast<const tmv_vote *>(dd + votes_at), tab,
-                                        dd + tab_at + vs->blob_at, doff, n, dd + L.msg, d.stream)) != hipSuccess) {
+                                        dd + tab_at + vs->blob_at, doff, n, dd + L.msg, ln.stream)) != hipSuccess) {
       set_error("k_vote_signbytes", e);
       return TMV_ERR_LAUNCH;
     }
-  } else if ((e = hipMemcpyAsync(d.d_in.ptr, h, total, hipMemcpyHostToDevice, d.stream)) != hipSuccess) {
+  } else if ((e = hipMemcpyAsync(ln.d_in.ptr, h, total, hipMemcpyHostToDevice, ln.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
   }
-  uint8_t *out = static_cast<uint8_t *>(d.d_out.ptr);
+  uint8_t *out = static_cast<uint8_t *>(ln.d_out.ptr);
   const uint32_t *dslots = reinterpret_cast<const uint32_t *>(dd + kind_at);
   int rc;
   switch (sch) {
     case Scheme::Ed25519:
-      rc = launch_ed25519(d, o, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, out, d.stream);
+      rc = launch_ed25519(d, o, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, out, ln.stream);
       break;
     case Scheme::Sr25519:
-      rc = launch_sr25519(d, o, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out), d.stream);
+      rc = launch_sr25519(d, o, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out), ln.stream);
       break;
     case Scheme::Ed25519Cached:
     case Scheme::Sr25519Cached:
       if (merged) {
         const uint32_t *rlo = reinterpret_cast<const uint32_t *>(dd + runs_at);
-        const tmv::KeyRuns runs{rlo, rlo + run_cap + 1, rlo + 2 * run_cap + 1, n_runs};
-        rc = launch_key_merged(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, doff, dslots, runs, n, out, d.stream);
+        const tmv::KeyRuns runs{rlo, rlo + run_cap + 1, rlo + 2 * run_cap + 1,
+                                reinterpret_cast<const uint32_t *>(dd + order_at), n_runs};
+        rc = launch_key_merged(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, doff, dslots, runs, n, out, ln.stream);
       } else {
-        rc = launch_cached(d, sr, dd + L.pk, dd + L.sig, dd + L.msg, doff, dslots, n, out, d.stream);
+        rc = launch_cached(d, sr, dd + L.pk, dd + L.sig, dd + L.msg, doff, dslots, n, out, ln.stream);
       }
       break;
     default:
       rc = launch_mixed(d, o, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg, doff, n, reinterpret_cast<int8_t *>(out),
-                        d.stream);
+                        ln.stream);
   }
   if (rc != 0) return rc;
-  if ((e = hipMemcpyAsync(d.h_out.ptr, d.d_out.ptr, n, hipMemcpyDeviceToHost, d.stream)) != hipSuccess) {
+  if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(D2H)", e);
     return TMV_ERR_LAUNCH;
   }
@@ -959,23 +1012,53 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   std::vector<uint32_t> bounds(shards + 1);
   for (uint32_t s = 0; s <= shards; s++) bounds[s] = (uint32_t)((uint64_t)n * s / shards);
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
+  // each shard is cut into chunks of up to g_host_chunk entries, alternating
+  // between the device's lanes
+  read_env();
+  // (chunks of at least g_host_chunk / 2 entries: at least 4 once there is
+  // room, then g_host_chunk each; fewer, larger chunks keep the key-merged
+  // form's per-chunk sort and launch chain cheap)
+  const uint32_t chunk = std::max<uint32_t>(2048, g_host_chunk);
+  std::vector<uint32_t> nchunks(shards);
+  uint32_t max_chunks = 0;
+  for (uint32_t s = 0; s < shards; s++) {
+    const uint32_t len = bounds[s + 1] - bounds[s];
+    nchunks[s] = std::max<uint32_t>(1, std::min<uint32_t>(len / (chunk / 2), std::max<uint32_t>(4, len / chunk)));
+    max_chunks = std::max(max_chunks, nchunks[s]);
+  }
   int rc = 0;
   EngineTimer tm;
-  for (uint32_t s = 0; s < shards && rc == 0; s++)
-    rc = stage_and_launch(ctx, flags, *ctx->devs[s], sch, kind, pk, sig, msg, msg_off, bounds[s], bounds[s + 1], vs);
+  auto harvest = [&](Device &d, HostLane &ln) {
+    if (ln.n == 0) return;
+    hipError_t e = hipStreamSynchronize(ln.stream);
+    if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
+    if (rc == 0) std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
+    if (rc == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
+    ln.n = 0;
+  };
+  for (uint32_t k = 0; k < max_chunks && rc == 0; k++) {
+    for (uint32_t s = 0; s < shards && rc == 0; s++) {
+      if (k >= nchunks[s]) continue;
+      Device &d = *ctx->devs[s];
+      const uint32_t len = bounds[s + 1] - bounds[s];
+      const uint32_t c0 = bounds[s] + (uint32_t)((uint64_t)len * k / nchunks[s]);
+      const uint32_t c1 = bounds[s] + (uint32_t)((uint64_t)len * (k + 1) / nchunks[s]);
+      HostLane &ln = d.lane[k % kLanes];
+      (void)hipSetDevice(d.id);
+      harvest(d, ln);  // the lane's previous chunk
+      if (rc != 0) break;
+      rc = stage_and_launch(ctx, flags, d, ln, sch, kind, pk, sig, msg, msg_off, c0, c1, vs);
+      if (rc == 0) { ln.lo = c0; ln.n = c1 - c0; }
+    }
+  }
   tm.mark("launched", n);
   for (uint32_t s = 0; s < shards; s++) {
     Device &d = *ctx->devs[s];
     (void)hipSetDevice(d.id);
-    hipError_t e = hipStreamSynchronize(d.stream);
-    if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
-    if (rc == 0 && d.permuted) {  // key-merged form: statuses in key order
-      const uint8_t *src = static_cast<const uint8_t *>(d.h_out.ptr);
-      for (uint32_t j = 0; j < bounds[s + 1] - bounds[s]; j++) out[bounds[s] + d.perm[j]] = src[j];
-    } else if (rc == 0) {
-      std::memcpy(out + bounds[s], d.h_out.ptr, bounds[s + 1] - bounds[s]);
+    for (HostLane &ln : d.lane) {
+      if (rc != 0) { if (ln.n) (void)hipStreamSynchronize(ln.stream); ln.n = 0; continue; }
+      harvest(d, ln);
     }
-    if (rc == 0 && ctx->stats) collect_stats(ctx, d, d.stream);
   }
   tm.mark("synced", n);
   if (rc != 0) return rc;

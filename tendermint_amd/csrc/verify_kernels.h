@@ -110,20 +110,24 @@ hipError_t launch_scatter(const BatchRefs &r, const int8_t *status, hipStream_t 
 // Key-merged batch equation (msm.h): R decode + challenge with Niels(-R) in
 // w.niels, and the key-cached comb verification of the entries of failing
 // groups (passing groups' entries take their pre-check status).
+// With idx, work slot e reads entry idx[e] (the key order) and writes the
+// status of idx[e]; per-entry work arrays are indexed by e.
 template <bool SR>
 hipError_t launch_prep_cached(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                              uint32_t n, const strobe_t *prefix, Ed25519Work w, int aligned, hipStream_t stream);
+                              const uint32_t *idx, uint32_t n, const strobe_t *prefix, Ed25519Work w, int aligned,
+                              hipStream_t stream);
 template <bool SR>
-hipError_t launch_comb_fallback(const uint8_t *sig, const uint32_t *key_slot, uint32_t n, Ed25519Work w, KeyTable kt,
-                                const fe *bcomb, uint8_t *out, int aligned, const uint8_t *group_ok,
-                                uint32_t group_log2, hipStream_t stream);
-// Runs of one key inside a group, in key order: run r covers entries
+hipError_t launch_comb_fallback(const uint8_t *sig, const uint32_t *key_slot, const uint32_t *idx, uint32_t n,
+                                Ed25519Work w, KeyTable kt, const fe *bcomb, uint8_t *out, int aligned,
+                                const uint8_t *group_ok, uint32_t group_log2, hipStream_t stream);
+// Runs of one key inside a group, in key order: run r covers work slots
 // [lo[r], lo[r + 1]) of key slot slot[r]; group g's runs are
-// [group_run0[g], group_run0[g + 1]).
+// [group_run0[g], group_run0[g + 1]).  order[e] is the entry at work slot e.
 struct KeyRuns {
   const uint32_t *lo;
   const uint32_t *slot;
   const uint32_t *group_run0;
+  const uint32_t *order;
   uint32_t n_runs;
 };
 hipError_t launch_key_merged_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,

@@ -345,12 +345,13 @@ k_key_build(const uint8_t *__restrict__ keys, const uint32_t *__restrict__ slots
 template <bool SR>
 __global__ void __launch_bounds__(kVerifyBlock)
 k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
-              const uint32_t *__restrict__ msg_off, uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix,
-              int aligned) {
+              const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, uint32_t n, Ed25519Work w,
+              const strobe_t *__restrict__ prefix, int aligned) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= 2 * n) return;
   const uint32_t task = j / n;
-  const uint32_t i = j - task * n;
+  const uint32_t e = j - task * n;  // work slot; the entry read is idx[e] (key order) or e
+  const uint32_t i = idx ? idx[e] : e;
   uint32_t a_w[8], r_w[8];
   if (aligned) load_words_aligned(r_w, sig + 64ull * i);
   else load_words_unaligned(r_w, sig + 64ull * i);
@@ -366,7 +367,7 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
       sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
       sc_reduce512(k, h);
     }
-    uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * i);
+    uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
     kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
     kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
     return;
@@ -374,17 +375,17 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
   ge_p3 P;
   bool ok = SR ? ristretto_decode(P, r_w) : ge_decode_zip215(P, r_w);
   if (!ok) ge_p3_identity(P);
-  w.flags[4 * i + 1] = ok ? 1 : 0;
-  if (w.niels) {  // -R in affine Niels form for the key-merged batch equation (point index i)
+  w.flags[4 * e + 1] = ok ? 1 : 0;
+  if (w.niels) {  // -R in affine Niels form for the key-merged batch equation (point index e)
     niels_pt np;
     fe t;
     fe_sub(t, P.Y, P.X); fe_carry(np.ypx, t);
     fe_add(t, P.Y, P.X); fe_carry(np.ymx, t);
     fe_mul(t, P.T, consts::d2()); fe_neg(np.xy2d, t);
     np.pad[0] = np.pad[1] = 0;
-    w.niels[i] = np;
+    w.niels[e] = np;
   }
-  fe *dst = w.Rc + 4ull * i;
+  fe *dst = w.Rc + 4ull * e;
   if (SR) {
     dst[0] = P.X; dst[1] = P.Y;
     fe t; fe_one(t); dst[2] = t;
@@ -404,16 +405,17 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
 // no doublings.  Table entries are prefetched kCombAhead additions ahead.
 template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
-k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_slot, uint32_t n, Ed25519Work w,
-              KeyTable kt, const fe *__restrict__ bcomb, uint8_t *__restrict__ out, int aligned,
-              const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
+k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_slot, const uint32_t *__restrict__ idx,
+              uint32_t n, Ed25519Work w, KeyTable kt, const fe *__restrict__ bcomb, uint8_t *__restrict__ out,
+              int aligned, const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
   __shared__ int8_t dig[kQuadSigs][2][64];
   if (blockIdx.x * kQuadSigs >= n) return;
   const int c = threadIdx.x & 3;
   const int q = threadIdx.x >> 2;
   const uint32_t raw = blockIdx.x * kQuadSigs + q;
   const bool live = raw < n;
-  const uint32_t i = live ? raw : n - 1;
+  const uint32_t e = live ? raw : n - 1;  // work slot (key order with idx)
+  const uint32_t i = idx ? idx[e] : e;    // entry: input rows, key slot, status
   uint32_t s_raw[8], s_w[8];
   if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
   else load_words_unaligned(s_raw, sig + 64ull * i + 32);
@@ -430,7 +432,7 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
   if (group_ok && group_ok[(blockIdx.x * kQuadSigs) >> group_log2]) {
     if (!live || c != 0) return;
     const bool a_ok = kt.ok[key_slot[i]] != 0;
-    const bool r_ok = w.flags[4 * i + 1] != 0;
+    const bool r_ok = w.flags[4 * e + 1] != 0;
     const int status = SR ? (!a_ok ? -1 : (!s_ok ? -2 : (r_ok ? 1 : 0))) : ((a_ok && r_ok && s_ok) ? 1 : 0);
     out[i] = (uint8_t)(int8_t)status;
     return;
@@ -438,7 +440,7 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
   if (!s_ok) s_w[7] &= 0x0fffffffu;
   {
     uint32_t k_w[8];
-    const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * i);
+    const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * e);
     const uint4 k0 = kp[0], k1 = kp[1];
     k_w[0] = k0.x; k_w[1] = k0.y; k_w[2] = k0.z; k_w[3] = k0.w;
     k_w[4] = k1.x; k_w[5] = k1.y; k_w[6] = k1.z; k_w[7] = k1.w;
@@ -448,7 +450,7 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
   __syncthreads();
   const uint32_t slot = key_slot[i];
   const bool a_ok = kt.ok[slot] != 0;
-  const bool r_ok = w.flags[4 * i + 1] != 0;
+  const bool r_ok = w.flags[4 * e + 1] != 0;
   const fe *krow = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
   fe acc, r, idq;
   quad::p3_identity(acc);
@@ -467,11 +469,11 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
   comb_accumulate<96>(acc, idq, entry_at);
   int status;
   if (SR) {
-    const fe Rq = w.Rc[4ull * i + c];
+    const fe Rq = w.Rc[4ull * e + c];
     const bool eq = quad::ristretto_equal(acc, Rq);
     status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
   } else {
-    fe Rq = w.Rc[4ull * i + c];
+    fe Rq = w.Rc[4ull * e + c];
     quad::cached_cneg(Rq, true);
     quad::add(r, acc, Rq);
     quad::p1p1_to_p3(acc, r);
@@ -628,44 +630,49 @@ hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, 
   }
   w.niels = nullptr;
   const uint32_t pblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
-  if (sr) hipLaunchKernelGGL(k_prep_cached<true>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
-  else hipLaunchKernelGGL(k_prep_cached<false>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix, aligned);
+  if (sr) hipLaunchKernelGGL(k_prep_cached<true>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, nullptr, n, w, prefix, aligned);
+  else hipLaunchKernelGGL(k_prep_cached<false>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, nullptr, n, w, prefix, aligned);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  if (sr) hipLaunchKernelGGL(k_verify_comb<true>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned,
-                             nullptr, 0u);
-  else hipLaunchKernelGGL(k_verify_comb<false>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out, aligned,
-                          nullptr, 0u);
+  if (sr) hipLaunchKernelGGL(k_verify_comb<true>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, nullptr, n, w, kt, bcomb, out,
+                             aligned, nullptr, 0u);
+  else hipLaunchKernelGGL(k_verify_comb<false>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, nullptr, n, w, kt, bcomb, out,
+                          aligned, nullptr, 0u);
   return hipGetLastError();
 }
 
 template <bool SR>
 hipError_t launch_prep_cached(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                              uint32_t n, const strobe_t *prefix, Ed25519Work w, int aligned, hipStream_t stream) {
+                              const uint32_t *idx, uint32_t n, const strobe_t *prefix, Ed25519Work w, int aligned,
+                              hipStream_t stream) {
   const uint32_t pblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
-  hipLaunchKernelGGL(k_prep_cached<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, n, w, prefix,
-                     aligned);
+  hipLaunchKernelGGL(k_prep_cached<SR>, dim3(pblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx, n, w,
+                     prefix, aligned);
   return hipGetLastError();
 }
 template hipError_t launch_prep_cached<false>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
-                                              uint32_t, const strobe_t *, Ed25519Work, int, hipStream_t);
+                                              const uint32_t *, uint32_t, const strobe_t *, Ed25519Work, int,
+                                              hipStream_t);
 template hipError_t launch_prep_cached<true>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
-                                             uint32_t, const strobe_t *, Ed25519Work, int, hipStream_t);
+                                             const uint32_t *, uint32_t, const strobe_t *, Ed25519Work, int,
+                                             hipStream_t);
 
 template <bool SR>
-hipError_t launch_comb_fallback(const uint8_t *sig, const uint32_t *key_slot, uint32_t n, Ed25519Work w, KeyTable kt,
-                                const fe *bcomb, uint8_t *out, int aligned, const uint8_t *group_ok,
-                                uint32_t group_log2, hipStream_t stream) {
+hipError_t launch_comb_fallback(const uint8_t *sig, const uint32_t *key_slot, const uint32_t *idx, uint32_t n,
+                                Ed25519Work w, KeyTable kt, const fe *bcomb, uint8_t *out, int aligned,
+                                const uint8_t *group_ok, uint32_t group_log2, hipStream_t stream) {
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  hipLaunchKernelGGL(k_verify_comb<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, n, w, kt, bcomb, out,
-                     aligned, group_ok, group_log2);
+  hipLaunchKernelGGL(k_verify_comb<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, key_slot, idx, n, w, kt, bcomb,
+                     out, aligned, group_ok, group_log2);
   return hipGetLastError();
 }
-template hipError_t launch_comb_fallback<false>(const uint8_t *, const uint32_t *, uint32_t, Ed25519Work, KeyTable,
-                                                const fe *, uint8_t *, int, const uint8_t *, uint32_t, hipStream_t);
-template hipError_t launch_comb_fallback<true>(const uint8_t *, const uint32_t *, uint32_t, Ed25519Work, KeyTable,
-                                               const fe *, uint8_t *, int, const uint8_t *, uint32_t, hipStream_t);
+template hipError_t launch_comb_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
+                                                Ed25519Work, KeyTable, const fe *, uint8_t *, int, const uint8_t *,
+                                                uint32_t, hipStream_t);
+template hipError_t launch_comb_fallback<true>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
+                                               Ed25519Work, KeyTable, const fe *, uint8_t *, int, const uint8_t *,
+                                               uint32_t, hipStream_t);
 
 static int is_aligned(const void *a, const void *b) {
   return ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;

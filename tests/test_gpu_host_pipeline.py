@@ -1,0 +1,79 @@
+"""Host-buffer pipeline: batches of at least two chunks (TMV_HOST_CHUNK)
+alternate between two staging lanes, so chunk k+1's staging and copy overlap
+chunk k's kernels.  Every path must still give the oracle's vector, in
+order, across chunk edges, with key builds and evictions between chunks."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CODE = r"""
+import random, sys, numpy as np
+sys.path.insert(0, '.'); sys.path.insert(0, 'oracle'); sys.path.insert(0, 'tests')
+import oracle_c as C
+import vote_cases as V
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import Batch, make_c2_batch, make_sr25519_batch
+from test_gpu_key_merged import _keyed_batch
+ctx = N.Context(1)
+ED, SR = N.TMV_KIND_ED25519, N.TMV_KIND_SR25519
+
+# uncached: per entry and batch equation, ragged chunk edges
+b = make_c2_batch(10000, seed=81, edge_scale=3.0)
+_, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+for flags in (N.TMV_FLAG_PER_ENTRY, N.TMV_FLAG_BATCH_EQUATION):
+    ok, st = ctx.verify_batch_ex(ED, flags, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st.astype(np.uint8), ref), flags
+ok, st = ctx.ed25519_verify_batch(b.pk, b.sig, b.msg, b.off)
+assert np.array_equal(st.astype(np.uint8), ref)
+
+# key cache: per entry and key-merged, keys spread over the chunks
+k = _keyed_batch(12000, 150, 82, bad={3, 4100, 9000, 11999})
+_, kref = C.ed25519_verify_packed(k.pk, k.sig, k.msg, k.off, threads=8)
+for flags in (N.TMV_FLAG_KEY_CACHE | N.TMV_FLAG_PER_ENTRY, N.TMV_FLAG_KEY_CACHE | N.TMV_FLAG_BATCH_EQUATION):
+    for _ in range(2):
+        ok, st = ctx.verify_batch_ex(ED, flags, k.pk, k.sig, k.msg, k.off)
+        assert np.array_equal(st.astype(np.uint8), kref), flags
+
+# sr25519
+s = make_sr25519_batch(5000, seed=83, bad_frac=0.02)
+sref = C.sr25519_status_packed(s.pk, s.sig, s.msg, s.off, threads=8)
+ok, st = ctx.verify_batch_ex(SR, N.TMV_FLAG_KEY_CACHE, s.pk, s.sig, s.msg, s.off)
+assert np.array_equal(st, sref)
+ok, st = ctx.sr25519_verify_batch(s.pk, s.sig, s.msg, s.off)
+assert np.array_equal(st, sref)
+
+# device-built vote messages, chunked
+rng = random.Random(84)
+tmpls, votes, msgs = V.random_votes(rng, 30, 9000)
+from tendermint_amd.testing._openssl import Ed25519Signer
+from tendermint_amd.testing.factory import key_seed
+ents = []
+for i, m in enumerate(msgs):
+    sg = Ed25519Signer(key_seed(i % 61))
+    sig = sg.sign(m)
+    if i % 1000 == 7:
+        sig = sig[:10] + bytes([sig[10] ^ 1]) + sig[11:]
+    ents.append((sg.public_key, m, sig))
+vb = Batch.from_entries(ents)
+_, vref = C.ed25519_verify_packed(vb.pk, vb.sig, vb.msg, vb.off, threads=8)
+segs = [V.segments(t) for t in tmpls]
+for flags in (N.TMV_FLAG_KEY_CACHE, N.TMV_FLAG_KEY_CACHE | N.TMV_FLAG_BATCH_EQUATION):
+    ok, st = ctx.verify_votes(ED, flags, segs, votes, vb.pk, vb.sig)
+    assert np.array_equal(st.astype(np.uint8), vref)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("chunk,capacity", [("2048", "4096"), ("3000", "100")])
+def test_chunked_host_batches(chunk, capacity):
+    """Capacity 100 < the keyed batch's 150 keys: that batch takes the
+    uncached path; the votes' 61 keys fit and evict slots between calls."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TMV_HOST_CHUNK=chunk, TMV_KEY_CACHE_CAPACITY=capacity)
+    out = subprocess.run([sys.executable, "-c", CODE], env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "ok" in out.stdout
