@@ -284,16 +284,19 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 // start to part_first (k_msm_wpart joins them).
 template <int L>
 __global__ void __launch_bounds__(256)
-k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, uint32_t per_xcd) {
+k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD a
-  // contiguous range of chunks so a group's points stay in one L2
+  // contiguous range of the LIVE chunks so a group's points stay in one L2
+  // (mixed batches size the grid for n but use only their kind's groups)
+  const uint32_t cpg = p.chunks_per_group();
+  const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
+  const uint32_t live_blocks = (live_groups * cpg + blockDim.x - 1) / blockDim.x;
+  const uint32_t per_xcd = (live_blocks + 7) / 8;
   if ((blockIdx.x >> 3) >= per_xcd) return;
   const uint32_t lb = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   const uint32_t t = lb * blockDim.x + threadIdx.x;
-  const uint32_t cpg = p.chunks_per_group();
   const uint32_t g = t / cpg;
-  if (g >= p.groups) return;
-  if ((g << p.m_log2) >= entry_count(count_ptr, n)) return;
+  if (g >= live_groups) return;
   const uint32_t base = t * L;
   uint32_t bk[L], pt[L];
   {
@@ -447,11 +450,11 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
   const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
   const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
   if (p.L == 8)
-    hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+    hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   else if (p.L == 16)
-    hipLaunchKernelGGL(k_msm_accum<16>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+    hipLaunchKernelGGL(k_msm_accum<16>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   else
-    hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p, per_xcd);
+    hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   hipError_t e;
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;

@@ -21,6 +21,7 @@ ap.add_argument("--headers", type=int, default=2000)
 ap.add_argument("--blocks", type=int, default=1000)
 ap.add_argument("--c5", type=int, default=1_000_000)
 ap.add_argument("--only", default="1,3,4,5")
+ap.add_argument("--c5-methods", default="", help="comma list of C5 method labels (default: all)")
 a = ap.parse_args()
 only = set(a.only.split(","))
 ctx = N.Context(1)
@@ -94,8 +95,11 @@ if "5" in only:
     do = t(b.off.view(np.int32))
     st = torch.cuda.Stream()
     ref = None
-    for label, flags, mlog in (("per-entry", N.TMV_FLAG_PER_ENTRY, 0), ("batch m=64", N.TMV_FLAG_BATCH_EQUATION, 6),
-                               ("batch m=256", N.TMV_FLAG_BATCH_EQUATION, 8)):
+    c5_methods = [("per-entry", N.TMV_FLAG_PER_ENTRY, 0), ("batch m=32", N.TMV_FLAG_BATCH_EQUATION, 5),
+                  ("batch m=64", N.TMV_FLAG_BATCH_EQUATION, 6), ("batch m=256", N.TMV_FLAG_BATCH_EQUATION, 8)]
+    if a.c5_methods:
+        c5_methods = [m for m in c5_methods if m[0] in a.c5_methods.split(",")]
+    for label, flags, mlog in c5_methods:
         ctx.set_batch_options(group_log2=mlog)
         dst = torch.zeros(a.c5, dtype=torch.int8, device=dev)
         run = lambda: ctx.verify_batch_device_ex(0, N.TMV_KIND_MIXED, flags, dk.data_ptr(), dp.data_ptr(),
