@@ -74,16 +74,31 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-def _load_traffic(method: str):
-    """HBM bytes per launch of 32 C2 batches from the committed PMC passes
+def _load_pmc(method: str):
+    """PMC summary of a launch of 32 C2 batches from the committed passes
     (tools/profile_round.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE)."""
+    correction + WRITE_SIZE; tools/pmc_derived.py: occupancy, VALU issue)."""
     name = "pmc_batch.json" if method == "batch" else "pmc_per_entry.json"
     try:
         with open(os.path.join(REPO, "profiles", "r01_msm", name)) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f)
     except Exception:
-        return None
+        return {}
+
+
+def _load_traffic(method: str):
+    return _load_pmc(method).get("hbm_bytes_per_launch")
+
+
+def _pmc_kernels(method: str):
+    """Per-kernel occupancy (mean waves / SIMD) and VALU issue utilisation."""
+    out = {}
+    for name, k in _load_pmc(method).get("kernels", {}).items():
+        d = k.get("derived")
+        if d:
+            out[name.replace("tmv::", "")] = {"occupancy": d["occupancy_waves_per_simd"],
+                                              "valu_issue_util": d["valu_issue_util"]}
+    return out or None
 
 
 def cpu_baseline(batch, seconds_target: float = 12.0):
@@ -280,7 +295,10 @@ def main():
                                            "than the timed span / launches; aggregate = verifies/s x 2.7e5",
                          "achieved_from": f"{K} x {n} sigs x 2.7e5 canonical products / average launch "
                                           "duration (HIP events on the launch stream)",
-                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d), single-verify equivalent)"},
+                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d), single-verify equivalent)",
+                         "pmc_kernels": _pmc_kernels(args.method) if K == 32 else None,
+                         "pmc_note": "each kernel alone under --pmc: occupancy = mean resident waves per SIMD, "
+                                     "valu_issue_util = share of SIMD cycles issuing VALU (tools/pmc_derived.py)"},
         }
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(batch)
