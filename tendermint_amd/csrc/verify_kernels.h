@@ -19,7 +19,8 @@ struct Ed25519Work {
   uint32_t *k;     // n x 8 words, k mod l
   uint8_t *flags;  // 4n bytes: decode ok for A (4e), R (4e+1)
   niels_pt *niels; // batch check only (else null): [2e] = -R_e, [2e+1] = -A_e
-  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4) + 256; }
+  fe *tabA;        // n x 8 x 4 fe: k_verify_quad's tables of -A when kept in global memory
+  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4 + 1280) + 256; }
   // carve a workspace for n entries out of base (16-byte aligned pieces)
   static Ed25519Work carve(void *base, uint32_t n) {
     uint8_t *b = static_cast<uint8_t *>(base);
@@ -28,6 +29,7 @@ struct Ed25519Work {
     w.Rc = reinterpret_cast<fe *>(b + 160ull * n);
     w.k = reinterpret_cast<uint32_t *>(b + 320ull * n);
     w.flags = b + 352ull * n;
+    w.tabA = reinterpret_cast<fe *>(b + ((356ull * n + 15) & ~15ull));
     w.niels = nullptr;
     return w;
   }

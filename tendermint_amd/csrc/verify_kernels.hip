@@ -7,6 +7,8 @@
 // 32x32->64 multiply-adds of the radix-2^25.5 field dominate (see DESIGN.md
 // for the roofline), so there is no MFMA or LDS tiling here.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <cstring>
 #include "ed25519_core.h"
 #include "quad.h"
 #include "sr25519_core.h"
@@ -145,12 +147,16 @@ constexpr int kQuadSigs = kQuadBlock / 4;
 //   sr25519: acc == R (Ristretto equality)
 // Each signature occupies one quad; writes out[i] (ed25519 1/0; sr25519
 // 1/0/-1/-2 as int8).
-template <bool SR>
+// GT: the 8-entry tables of -A live in a global scratch (w.tabA, L2-resident
+// while the wave runs) instead of LDS, so LDS (22.5 KB per wave otherwise)
+// no longer caps residency; each window's entry is loaded before its four
+// doublings, like the B entry.
+template <bool SR, bool GT>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
               const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
-  __shared__ fe tabA[kQuadSigs * 8 * 4];
+  __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
   const uint32_t m = entry_count(count_ptr, n);
   if (blockIdx.x * kQuadSigs >= m) return;  // block-uniform
@@ -208,21 +214,22 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   const bool r_ok = w.flags[4 * e + 1] != 0;
 
   // table of (m+1)(-A), m < 8, in CachedQ layout
+  fe *tabA = GT ? w.tabA + 32ull * e : tabA_lds + q * 32;
   fe P = w.negA[4ull * e + c];
   fe r, Pm, Q, Q0;
   quad::to_cached(Q0, P);
-  tabA[(q * 8 + 0) * 4 + c] = Q0;
+  tabA[0 * 4 + c] = Q0;
   quad::dbl(r, P);
   quad::p1p1_to_p3(Pm, r);
   quad::to_cached(Q, Pm);
-  tabA[(q * 8 + 1) * 4 + c] = Q;
+  tabA[1 * 4 + c] = Q;
   for (int t = 2; t < 8; t++) {
     quad::add(r, Pm, Q0);
     quad::p1p1_to_p3(Pm, r);
     quad::to_cached(Q, Pm);
-    tabA[(q * 8 + t) * 4 + c] = Q;
+    tabA[t * 4 + c] = Q;
   }
-  __syncthreads();
+  __syncthreads();  // digits (and the LDS table) written by other lanes
 
   fe acc;
   quad::p3_identity(acc);
@@ -232,8 +239,11 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   for (int wdx = 63; wdx >= 0; wdx--) {
     const int db = dig[q][1][wdx >> 1];
     const int ab = db < 0 ? -db : db;
-    fe bent;
+    const int da = dig[q][0][wdx];
+    const int aa = da < 0 ? -da : da;
+    fe bent, ent;
     if ((wdx & 1) == 0) bent = btab_q[(ab ? ab - 1 : 0) * 4 + c];
+    ent = tabA[(aa ? aa - 1 : 0) * 4 + c];
     if (wdx != 63) {
 #pragma unroll
       for (int d = 0; d < 4; d++) {
@@ -241,11 +251,8 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
         quad::p1p1_to_p3(acc, r);
       }
     }
-    const int da = dig[q][0][wdx];
-    fe ent, idq;
+    fe idq;
     quad::cached_identity(idq);
-    const int aa = da < 0 ? -da : da;
-    ent = tabA[(q * 8 + (aa ? aa - 1 : 0)) * 4 + c];
     fe_cmov(ent, idq, aa == 0);
     quad::cached_cneg(ent, da < 0);
     quad::add(r, acc, ent);
@@ -674,6 +681,31 @@ template hipError_t launch_comb_fallback<true>(const uint8_t *, const uint32_t *
                                                Ed25519Work, KeyTable, const fe *, uint8_t *, int, const uint8_t *,
                                                uint32_t, hipStream_t);
 
+// k_verify_quad's -A tables: LDS (default) or global scratch
+// (TMV_QUAD_TABLE=global).  Measured on the C2 bench in one GPU call
+// (profiles/r01_msm/ab_quad_table.log): LDS 72.8 / 73.5 M/s, global 70.8 /
+// 71.2 M/s (5 instead of 2 waves per SIMD, but every window's entry then
+// comes from L2); per entry 45.6-45.7 M/s either way.
+static bool quad_table_global() {
+  static const bool g = [] {
+    const char *e = getenv("TMV_QUAD_TABLE");
+    return e && !strcmp(e, "global");
+  }();
+  return g;
+}
+
+template <bool SR>
+static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig, const uint32_t *idx,
+                        const uint32_t *count_ptr, uint32_t n, Ed25519Work w, const fe *btab_q, uint8_t *out,
+                        int aligned, const uint8_t *group_ok, uint32_t group_log2) {
+  if (quad_table_global())
+    hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
+                       w, btab_q, out, aligned, group_ok, group_log2);
+  else
+    hipLaunchKernelGGL((k_verify_quad<SR, false>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
+                       w, btab_q, out, aligned, group_ok, group_log2);
+}
+
 static int is_aligned(const void *a, const void *b) {
   return ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
 }
@@ -688,8 +720,7 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  hipLaunchKernelGGL(k_verify_quad<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
-                     btab_q, out, aligned, (const uint8_t *)nullptr, 0u);
+  launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, nullptr, 0u);
   return hipGetLastError();
 }
 
@@ -700,8 +731,7 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
                                 const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
                                 uint8_t *out, int aligned, hipStream_t stream) {
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  hipLaunchKernelGGL(k_verify_quad<SR>, dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
-                     btab_q, out, aligned, group_ok, group_log2);
+  launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2);
   return hipGetLastError();
 }
 template hipError_t launch_quad_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
