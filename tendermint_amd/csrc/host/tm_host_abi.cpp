@@ -343,12 +343,6 @@ struct PhaseTimer {
   }
 };
 
-struct OwnedCommitArgs {
-  std::unique_ptr<tmh::ValidatorSet> vals;
-  tmh::Commit *commit = nullptr;
-  tmh::BlockID block_id;
-};
-
 std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index) {
   if (!vals) return nullptr;
   auto vs = std::make_unique<tmh::ValidatorSet>();
@@ -376,9 +370,9 @@ std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit) {
     const tmv_commit_sig &s = commit->sigs[i];
     tmh::CommitSig &c = cm->signatures[i];
     c.block_id_flag = (tmh::BlockIDFlag)s.block_id_flag;
-    c.validator_address = bytes_of(s.validator_address, s.validator_address_len);
+    c.validator_address = tmh::ByteView(s.validator_address, s.validator_address_len);
     c.timestamp = tmh::Timestamp{s.ts_seconds, s.ts_nanos};
-    c.signature = bytes_of(s.signature, s.signature_len);
+    c.signature = tmh::ByteView(s.signature, s.signature_len);
   }
   return cm;
 }
@@ -431,33 +425,71 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
   tm.mark("plan");
   // dedupe identical entries across plans: same commit object and signature
   // index, same public key object, same verifier kind and the same chain_id
-  // (hence the same message; one slot per (commit, index, kind) instead of a
-  // hash map)
-  std::vector<VoteRef> uniq;
+  // (hence the same message).  Only jobs over one commit object can share
+  // entries, so commits are deduplicated independently (in parallel, one
+  // slot array per (commit, verifier kind)) and the unique entries are
+  // numbered commit by commit.
   std::vector<std::vector<uint32_t>> where(n_jobs);
-  const bool dedup = n_jobs > 1;
-  std::vector<std::vector<uint32_t>> slot(dedup ? 2 * commits.size() : 0);
+  std::vector<std::vector<uint32_t>> by_commit(commits.size());
+  std::vector<uint32_t> solo;  // jobs with entries but no commit index (none today; kept general)
   for (uint32_t j = 0; j < n_jobs; j++) {
-    const tmh::CommitPlan &pl = plans[j];
-    if (pl.early) continue;
-    where[j].resize(pl.entries.size());
-    std::vector<uint32_t> *sl = nullptr;
-    if (dedup && jc[j] != SIZE_MAX) {
-      sl = &slot[2 * jc[j] + (pl.batch ? 1 : 0)];
-      if (sl->empty()) sl->assign(pl.commit->signatures.size(), UINT32_MAX);
+    if (plans[j].early || plans[j].entries.empty()) continue;
+    if (jc[j] != SIZE_MAX) by_commit[jc[j]].push_back(j);
+    else solo.push_back(j);
+  }
+  std::vector<std::vector<VoteRef>> local(commits.size());
+  parallel_for(commits.size(), 8, [&](size_t c) {
+    const auto &js = by_commit[c];
+    if (js.empty()) return;
+    auto &loc = local[c];
+    if (js.size() == 1) {  // nothing to share
+      const tmh::CommitPlan &pl = plans[js[0]];
+      where[js[0]].resize(pl.entries.size());
+      loc.reserve(pl.entries.size());
+      for (size_t e = 0; e < pl.entries.size(); e++) {
+        where[js[0]][e] = (uint32_t)e;
+        loc.push_back(VoteRef{&pl, (uint32_t)e});
+      }
+      return;
     }
-    for (size_t e = 0; e < pl.entries.size(); e++) {
-      const tmh::SigEntry &en = pl.entries[e];
-      if (sl) {
-        uint32_t &u = (*sl)[(size_t)pl.sig_idx[e]];
-        if (u != UINT32_MAX && uniq[u].entry().pk == en.pk && uniq[u].pl->chain_id == pl.chain_id) {
+    std::vector<uint32_t> slot[2];
+    for (uint32_t j : js) {
+      const tmh::CommitPlan &pl = plans[j];
+      std::vector<uint32_t> &sl = slot[pl.batch ? 1 : 0];
+      if (sl.empty()) sl.assign(pl.commit->signatures.size(), UINT32_MAX);
+      where[j].resize(pl.entries.size());
+      for (size_t e = 0; e < pl.entries.size(); e++) {
+        const tmh::SigEntry &en = pl.entries[e];
+        uint32_t &u = sl[(size_t)pl.sig_idx[e]];
+        if (u != UINT32_MAX && loc[u].entry().pk == en.pk && loc[u].pl->chain_id == pl.chain_id) {
           where[j][e] = u;
           continue;
         }
-        u = (uint32_t)uniq.size();
+        u = (uint32_t)loc.size();
+        where[j][e] = u;
+        loc.push_back(VoteRef{&pl, (uint32_t)e});
       }
+    }
+  });
+  std::vector<VoteRef> uniq;
+  {
+    size_t total = 0;
+    for (auto &l : local) total += l.size();
+    for (uint32_t j : solo) total += plans[j].entries.size();
+    uniq.reserve(total);
+  }
+  for (size_t c = 0; c < commits.size(); c++) {
+    const uint32_t base = (uint32_t)uniq.size();
+    uniq.insert(uniq.end(), local[c].begin(), local[c].end());
+    if (base)
+      for (uint32_t j : by_commit[c])
+        for (uint32_t &w : where[j]) w += base;
+  }
+  for (uint32_t j : solo) {
+    where[j].resize(plans[j].entries.size());
+    for (size_t e = 0; e < plans[j].entries.size(); e++) {
       where[j][e] = (uint32_t)uniq.size();
-      uniq.push_back(VoteRef{&pl, (uint32_t)e});
+      uniq.push_back(VoteRef{&plans[j], (uint32_t)e});
     }
   }
   tm.mark("dedup");

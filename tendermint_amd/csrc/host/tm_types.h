@@ -36,6 +36,20 @@ namespace tmh {
 using Bytes = std::vector<uint8_t>;
 using Error = std::optional<std::string>;
 
+// A read-only view of bytes owned elsewhere (the caller's C structs during a
+// tmv_verify_commits call, or a Bytes): commit signatures are not copied.
+struct ByteView {
+  const uint8_t *p = nullptr;
+  size_t n = 0;
+  ByteView() = default;
+  ByteView(const uint8_t *ptr, size_t len) : p(len ? ptr : nullptr), n(len) {}
+  ByteView(const Bytes &b) : p(b.data()), n(b.size()) {}  // NOLINT: implicit on purpose
+  const uint8_t *data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  bool operator==(const ByteView &o) const { return n == o.n && (n == 0 || std::memcmp(p, o.p, n) == 0); }
+};
+
 // ---------------------------------------------------------------- Go-style formatting
 inline std::string HexUpper(const uint8_t *p, size_t n) {
   static const char *d = "0123456789ABCDEF";
@@ -47,12 +61,12 @@ inline std::string HexUpper(const uint8_t *p, size_t n) {
   }
   return s;
 }
-inline std::string HexUpper(const Bytes &b) { return HexUpper(b.data(), b.size()); }
+inline std::string HexUpper(ByteView b) { return HexUpper(b.data(), b.size()); }
 inline std::string HexUpper(const std::string &s) {
   return HexUpper(reinterpret_cast<const uint8_t *>(s.data()), s.size());
 }
 // libs/bytes.Fingerprint: first 6 bytes, zero padded
-inline Bytes Fingerprint(const Bytes &b) {
+inline Bytes Fingerprint(ByteView b) {
   Bytes f(6, 0);
   std::memcpy(f.data(), b.data(), std::min<size_t>(6, b.size()));
   return f;
@@ -156,9 +170,9 @@ struct BlockID {
 
 struct CommitSig {
   BlockIDFlag block_id_flag = BlockIDFlagAbsent;
-  Bytes validator_address;
+  ByteView validator_address;  // views into the caller's tmv_commit_sig
   Timestamp timestamp;
-  Bytes signature;
+  ByteView signature;
   // types/block.go:633-639
   std::string String() const {
     return "CommitSig{" + HexUpper(Fingerprint(signature)) + " by " + HexUpper(Fingerprint(validator_address)) +
@@ -370,9 +384,9 @@ struct ValidatorSet {
     total_voting_power = TotalVotingPower();
   }
   // types/validator_set.go:267-274 (linear scan, like the reference)
-  std::pair<int32_t, const Validator *> GetByAddress(const Bytes &addr) const {
+  std::pair<int32_t, const Validator *> GetByAddress(ByteView addr) const {
     for (size_t i = 0; i < validators.size(); i++)
-      if (validators[i].address == addr) return {(int32_t)i, &validators[i]};
+      if (ByteView(validators[i].address) == addr) return {(int32_t)i, &validators[i]};
     return {-1, nullptr};
   }
   // types/validator_set.go:322-344: highest priority, ties to the smaller address
@@ -436,7 +450,7 @@ inline bool ScalarCanonical(const uint8_t s[32]) {
   return false;
 }
 
-inline AddCheck CheckAdd(KeyType batch_kind, const PubKey &key, const Bytes &sig) {
+inline AddCheck CheckAdd(KeyType batch_kind, const PubKey &key, ByteView sig) {
   AddCheck r;
   if (batch_kind == KeyType::Ed25519) {
     if (key.type != KeyType::Ed25519) { r.sync = std::string("pubkey is not Ed25519"); return r; }
