@@ -200,6 +200,20 @@ void parallel_for(size_t n, size_t min_per_thread, F fn) {
   tmh::parallel_for_n(n, n / std::max<size_t>(1, min_per_thread), fn);
 }
 
+// Phase timing of tmv_verify_commits, printed to stderr when the
+// environment variable TMV_HOST_TIMING is set (profiling aid).
+struct PhaseTimer {
+  bool on = std::getenv("TMV_HOST_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[tmv_verify_commits] %-8s %9.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+
 // Signature backend over the device: entries split by key kind, each kind one
 // tmv_verify_votes call with the key cache (validator keys repeat).  The
 // sign-bytes are built on the device from one template per (commit,
@@ -208,6 +222,7 @@ void parallel_for(size_t n, size_t min_per_thread, F fn) {
 // Packing buffers reused across calls on a thread: fresh multi-megabyte
 // vectors would be new mappings, page-faulted in on every call.
 struct PackBuffers {
+  std::vector<uint8_t> cls;
   std::vector<uint32_t> idx, off;
   std::vector<uint8_t> pk, sig, msg;
   std::vector<tmv_vote> votes;
@@ -238,6 +253,7 @@ struct GpuBackend {
   void operator()(const std::vector<VoteRef> &es, std::vector<int8_t> &st) {
     static thread_local PackBuffers tls;
     PackBuffers &pb = tls;  // the workers below must use this thread's buffers, not their own
+    PhaseTimer tm;
     st.assign(es.size(), 0);
     // one template per (commit object, chain_id)
     std::vector<tmh::VoteTemplate> tmpls;
@@ -269,6 +285,7 @@ struct GpuBackend {
       }
       ent_tmpl[i] = last_t;
     }
+    tm.mark("b:tmpl");
     std::vector<tmv_vote_template> tv(tmpls.size());
     for (size_t t = 0; t < tmpls.size(); t++) {
       const tmh::VoteTemplate &vt = tmpls[t];
@@ -276,33 +293,63 @@ struct GpuBackend {
       tv[t] = tmv_vote_template{b, vt.head_len, b + vt.head_len, vt.block_len, b + vt.head_len + vt.block_len,
                                 vt.chain_len};
     }
-    for (int kind = 0; kind < 2; kind++) {
-      const tmh::KeyType kt = kind == 0 ? tmh::KeyType::Ed25519 : tmh::KeyType::Sr25519;
-      pb.idx.clear();
-      for (size_t i = 0; i < es.size(); i++) {
+    // verifier kind of every entry (2: not verified -- VerifySignature is
+    // false for a wrong key or signature size), classified in parallel
+    // chunks, then each kind's index list is filled chunk by chunk
+    constexpr size_t kChunk = 4096;
+    const size_t nch = (es.size() + kChunk - 1) / kChunk;
+    pb.cls.resize(es.size());
+    std::vector<uint32_t> ccount(2 * nch + 2, 0);
+    parallel_for(nch, 1, [&](size_t c) {
+      uint32_t k0 = 0, k1 = 0;
+      for (size_t i = c * kChunk; i < std::min(es.size(), c * kChunk + kChunk); i++) {
         const tmh::SigEntry &e = es[i].entry();
-        if (e.kind != kt) continue;
-        if (e.pk->size() != 32 || e.sig_len != 64) continue;  // VerifySignature: false
-        pb.idx.push_back((uint32_t)i);
+        uint8_t k = e.kind == tmh::KeyType::Ed25519 ? 0 : (e.kind == tmh::KeyType::Sr25519 ? 1 : 2);
+        if (e.pk->size() != 32 || e.sig_len != 64) k = 2;
+        pb.cls[i] = k;
+        k0 += k == 0;
+        k1 += k == 1;
       }
-      if (pb.idx.empty()) continue;
-      const size_t m = pb.idx.size();
+      ccount[2 * c] = k0;
+      ccount[2 * c + 1] = k1;
+    });
+    uint32_t kind_n[2] = {0, 0};
+    for (size_t c = 0; c < nch; c++)
+      for (int k = 0; k < 2; k++) {
+        const uint32_t v = ccount[2 * c + k];
+        ccount[2 * c + k] = kind_n[k];
+        kind_n[k] += v;
+      }
+    pb.idx.resize((size_t)kind_n[0] + kind_n[1]);
+    parallel_for(nch, 1, [&](size_t c) {
+      uint32_t at[2] = {ccount[2 * c], kind_n[0] + ccount[2 * c + 1]};
+      for (size_t i = c * kChunk; i < std::min(es.size(), c * kChunk + kChunk); i++) {
+        const uint8_t k = pb.cls[i];
+        if (k < 2) pb.idx[at[k]++] = (uint32_t)i;
+      }
+    });
+    tm.mark("b:cls");
+    for (int kind = 0; kind < 2; kind++) {
+      const uint32_t *kidx = pb.idx.data() + (kind == 0 ? 0 : kind_n[0]);
+      const size_t m = kind_n[kind];
+      if (m == 0) continue;
       pb.pk.resize(32 * m);
       pb.sig.resize(64 * m);
       pb.votes.resize(m);
       pb.out.resize(m);
       parallel_for((m + 1023) / 1024, 1, [&](size_t c) {
         for (size_t t = c * 1024; t < std::min(m, c * 1024 + 1024); t++) {
-          const VoteRef &r = es[pb.idx[t]];
+          const VoteRef &r = es[kidx[t]];
           const tmh::SigEntry &e = r.entry();
           const tmh::CommitSig &cs = r.pl->commit->signatures[(size_t)r.pl->sig_idx[r.e]];
           std::memcpy(&pb.pk[32 * t], e.pk->data(), 32);
           std::memcpy(&pb.sig[64 * t], e.sig, 64);
           pb.votes[t] = tmv_vote{cs.timestamp.seconds, cs.timestamp.nanos,
-                                 ent_tmpl[pb.idx[t]] |
+                                 ent_tmpl[kidx[t]] |
                                      (cs.block_id_flag == tmh::BlockIDFlagCommit ? TMV_VOTE_WITH_BLOCK : 0u)};
         }
       });
+      tm.mark("b:pack");
       int rc;
       if (m >= device_signbytes_min()) {
         rc = tmv_verify_votes(ctx, kind == 0 ? TMV_KIND_ED25519 : TMV_KIND_SR25519, TMV_FLAG_KEY_CACHE, tv.data(),
@@ -323,23 +370,13 @@ struct GpuBackend {
                                  pb.pk.data(), pb.sig.data(), pb.msg.data(), pb.off.data(), (uint32_t)m,
                                  pb.out.data());
       }
+      tm.mark("b:engine");
       if (rc < 0) { infra = rc; continue; }
-      for (size_t t = 0; t < m; t++) st[pb.idx[t]] = pb.out[t];
+      parallel_for((m + kChunk - 1) / kChunk, 4, [&](size_t c) {
+        for (size_t t = c * kChunk; t < std::min(m, c * kChunk + kChunk); t++) st[kidx[t]] = pb.out[t];
+      });
+      tm.mark("b:scatter");
     }
-  }
-};
-
-// Phase timing of tmv_verify_commits, printed to stderr when the
-// environment variable TMV_HOST_TIMING is set (profiling aid).
-struct PhaseTimer {
-  bool on = std::getenv("TMV_HOST_TIMING") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  void mark(const char *what) {
-    if (!on) return;
-    const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[tmv_verify_commits] %-8s %9.3f ms\n", what,
-                 std::chrono::duration<double, std::milli>(now - t).count());
-    t = now;
   }
 };
 
@@ -426,10 +463,14 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
   // dedupe identical entries across plans: same commit object and signature
   // index, same public key object, same verifier kind and the same chain_id
   // (hence the same message).  Only jobs over one commit object can share
-  // entries, so commits are deduplicated independently (in parallel, one
-  // slot array per (commit, verifier kind)) and the unique entries are
-  // numbered commit by commit.
-  std::vector<std::vector<uint32_t>> where(n_jobs);
+  // entries, so commits are deduplicated independently, in parallel, into
+  // flat arrays: pass 1 gives each entry a commit-local unique index (bit 31
+  // marks its first occurrence), pass 2 places the unique entries commit by
+  // commit and rebases the indices.
+  std::vector<size_t> joff(n_jobs + 1, 0);
+  for (uint32_t j = 0; j < n_jobs; j++)
+    joff[j + 1] = joff[j] + (plans[j].early ? 0 : plans[j].entries.size());
+  std::vector<uint32_t> where(joff[n_jobs]);
   std::vector<std::vector<uint32_t>> by_commit(commits.size());
   std::vector<uint32_t> solo;  // jobs with entries but no commit index (none today; kept general)
   for (uint32_t j = 0; j < n_jobs; j++) {
@@ -437,60 +478,68 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
     if (jc[j] != SIZE_MAX) by_commit[jc[j]].push_back(j);
     else solo.push_back(j);
   }
-  std::vector<std::vector<VoteRef>> local(commits.size());
+  constexpr uint32_t kFirst = 0x80000000u;
+  std::vector<uint32_t> n_new(commits.size() + 1, 0);
   parallel_for(commits.size(), 8, [&](size_t c) {
     const auto &js = by_commit[c];
     if (js.empty()) return;
-    auto &loc = local[c];
+    static thread_local std::vector<uint32_t> slot[2];  // commit-local index per signature, per kind
+    static thread_local std::vector<std::pair<uint32_t, uint32_t>> first;  // (job, entry) of each local index
+    uint32_t cnt = 0;
     if (js.size() == 1) {  // nothing to share
-      const tmh::CommitPlan &pl = plans[js[0]];
-      where[js[0]].resize(pl.entries.size());
-      loc.reserve(pl.entries.size());
-      for (size_t e = 0; e < pl.entries.size(); e++) {
-        where[js[0]][e] = (uint32_t)e;
-        loc.push_back(VoteRef{&pl, (uint32_t)e});
-      }
+      const uint32_t j = js[0];
+      for (size_t e = 0; e < plans[j].entries.size(); e++) where[joff[j] + e] = kFirst | cnt++;
+      n_new[c] = cnt;
       return;
     }
-    std::vector<uint32_t> slot[2];
+    bool used[2] = {false, false};
+    first.clear();
     for (uint32_t j : js) {
       const tmh::CommitPlan &pl = plans[j];
-      std::vector<uint32_t> &sl = slot[pl.batch ? 1 : 0];
-      if (sl.empty()) sl.assign(pl.commit->signatures.size(), UINT32_MAX);
-      where[j].resize(pl.entries.size());
+      const int kind = pl.batch ? 1 : 0;
+      std::vector<uint32_t> &sl = slot[kind];
+      if (!used[kind]) { sl.assign(pl.commit->signatures.size(), UINT32_MAX); used[kind] = true; }
       for (size_t e = 0; e < pl.entries.size(); e++) {
         const tmh::SigEntry &en = pl.entries[e];
         uint32_t &u = sl[(size_t)pl.sig_idx[e]];
-        if (u != UINT32_MAX && loc[u].entry().pk == en.pk && loc[u].pl->chain_id == pl.chain_id) {
-          where[j][e] = u;
-          continue;
+        if (u != UINT32_MAX) {
+          const tmh::CommitPlan &fpl = plans[first[u].first];  // first occurrence of u
+          if (fpl.entries[first[u].second].pk == en.pk && (&fpl == &pl || fpl.chain_id == pl.chain_id)) {
+            where[joff[j] + e] = u;
+            continue;
+          }
         }
-        u = (uint32_t)loc.size();
-        where[j][e] = u;
-        loc.push_back(VoteRef{&pl, (uint32_t)e});
+        u = cnt++;
+        first.emplace_back(j, (uint32_t)e);
+        where[joff[j] + e] = kFirst | u;
       }
     }
+    n_new[c] = cnt;
   });
-  std::vector<VoteRef> uniq;
+  std::vector<uint32_t> cbase(commits.size() + 1, 0);
+  for (size_t c = 0; c < commits.size(); c++) cbase[c + 1] = cbase[c] + n_new[c];
+  size_t total = cbase[commits.size()];
+  for (uint32_t j : solo) total += plans[j].entries.size();
+  std::vector<VoteRef> uniq(total);
+  parallel_for(commits.size(), 64, [&](size_t c) {
+    for (uint32_t j : by_commit[c])
+      for (size_t e = 0; e < plans[j].entries.size(); e++) {
+        uint32_t &w = where[joff[j] + e];
+        if (w & kFirst) {
+          w = cbase[c] + (w & ~kFirst);
+          uniq[w] = VoteRef{&plans[j], (uint32_t)e};
+        } else {
+          w += cbase[c];
+        }
+      }
+  });
   {
-    size_t total = 0;
-    for (auto &l : local) total += l.size();
-    for (uint32_t j : solo) total += plans[j].entries.size();
-    uniq.reserve(total);
-  }
-  for (size_t c = 0; c < commits.size(); c++) {
-    const uint32_t base = (uint32_t)uniq.size();
-    uniq.insert(uniq.end(), local[c].begin(), local[c].end());
-    if (base)
-      for (uint32_t j : by_commit[c])
-        for (uint32_t &w : where[j]) w += base;
-  }
-  for (uint32_t j : solo) {
-    where[j].resize(plans[j].entries.size());
-    for (size_t e = 0; e < plans[j].entries.size(); e++) {
-      where[j][e] = (uint32_t)uniq.size();
-      uniq.push_back(VoteRef{&plans[j], (uint32_t)e});
-    }
+    uint32_t u = cbase[commits.size()];
+    for (uint32_t j : solo)
+      for (size_t e = 0; e < plans[j].entries.size(); e++) {
+        where[joff[j] + e] = u;
+        uniq[u++] = VoteRef{&plans[j], (uint32_t)e};
+      }
   }
   tm.mark("dedup");
   GpuBackend be{ctx};
@@ -504,8 +553,8 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
   int bad = 0;
   std::vector<int8_t> buf;
   for (uint32_t j = 0; j < n_jobs; j++) {
-    buf.resize(where[j].size());
-    for (size_t e = 0; e < where[j].size(); e++) buf[e] = st[where[j][e]];
+    buf.resize(joff[j + 1] - joff[j]);
+    for (size_t e = 0; e < buf.size(); e++) buf[e] = st[where[joff[j] + e]];
     tmh::Error e = tmh::CommitVerifier::Finish(plans[j], buf.data());
     if (results) results[j] = e ? 1 : 0;
     if (errs && err_stride) put_err(errs + (size_t)j * err_stride, err_stride, e ? *e : std::string());
