@@ -117,9 +117,49 @@ def cpu_baseline(batch, seconds_target: float = 12.0):
     for _ in range(reps):
         oracle_c.ed25519_verify_packed(batch.pk, batch.sig, batch.msg, batch.off, threads=threads)
     wall = time.perf_counter() - t0
-    return {"value": round(reps * batch.n / wall, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
-            "sample": f"C2 batch ({batch.n} sigs) x {reps} passes, oracle/c/ed25519_oracle.c, "
-                      f"{threads} pthreads; Go/curve25519-voi not buildable here (no toolchain)"}
+    out = {"value": round(reps * batch.n / wall, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
+           "sample": f"C2 batch ({batch.n} sigs) x {reps} passes, oracle/c/ed25519_oracle.c, "
+                     f"{threads} pthreads; Go/curve25519-voi not buildable here (no toolchain)"}
+    out["openssl_proxy"] = _openssl_proxy(threads)
+    return out
+
+
+def _openssl_proxy(threads: int, seconds_target: float = 5.0):
+    """SURVEY 8(d)'s strict-semantics CPU proxy when voi cannot run: OpenSSL 3
+    Ed25519 single-verify/s on the same host threads, honest signatures only
+    (RFC 8032 cofactorless verification disagrees with ZIP-215 on edge cases)."""
+    import ctypes
+    path = os.path.join(REPO, "oracle", "_build", "libopenssl_proxy.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    honest = make_c1_commit_batch()  # 2,000 validators, one signature each
+    b = honest.tile(20000)
+    keys = honest.pk.copy()
+    key_idx = (np.arange(b.n) % honest.n).astype(np.uint32)
+    u8 = ctypes.POINTER(ctypes.c_uint8)
+    u32 = ctypes.POINTER(ctypes.c_uint32)
+    out = np.zeros(b.n, np.uint8)
+    args = lambda: (b.pk.ctypes.data_as(u8), b.sig.ctypes.data_as(u8), b.msg.ctypes.data_as(u8),  # noqa: E731
+                    b.off.ctypes.data_as(u32), b.n, out.ctypes.data_as(u8), threads, keys.ctypes.data_as(u8),
+                    key_idx.ctypes.data_as(u32), honest.n)
+    t0 = time.perf_counter()
+    assert L.openssl_ed25519_verify_batch(*args()) == 1
+    first = time.perf_counter() - t0
+    reps = max(1, int(seconds_target / max(first, 1e-3)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        L.openssl_ed25519_verify_batch(*args())
+    wall = time.perf_counter() - t0
+    return {"value": round(reps * b.n / wall, 1), "unit": "verifies/s", "cores": threads,
+            "kind": "openssl-proxy", "sample": f"{b.n} honest commit-vote sigs x {reps} passes (2,000 keys decoded "
+                                               "once), OpenSSL 3 EVP Ed25519 verify (strict RFC 8032; not ZIP-215, "
+                                               "not batched)"}
+
+
+def make_c1_commit_batch():
+    from tendermint_amd.testing.factory import make_commit_batch
+    return make_commit_batch(2000)
 
 
 def _c2(a):
