@@ -58,6 +58,7 @@ struct DeviceBuf {
   void *ptr = nullptr;
   size_t cap = 0;
   bool pinned = false;
+  void *dev = nullptr;  // pinned buffers: the device's address of the same memory
   hipError_t ensure(size_t bytes, bool host_pinned) {
     if (bytes <= cap) return hipSuccess;
     release();
@@ -67,12 +68,15 @@ struct DeviceBuf {
     if (e != hipSuccess) { ptr = nullptr; cap = 0; return e; }
     cap = want;
     pinned = host_pinned;
+    dev = nullptr;
+    if (pinned && hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) dev = nullptr;
     return hipSuccess;
   }
   void release() {
     if (!ptr) return;
     if (pinned) (void)hipHostFree(ptr); else (void)hipFree(ptr);
     ptr = nullptr;
+    dev = nullptr;
     cap = 0;
   }
 };
@@ -200,6 +204,9 @@ uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk len
 // Key-cached batches up to this size run as one fused latency kernel
 // (TMV_CACHED_FUSED_MAX; commit-sized calls such as VerifyCommit).
 uint32_t g_cached_fused_max = 4096;
+// Fused-path batches read their inputs and write their statuses in pinned
+// host memory instead of copying (TMV_ZERO_COPY=0 turns it off).
+int g_zero_copy = 1;
 // Host-buffer batches of at least this many entries per device are
 // pipelined in chunks (of half to one of these) over two lanes
 // (TMV_HOST_CHUNK).
@@ -217,6 +224,8 @@ void read_env() {
     if (mm) g_msm_min = (uint32_t)strtoul(mm, nullptr, 10);
     const char *cf = getenv("TMV_CACHED_FUSED_MAX");
     if (cf) g_cached_fused_max = (uint32_t)strtoul(cf, nullptr, 10);
+    const char *zc = getenv("TMV_ZERO_COPY");
+    if (zc) g_zero_copy = atoi(zc);
     const char *hc = getenv("TMV_HOST_CHUNK");
     if (hc) g_host_chunk = (uint32_t)strtoul(hc, nullptr, 10);
     const char *mc = getenv("TMV_MSM_CHUNK");
@@ -941,9 +950,17 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     rg0[G] = n_runs;
   }
   tm.mark("stage", n);
-  uint8_t *dd = static_cast<uint8_t *>(ln.d_in.ptr);
+  // Small key-cached batches (the VerifyCommit latency path) skip both
+  // copies: the fused kernel reads the pinned staging and writes the
+  // statuses to pinned memory over PCIe (coherent host memory).
+  read_env();
+  const bool zero_copy = g_zero_copy && cached && !merged && !vs && n <= g_cached_fused_max && ln.h_in.dev &&
+                         ln.h_out.dev;
+  uint8_t *dd = static_cast<uint8_t *>(zero_copy ? ln.h_in.dev : ln.d_in.ptr);
   const uint32_t *doff = reinterpret_cast<uint32_t *>(dd + L.off);
-  if (vs) {  // everything but the message region, which the device writes
+  if (zero_copy) {
+    // inputs are read in place
+  } else if (vs) {  // everything but the message region, which the device writes
     if ((e = hipMemcpyAsync(dd, h, L.msg, hipMemcpyHostToDevice, ln.stream)) != hipSuccess ||
         (e = hipMemcpyAsync(dd + L.total, h + L.total, total - L.total, hipMemcpyHostToDevice, ln.stream)) !=
             hipSuccess) {
@@ -960,7 +977,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
   }
-  uint8_t *out = static_cast<uint8_t *>(ln.d_out.ptr);
+  uint8_t *out = static_cast<uint8_t *>(zero_copy ? ln.h_out.dev : ln.d_out.ptr);
   const uint32_t *dslots = reinterpret_cast<const uint32_t *>(dd + kind_at);
   int rc;
   switch (sch) {
@@ -986,6 +1003,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
                         ln.stream);
   }
   if (rc != 0) return rc;
+  if (zero_copy) return 0;
   if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(D2H)", e);
     return TMV_ERR_LAUNCH;
