@@ -206,6 +206,23 @@ TMV_HD void chacha20_block(uint32_t out[16], const uint32_t key[8], uint32_t cou
 }
 #undef TMV_QR
 
+// The affine Niels point (y+x, y-x) as an extended point.  (E, H, G, F) =
+// (ypx - ymx, ypx + ymx, 2, 2) is the completed form of O + q, so
+// X = E F = 2E, Y = H G = 2H, Z = G F = 4, T = E H: one multiply instead of
+// the seven of a mixed addition onto the identity.
+TMV_HD void niels_to_p3(ge_p3 &r, const fe &ypx, const fe &ymx) {
+  fe e, h;
+  fe_sub(e, ypx, ymx);  // level 2
+  fe_add(h, ypx, ymx);  // level 2
+  fe_mul(r.T, e, h);
+  fe_add(e, e, e);      // level 4: carried below
+  fe_add(h, h, h);
+  fe_carry(r.X, e);
+  fe_carry(r.Y, h);
+  fe_zero(r.Z);
+  r.Z.v[0] = 4;
+}
+
 // ---------------------------------------------------------------- scalars
 // r = (a * b) mod l, a: na words (na <= 8), b: 8 words.
 TMV_HD void sc_mul_mod(uint32_t r[8], const uint32_t *a, int na, const uint32_t b[8]) {

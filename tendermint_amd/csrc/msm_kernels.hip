@@ -316,13 +316,19 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     else if (re == base + L && re < be) mw.part_last[t] = acc;
     else mw.part_first[t] = acc;
   };
+  // every lane's first run starts at entry 0: take that point as the
+  // accumulator (one multiply) instead of adding it to the identity (seven)
   ge_p3 acc;
-  ge_p3_identity(acc);
+  {
+    const niels_pt P = mw.pts[pt[0] >> 1];
+    const bool neg = pt[0] & 1;
+    niels_to_p3(acc, neg ? P.ymx : P.ypx, neg ? P.ypx : P.ymx);
+  }
   uint32_t cur = bk[0], rs = base;
-  uint32_t j = 0;
+  uint32_t j = 1;
   bool more = true;
 #pragma unroll
-  for (int q = 0; q < L; q++) {
+  for (int q = 1; q < L; q++) {
     more = more && bk[q] != kMsmEmpty;  // padding only follows the last bucket
     if (!more) continue;
     if (bk[q] != cur) {

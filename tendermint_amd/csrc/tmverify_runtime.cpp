@@ -157,7 +157,7 @@ struct HostLane {
   DeviceBuf h_in, d_in, h_out, d_out;
   uint32_t lo = 0, n = 0;  // chunk in flight (n == 0: idle)
 };
-constexpr int kLanes = 2;
+constexpr int kLanes = 4;  // streams per device; TMV_HOST_LANES of them carry chunks
 
 struct Device {
   int id = -1;
@@ -211,6 +211,8 @@ int g_zero_copy = 1;
 // pipelined in chunks (of half to one of these) over two lanes
 // (TMV_HOST_CHUNK).
 uint32_t g_host_chunk = 262144;
+// Lanes the chunks rotate over (TMV_HOST_LANES, 1..kLanes).
+uint32_t g_host_lanes = 2;
 
 void read_env() {
   static std::once_flag once;
@@ -228,6 +230,8 @@ void read_env() {
     if (zc) g_zero_copy = atoi(zc);
     const char *hc = getenv("TMV_HOST_CHUNK");
     if (hc) g_host_chunk = (uint32_t)strtoul(hc, nullptr, 10);
+    const char *hl = getenv("TMV_HOST_LANES");
+    if (hl) g_host_lanes = std::min<uint32_t>(kLanes, std::max<uint32_t>(1, (uint32_t)strtoul(hl, nullptr, 10)));
     const char *mc = getenv("TMV_MSM_CHUNK");
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
   });
@@ -1061,7 +1065,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
       const uint32_t len = bounds[s + 1] - bounds[s];
       const uint32_t c0 = bounds[s] + (uint32_t)((uint64_t)len * k / nchunks[s]);
       const uint32_t c1 = bounds[s] + (uint32_t)((uint64_t)len * (k + 1) / nchunks[s]);
-      HostLane &ln = d.lane[k % kLanes];
+      HostLane &ln = d.lane[k % g_host_lanes];
       (void)hipSetDevice(d.id);
       harvest(d, ln);  // the lane's previous chunk
       if (rc != 0) break;

@@ -1,0 +1,47 @@
+"""End-to-end (host buffers: pinned staging + PCIe + kernels + D2H) rate of
+the bench's 320k-signature C2 call under the current TMV_* environment
+(development tool).  The batch is generated once and cached in /tmp, so a
+shell loop can A/B runtime knobs in separate processes:
+
+  for l in 2 4; do TMV_HOST_LANES=$l python tools/e2e_probe.py; done
+"""
+import json, os, statistics, sys, time
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+from concurrent.futures import ProcessPoolExecutor
+import numpy as np
+
+CACHE = "/tmp/tmv_e2e_c2x32.npz"
+
+
+def _c2(seed):
+    from tendermint_amd.testing.factory import make_c2_batch
+    b = make_c2_batch(10_000, seed=seed)
+    return b.pk, b.sig, b.msg, b.off
+
+
+def main():
+    if not os.path.exists(CACHE):
+        with ProcessPoolExecutor(8) as ex:
+            parts = list(ex.map(_c2, [0xED25519 + j for j in range(32)]))
+        from tendermint_amd.testing.factory import Batch
+        hb = Batch.concat([Batch(pk, sig, msg, off) for pk, sig, msg, off in parts])
+        np.savez(CACHE, pk=hb.pk, sig=hb.sig, msg=hb.msg, off=hb.off)
+    z = np.load(CACHE)
+    pk, sig, msg, off = z["pk"], z["sig"], z["msg"], z["off"]
+    from tendermint_amd import _native as N
+    ctx = N.Context(1)
+    flags = N.TMV_FLAG_BATCH_EQUATION
+    n = len(off) - 1
+    ts = []
+    for i in range(9):
+        t = time.perf_counter()
+        ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, pk, sig, msg, off)
+        ts.append(time.perf_counter() - t)
+        assert int((st == 1).sum()) == 32 * 9950
+    m = statistics.median(ts[2:])
+    env = {k: v for k, v in os.environ.items() if k.startswith("TMV_")}
+    print(json.dumps({"env": env, "n": n, "median_ms": round(m * 1e3, 3), "e2e_verifies_per_s": round(n / m)}))
+
+
+if __name__ == "__main__":
+    main()
