@@ -186,7 +186,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    K = max(1, min(32, args.per_launch))
+    K = max(1, min(64, args.per_launch))
     F = max(1, args.inflight)
     # K distinct C2 batches per rank (own keys / messages), generated on the
     # host before this process touches the GPU (worker processes are forked)

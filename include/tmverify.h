@@ -126,6 +126,12 @@ int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bit
                           uint32_t opt_flags);
 /* Groups checked / failed since the context was opened (TMV_BATCHOPT_STATS). */
 int tmv_batch_stats(tmv_ctx *ctx, uint64_t *groups, uint64_t *groups_failed);
+/* Sub-groups of failing groups checked / failed (k_msm_subcheck: a failing
+ * group's sub-groups of 8 entries are re-checked with the same equation
+ * before entry-by-entry verification; TMV_BATCHOPT_STATS; 0 with
+ * TMV_SUBCHECK=0).  No reference counterpart (voi verifies a failing batch
+ * entry by entry, crypto/ed25519/ed25519.go:231-233). */
+int tmv_subgroup_stats(tmv_ctx *ctx, uint64_t *subgroups, uint64_t *subgroups_failed);
 /* Mixed batch with flags (see tmv_verify_mixed_batch). */
 int tmv_verify_mixed_batch_ex(tmv_ctx *ctx, uint32_t flags, const uint8_t *kind, const uint8_t *pk,
                               const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off, uint32_t n,
@@ -160,7 +166,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
  * written to its own d_status (as tmv_verify_batch_device_ex).  Verdicts are
  * per entry, so this equals n_batches separate calls; it only widens the
  * launches (a node draining a queue of batches, blocksync look-ahead).
- * msg_bytes = msg_off[n] - msg_off[0].  Up to 32 batches; key_kind
+ * msg_bytes = msg_off[n] - msg_off[0].  Up to 64 batches; key_kind
  * TMV_KIND_ED25519 or TMV_KIND_SR25519.  Asynchronous like the other
  * device-resident entry points. */
 typedef struct tmv_batch_ref {

@@ -43,6 +43,7 @@ EXPORTS = [
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
     "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
+    "tmv_subgroup_stats",
     "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
     "tmv_verify_votes", "tmv_vote_sign_bytes_device",
     # include/tmhost.h
@@ -122,6 +123,7 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.tmv_set_batch_options.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint32]
         L.tmv_batch_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.tmv_subgroup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.tmv_verify_mixed_batch_ex.argtypes = [vp, ctypes.c_uint32, u8p, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
         L.tmv_verify_batch_device_ex.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32, vp, vp, vp, vp,
                                                  vp, ctypes.c_uint32, vp, vp]
@@ -292,7 +294,9 @@ class Context:
     def batch_stats(self):
         g, f = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self._lib.tmv_batch_stats(self._h, ctypes.byref(g), ctypes.byref(f)), "tmv_batch_stats")
-        return {"groups": g.value, "failed": f.value}
+        sg, sf = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._lib.tmv_subgroup_stats(self._h, ctypes.byref(sg), ctypes.byref(sf)), "tmv_subgroup_stats")
+        return {"groups": g.value, "failed": f.value, "subgroups": sg.value, "sub_failed": sf.value}
 
     def verify_batch_device_ex(self, device: int, key_kind: int, flags: int, d_kind: int, d_pk: int, d_sig: int,
                                d_msg: int, d_off: int, n: int, d_status: int, stream: int = 0) -> None:

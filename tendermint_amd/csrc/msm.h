@@ -48,6 +48,8 @@ namespace tmv {
 constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 8, 16 or 32
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
+constexpr uint32_t kSubGroupLog2 = 3;        // k_msm_subcheck: 8 entries per sub-group
+constexpr uint32_t kSubGroup = 1u << kSubGroupLog2;
 
 // Affine Niels point padded to one 128-byte line.
 struct alignas(16) niels_pt {
@@ -115,6 +117,12 @@ struct MsmWork {
   ge_p3 *wsum;         // groups x W: window sums
   uint8_t *group_ok;   // groups
   uint32_t n_pts;      // index of B (= 2n)
+  // sub-group bisection of failing groups (k_msm_subcheck; null in the
+  // key-merged form, whose fallback is the key-cached comb)
+  uint32_t *fail_count;  // failing groups (reset by k_msm_sort, counted by k_msm_horner)
+  uint32_t *fail_list;   // groups: ids of the failing groups
+  uint8_t *sub_ok;       // groups x m / kSubGroup: verdict of each sub-group of a failing group
+  fe *tabR;              // n x 8 x 4 fe: k_msm_subcheck's tables of -R (its -A tables use Ed25519Work::tabA)
   // key-merged form only (null otherwise)
   uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
   uint32_t *bscal;     // groups x 8 words: B scalar of the group
@@ -129,6 +137,7 @@ struct MsmWork {
     size_t b = (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
                2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 16 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
+    else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16;
     return b;
   }
   static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
@@ -152,6 +161,15 @@ struct MsmWork {
     w.n_pts = 2 * n;
     w.wscal = w.bscal = nullptr;
     w.item_pt = nullptr;
+    w.fail_count = w.fail_list = nullptr;
+    w.sub_ok = nullptr;
+    w.tabR = nullptr;
+    if (!p.merged) {
+      w.fail_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
+      w.fail_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
+      w.sub_ok = b + o; o = up(o + (G << p.m_log2) / kSubGroup);
+      w.tabR = reinterpret_cast<fe *>(b + o); o = up(o + (size_t)n * 32 * sizeof(fe));
+    }
     if (p.merged) {
       w.wscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32ull * n);
       w.bscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32 * G);

@@ -6,6 +6,8 @@
 // the sorted entries (no atomics on points), and a per-group Horner
 // combination in quad-lane arithmetic (quad.h).  All integer VALU work.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <cstring>
 #include "ed25519_core.h"
 #include "kernel_util.h"
 #include "comb.h"
@@ -109,6 +111,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     bp.xy2d = btab_q[2];
     bp.pad[0] = bp.pad[1] = 0;
     mw.pts[mw.n_pts] = bp;
+    if (mw.fail_count) *mw.fail_count = 0;  // k_msm_horner appends the failing groups
   }
   if (e0 >= cnt) return;  // block-uniform
   const uint32_t mlive = min(p.m(), cnt - e0);
@@ -447,7 +450,217 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
   } else {
     ok = quad::is_identity_times8(acc);
   }
-  if (live && c == 0) mw.group_ok[g] = ok ? 1 : 0;
+  if (live && c == 0) {
+    mw.group_ok[g] = ok ? 1 : 0;
+    if (!ok && mw.fail_list) mw.fail_list[atomicAdd(mw.fail_count, 1u)] = g;
+  }
+}
+
+// Sub-group bisection (row H, before the per-entry fallback): a failing group
+// usually holds one bad signature, so instead of verifying all m entries one
+// by one, each sub-group of kSubGroup = 8 entries of a failing group is
+// checked with the same equation and the same z_i,
+//   T = [sum z_i s_i]B + sum [z_i](-R_i) + sum [z_i k_i](-A_i),
+// by Straus with shared doublings (64 signed radix-16 windows; the 128-bit
+// z_i need only the low 33; B digits radix 256 on even windows): 252
+// doublings + ~810 additions for 8 entries, against 8 x (252 + 96) per
+// entry.  Only the 16-entry fallback blocks holding a failing sub-group then
+// verify entry by entry.  One quad per sub-group (lane c holds coordinate c);
+// the failing groups come from k_msm_horner's list, so quads are dense.
+// A passing sub-group carries the same <= 2^-128 false-accept bound as a
+// group (z_i independent of the inputs).  Tables of (j+1)(-A), (j+1)(-R),
+// j < 8, go to global scratch (w.tabA / mw.tabR, written and read by the
+// same lane).
+template <bool SR>
+__global__ void __launch_bounds__(64)
+k_msm_subcheck(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+               uint32_t n, Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q,
+               int aligned) {
+  constexpr int kQ = 16;                           // quads (sub-groups) per wave
+  __shared__ int8_t dig[kQ][kSubGroup][2][64];     // [0]: z k mod l, [1]: z (33 digits used)
+  __shared__ int8_t bdig[kQ][32];
+  const uint32_t subs = *mw.fail_count << (p.m_log2 - kSubGroupLog2);
+  if (blockIdx.x * kQ >= subs) return;  // block-uniform
+  const int c = (int)(threadIdx.x & 3);
+  const int q = (int)(threadIdx.x >> 2);
+  const uint32_t raw = blockIdx.x * kQ + q;
+  const bool live = raw < subs;
+  const uint32_t t = live ? raw : subs - 1;  // whole quads stay active for DPP
+  const uint32_t sh = p.m_log2 - kSubGroupLog2;
+  const uint32_t g = mw.fail_list[t >> sh];
+  const uint32_t e0 = (g << p.m_log2) + ((t & ((1u << sh) - 1)) << kSubGroupLog2);
+  const uint32_t cnt = entry_count(count_ptr, n);
+
+  // scalars: lane c takes entries c and c + 4 (as k_msm_sort forms them)
+  uint32_t bacc[9];
+#pragma unroll
+  for (int u = 0; u < 9; u++) bacc[u] = 0;
+  uint8_t in_sum = 0;  // bit jj: entry jj is part of the sums (all lanes learn it below)
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int jj = c + 4 * h;
+    const uint32_t e = e0 + jj;
+    uint32_t z[8], wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) z[u] = wv[u] = 0;
+    if (e < cnt) {
+      const uint32_t i = idx ? idx[e] : e;
+      uint32_t s_raw[8], s[8];
+      if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+      else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+      bool s_ok;
+      if (SR) {
+        s_ok = sr25519_decode_s(s, s_raw);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8; u++) s[u] = s_raw[u];
+        s_ok = sc_is_canonical(s);
+      }
+      if (s_ok && w.flags[4 * e] && w.flags[4 * e + 1]) {
+        in_sum |= (uint8_t)(1u << jj);
+        uint32_t blk[16];
+        chacha20_block(blk, seed.key, e, seed.nonce);
+#pragma unroll
+        for (int u = 0; u < 4; u++) z[u] = blk[u];
+        uint32_t k[8];
+        const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * e);
+        const uint4 k0 = kp[0], k1 = kp[1];
+        k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w;
+        k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
+        sc_mul_mod(wv, z, 4, k);
+        uint32_t zs[8];
+        sc_mul_mod(zs, z, 4, s);
+        uint64_t cy = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          cy += (uint64_t)bacc[u] + zs[u];
+          bacc[u] = (uint32_t)cy;
+          cy >>= 32;
+        }
+        bacc[8] += (uint32_t)cy;
+      }
+    }
+    recode16_store(&dig[q][jj][0][0], wv, true);
+    recode16_store(&dig[q][jj][1][0], z, true);
+  }
+  // B scalar: sum over the quad (each lane < 2 l, the total < 2^256), mod l
+#pragma unroll
+  for (int x = 1; x <= 2; x <<= 1) {
+    uint32_t o[9];
+#pragma unroll
+    for (int u = 0; u < 9; u++) o[u] = (uint32_t)__shfl_xor((int)bacc[u], x, 4);
+    uint64_t cy = 0;
+#pragma unroll
+    for (int u = 0; u < 9; u++) {
+      cy += (uint64_t)bacc[u] + o[u];
+      bacc[u] = (uint32_t)cy;
+      cy >>= 32;
+    }
+  }
+  in_sum |= (uint8_t)__shfl_xor((int)in_sum, 1, 4);
+  in_sum |= (uint8_t)__shfl_xor((int)in_sum, 2, 4);
+  if (c == 0) {
+    uint32_t x[16], b[8];
+#pragma unroll
+    for (int u = 0; u < 16; u++) x[u] = u < 9 ? bacc[u] : 0;
+    sc_reduce512(b, x);
+    recode256_store(&bdig[q][0], b);
+  }
+
+  // tables of (j+1)(-R_e), (j+1)(-A_e) from the affine Niels points
+  // (y+x, y-x, 2dxy): P3 = (2E, 2H, 4, E H) with E = ypx - ymx, H = ypx + ymx
+#pragma unroll 1
+  for (int jj = 0; jj < (int)kSubGroup; jj++) {
+    if (!((in_sum >> jj) & 1)) continue;  // quad-uniform
+    const uint32_t e = e0 + jj;
+#pragma unroll 1
+    for (int ra = 0; ra < 2; ra++) {
+      const niels_pt &np = mw.pts[2ull * e + ra];
+      fe E, H, P;
+      fe_sub(E, np.ypx, np.ymx);
+      fe_add(H, np.ypx, np.ymx);
+      fe_mul(P, E, H);  // T (every lane: quad-uniform work)
+      if (c == 0) { fe_add(E, E, E); fe_carry(P, E); }
+      else if (c == 1) { fe_add(H, H, H); fe_carry(P, H); }
+      else if (c == 2) { fe_zero(P); P.v[0] = 4; }
+      fe *tab = (ra ? w.tabA : mw.tabR) + 32ull * e;
+      fe r, Pm, Q, Q0;
+      quad::to_cached(Q0, P);
+      tab[c] = Q0;
+      quad::dbl(r, P);
+      quad::p1p1_to_p3(Pm, r);
+      quad::to_cached(Q, Pm);
+      tab[4 + c] = Q;
+      for (int m = 2; m < 8; m++) {
+        quad::add(r, Pm, Q0);
+        quad::p1p1_to_p3(Pm, r);
+        quad::to_cached(Q, Pm);
+        tab[m * 4 + c] = Q;
+      }
+    }
+  }
+  __syncthreads();  // digits written by other lanes (one wave per block)
+
+  // Straus: 64 windows; per window 8 A additions, 8 R additions (windows <=
+  // 32), one B addition (even windows), each addend loaded one addition
+  // ahead (the window's first one before its doublings).  Entries left out
+  // (or past the batch end, whose table slots may lie past the scratch) read
+  // a B-table entry and add the identity.
+  const fe *tA = w.tabA + 32ull * e0 + c;
+  const fe *tR = mw.tabR + 32ull * e0 + c;
+  auto adds_in = [](int wdx) { return 8 + (wdx <= 32 ? 8 : 0) + ((wdx & 1) ? 0 : 1); };
+  auto fetch = [&](int wdx, int k, int &d) -> fe {
+    if (k < 16) {
+      const int jj = k & 7;
+      const bool in = (in_sum >> jj) & 1;
+      d = in ? dig[q][jj][k >> 3][wdx] : 0;
+      const int a = d < 0 ? -d : d;
+      return in ? (k < 8 ? tA : tR)[32 * jj + (a ? a - 1 : 0) * 4] : btab_q[c];
+    }
+    d = bdig[q][wdx >> 1];
+    const int a = d < 0 ? -d : d;
+    return btab_q[(a ? a - 1 : 0) * 4 + c];
+  };
+  fe idq, acc, r, nxt;
+  int dn;
+  quad::cached_identity(idq);
+  quad::p3_identity(acc);
+  nxt = fetch(63, 0, dn);
+#pragma unroll 1
+  for (int wdx = 63; wdx >= 0; wdx--) {
+    if (wdx != 63) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        quad::dbl(r, acc);
+        quad::p1p1_to_p3(acc, r);
+      }
+    }
+    const int na = adds_in(wdx);
+#pragma unroll 1
+    for (int k = 0; k < na; k++) {
+      fe ent = nxt;
+      const int d = dn;
+      if (k + 1 < na) {
+        const int kn = (k + 1 >= 8 && wdx > 32) ? 16 : k + 1;  // a window > 32 has no R additions
+        nxt = fetch(wdx, kn, dn);
+      } else if (wdx > 0) {
+        nxt = fetch(wdx - 1, 0, dn);
+      }
+      fe_cmov(ent, idq, d == 0);
+      quad::cached_cneg(ent, d < 0);
+      quad::add(r, acc, ent);
+      quad::p1p1_to_p3(acc, r);
+    }
+  }
+  bool ok;
+  if (SR) {
+    fe id;
+    quad::p3_identity(id);
+    ok = quad::ristretto_equal(acc, id);
+  } else {
+    ok = quad::is_identity_times8(acc);
+  }
+  if (live && c == 0) mw.sub_ok[e0 >> kSubGroupLog2] = ok ? 1 : 0;
 }
 
 // Bucket sums, window parts and window sums (shared by both forms).
@@ -471,6 +684,25 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
   return hipGetLastError();
 }
 
+// Sub-group bisection is worth its latency only for large groups: measured
+// on C5 (1M mixed, ~1% invalid, one launch): m = 64 16.2 ms without, 16.9 ms
+// with; m = 256 20.2 ms without, 19.4 ms with; the C2 bench (m = 64, 4
+// launches in flight) 76.3 vs 69.7 M/s -- the check is a ~1.1k-addition
+// chain per quad that lengthens every launch's critical path by ~1.4 ms.
+// Default: groups of >= 256 entries.  TMV_SUBCHECK=0 never, =1 always.
+static int subcheck_mode() {
+  static const int mode = [] {
+    const char *e = getenv("TMV_SUBCHECK");
+    if (!e) return -1;
+    return strcmp(e, "0") ? 1 : 0;
+  }();
+  return mode;
+}
+bool subcheck_enabled(uint32_t m_log2) {
+  const int mode = subcheck_mode();
+  return mode < 0 ? m_log2 >= 8 : mode == 1;
+}
+
 template <bool SR>
 static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                                const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const fe *btab_q,
@@ -489,7 +721,17 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
                      nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream);
+  const uint8_t *sub_ok = nullptr;
+  if (subcheck_enabled(p.m_log2)) {
+    // grid for every group failing; blocks past the failing count exit at once
+    const uint64_t subs = (uint64_t)p.groups << (p.m_log2 - kSubGroupLog2);
+    hipLaunchKernelGGL(k_msm_subcheck<SR>, dim3((uint32_t)((subs + 15) / 16)), dim3(64), 0, stream, sig, idx,
+                       count_ptr, n, w, mw, p, seed, btab_q, aligned);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    sub_ok = mw.sub_ok;
+  }
+  return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream,
+                                  sub_ok);
 }
 
 // Key-merged form: one quad per item.  Items [0, n_runs) are runs of one key

@@ -144,6 +144,7 @@ struct Workspace {
   hipEvent_t done = nullptr;
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
+  const uint8_t *sub_ok[2] = {nullptr, nullptr};  // sub-group verdicts (k_msm_subcheck), if it ran
   uint32_t groups = 0, m_log2 = 0;
   const uint32_t *counts = nullptr;  // mixed launches: per-kind entry counts on the device
 };
@@ -306,7 +307,7 @@ struct tmv_ctx {
   bool fixed_seed = false, stats = false;
   uint8_t seed[32] = {0};
   std::atomic<uint64_t> launches{0};
-  std::atomic<uint64_t> groups{0}, groups_failed{0};
+  std::atomic<uint64_t> groups{0}, groups_failed{0}, subgroups{0}, subgroups_failed{0};
   std::mutex opt_mu;
 };
 
@@ -364,8 +365,20 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
     for (uint8_t v : ok) failed += v ? 0 : 1;
     ctx->groups += live[k];
     ctx->groups_failed += failed;
+    if (!w.sub_ok[k] || !failed) continue;
+    // sub-groups of the failing groups (the only ones k_msm_subcheck writes)
+    const uint32_t per = 1u << (w.m_log2 - tmv::kSubGroupLog2);
+    std::vector<uint8_t> sub((size_t)live[k] * per);
+    if (hipMemcpy(sub.data(), w.sub_ok[k], sub.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t sfail = 0;
+    for (uint32_t g = 0; g < live[k]; g++)
+      if (!ok[g])
+        for (uint32_t j = 0; j < per; j++) sfail += sub[(size_t)g * per + j] ? 0 : 1;
+    ctx->subgroups += failed * per;
+    ctx->subgroups_failed += sfail;
   }
   w.group_ok[0] = w.group_ok[1] = nullptr;
+  w.sub_ok[0] = w.sub_ok[1] = nullptr;
 }
 
 static int init_device(Device &d) {
@@ -646,6 +659,8 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   if (e != hipSuccess) { set_error("batch check launch", e); return TMV_ERR_LAUNCH; }
   ws->group_ok[0] = mw.group_ok;
   ws->group_ok[1] = nullptr;
+  ws->sub_ok[0] = tmv::subcheck_enabled(o.p.m_log2) ? mw.sub_ok : nullptr;
+  ws->sub_ok[1] = nullptr;
   ws->groups = (n + o.p.m() - 1) >> o.p.m_log2;
   ws->m_log2 = o.p.m_log2;
   ws->counts = nullptr;
@@ -683,6 +698,8 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
                                       o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s);
     ws->group_ok[0] = m1.group_ok;
     ws->group_ok[1] = m2.group_ok;
+    ws->sub_ok[0] = tmv::subcheck_enabled(o.p.m_log2) ? m1.sub_ok : nullptr;
+    ws->sub_ok[1] = tmv::subcheck_enabled(o.p.m_log2) ? m2.sub_ok : nullptr;
     ws->groups = o.p.groups;
     ws->m_log2 = o.p.m_log2;
     ws->counts = counts;
@@ -723,6 +740,7 @@ static int launch_key_merged(Device &d, const LaunchOpts &o, bool sr, const uint
   if (e != hipSuccess) { set_error("key-merged check launch", e); return TMV_ERR_LAUNCH; }
   ws->group_ok[0] = mw.group_ok;
   ws->group_ok[1] = nullptr;
+  ws->sub_ok[0] = ws->sub_ok[1] = nullptr;
   ws->groups = o.p.groups;
   ws->m_log2 = o.p.m_log2;
   ws->counts = nullptr;
@@ -1249,6 +1267,13 @@ int tmv_batch_stats(tmv_ctx *ctx, uint64_t *groups, uint64_t *groups_failed) {
   if (!ctx) return TMV_ERR_ARG;
   if (groups) *groups = ctx->groups.load();
   if (groups_failed) *groups_failed = ctx->groups_failed.load();
+  return 0;
+}
+
+int tmv_subgroup_stats(tmv_ctx *ctx, uint64_t *subgroups, uint64_t *subgroups_failed) {
+  if (!ctx) return TMV_ERR_ARG;
+  if (subgroups) *subgroups = ctx->subgroups.load();
+  if (subgroups_failed) *subgroups_failed = ctx->subgroups_failed.load();
   return 0;
 }
 

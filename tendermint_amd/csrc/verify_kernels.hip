@@ -155,7 +155,7 @@ template <bool SR, bool GT>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
-              const uint8_t *__restrict__ group_ok, uint32_t group_log2) {
+              const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok) {
   __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
   const uint32_t m = entry_count(count_ptr, n);
@@ -169,7 +169,18 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   // Batch equation held for this block's group (groups are >= 32 entries, so
   // the test is block-uniform): every entry that passed decoding and the S
   // check is valid; the rest keep their pre-check status.
-  if (group_ok && group_ok[(blockIdx.x * kQuadSigs) >> group_log2]) {
+  // With the sub-group verdicts (k_msm_subcheck) a block of a failing group
+  // passes when every sub-group it covers passed.
+  bool pass = false;
+  if (group_ok) {
+    const uint32_t b0 = blockIdx.x * kQuadSigs;
+    pass = group_ok[b0 >> group_log2];
+    if (!pass && sub_ok) {
+      pass = true;
+      for (uint32_t s = b0 >> kSubGroupLog2; s <= (b0 + kQuadSigs - 1) >> kSubGroupLog2; s++) pass = pass && sub_ok[s];
+    }
+  }
+  if (pass) {
     if (!live || c != 0) return;
     uint32_t s_raw[8], s_w[8];
     if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
@@ -697,13 +708,14 @@ static bool quad_table_global() {
 template <bool SR>
 static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig, const uint32_t *idx,
                         const uint32_t *count_ptr, uint32_t n, Ed25519Work w, const fe *btab_q, uint8_t *out,
-                        int aligned, const uint8_t *group_ok, uint32_t group_log2) {
+                        int aligned, const uint8_t *group_ok, uint32_t group_log2,
+                        const uint8_t *sub_ok = nullptr) {
   if (quad_table_global())
     hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
-                       w, btab_q, out, aligned, group_ok, group_log2);
+                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok);
   else
     hipLaunchKernelGGL((k_verify_quad<SR, false>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
-                       w, btab_q, out, aligned, group_ok, group_log2);
+                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok);
 }
 
 static int is_aligned(const void *a, const void *b) {
@@ -729,17 +741,17 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
 template <bool SR>
 hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                                 const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
-                                uint8_t *out, int aligned, hipStream_t stream) {
+                                uint8_t *out, int aligned, hipStream_t stream, const uint8_t *sub_ok) {
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2);
+  launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok);
   return hipGetLastError();
 }
 template hipError_t launch_quad_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
                                                 const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
-                                                hipStream_t);
+                                                hipStream_t, const uint8_t *);
 template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
                                                const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
-                                               hipStream_t);
+                                               hipStream_t, const uint8_t *);
 
 template <bool SR>
 hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,

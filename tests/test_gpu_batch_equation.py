@@ -35,12 +35,15 @@ def honest():
     return make_commit_batch(1500)
 
 
-def _run(ctx, kind, b, **opts):
+def _run(ctx, kind, b, sub=False, **opts):
     ctx.set_batch_options(seed=opts.pop("seed", SEED), stats=True, **opts)
     s0 = ctx.batch_stats()
     ok, st = ctx.verify_batch_ex(kind, BEQ, b.pk, b.sig, b.msg, b.off)
     s1 = ctx.batch_stats()
-    return ok, st, s1["groups"] - s0["groups"], s1["failed"] - s0["failed"]
+    r = (ok, st, s1["groups"] - s0["groups"], s1["failed"] - s0["failed"])
+    if sub:
+        r += (s1["subgroups"] - s0["subgroups"], s1["sub_failed"] - s0["sub_failed"])
+    return r
 
 
 def test_c2_full_size_bit_exact(bctx, golden):
@@ -53,6 +56,50 @@ def test_c2_full_size_bit_exact(bctx, golden):
     # exactly the groups holding a bit-flipped entry that still decodes fail
     want = C.failing_groups(C.ed25519_prechecks(b.pk, b.sig), st == 1, 64)
     assert 0 < want <= 20 and failed == want, (failed, want)
+
+
+def test_c2_subgroups_bisect(bctx):
+    """k_msm_subcheck (groups >= 256): every sub-group (8 entries) of a failing group is
+    re-checked; exactly those holding a pre-valid invalid entry fail, so the
+    per-entry fallback only runs over the 16-entry blocks that hold them."""
+    b = make_c2_batch()
+    ok, st, groups, failed, subs, sub_failed = _run(bctx, ED, b, sub=True, group_log2=8)
+    pre = C.ed25519_prechecks(b.pk, b.sig)
+    assert failed == C.failing_groups(pre, st == 1, 256) and failed > 0
+    assert subs == failed * 32
+    assert sub_failed == C.failing_groups(pre, st == 1, 8) and 0 < sub_failed < subs
+    # m = 64 (the default for C2-sized launches) skips the bisection
+    ok, st2, groups, failed, subs, sub_failed = _run(bctx, ED, b, sub=True)
+    assert np.array_equal(st, st2) and failed > 0 and subs == 0
+
+
+@pytest.mark.parametrize("n,bad", [
+    (200, [0]), (200, [7, 8]), (200, [63, 64, 127]), (600, [255, 256, 511]), (1000, list(range(256, 512))),
+    (1000, list(range(0, 1000, 9))), (999, [998]), (1001, [1000, 992]), (65, [64]),
+])
+def test_subgroup_placements(bctx, n, bad):
+    """Invalid signatures at sub-group / block / group edges, whole failing
+    groups, dense failures and ragged tails: the vector equals the oracle's
+    and exactly the sub-groups holding a pre-valid invalid entry fail."""
+    b = make_commit_batch(n, seed=11)
+    sig = b.sig.copy()
+    for i in bad:
+        sig[64 * i + 5] ^= 0x10  # R byte: R mostly still decodes, the equation fails
+    ok_o, vec_o = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=4)
+    ok, st, groups, failed, subs, sub_failed = _run(bctx, ED, _B(b.pk, sig, b.msg, b.off), sub=True, group_log2=8)
+    assert ok == ok_o and np.array_equal(st.astype(np.uint8), vec_o)
+    pre = C.ed25519_prechecks(b.pk, sig)
+    assert failed == C.failing_groups(pre, vec_o == 1, 256) and subs == failed * 32
+    assert sub_failed == C.failing_groups(pre, vec_o == 1, 8)
+
+
+def test_sr25519_subgroups(bctx):
+    b = make_sr25519_batch(600, seed=9, bad_frac=0.02)
+    ok, st, groups, failed, subs, sub_failed = _run(bctx, SR, b, sub=True, group_log2=8)
+    ref = C.sr25519_status_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    assert np.array_equal(st, ref)
+    pre = C.sr25519_prechecks(b.pk, b.sig)
+    assert failed > 0 and subs == failed * 32 and sub_failed == C.failing_groups(pre, ref == 1, 8)
 
 
 def test_honest_groups_pass(bctx, honest):
