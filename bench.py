@@ -78,7 +78,7 @@ def _load_pmc(method: str):
     """PMC summary of a launch of 32 C2 batches from the committed passes
     (tools/profile_round.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950
     correction + WRITE_SIZE; tools/pmc_derived.py: occupancy, VALU issue)."""
-    path = (os.path.join(REPO, "profiles", "r01_final", "pmc_batch.json") if method == "batch"
+    path = (os.path.join(REPO, "profiles", "r01_close", "pmc_batch.json") if method == "batch"
             else os.path.join(REPO, "profiles", "r01_msm", "pmc_per_entry.json"))
     try:
         with open(path) as f:
@@ -325,7 +325,7 @@ def main():
             "roofline": {"bound": "valu-int-mul", "achieved": round(achieved / 1e12, 4),
                          "peak": round(peak / 1e12, 4), "unit": "Tmul/s", "frac": round(achieved / peak, 4),
                          "traffic": _load_traffic(args.method) if K == 32 else None,
-                         "traffic_note": "HBM bytes per launch (PMC, profiles/r01_final/pmc_batch.json); algorithmic "
+                         "traffic_note": "HBM bytes per launch (PMC, profiles/r01_close/pmc_batch.json); algorithmic "
                                          "input bytes per launch = 32 x 10k x ~222 B = 71 MB",
                          "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if args.method == "batch"
                                     else "k_prep + k_verify_quad"),
