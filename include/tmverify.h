@@ -126,6 +126,17 @@ int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bit
                           uint32_t opt_flags);
 /* Groups checked / failed since the context was opened (TMV_BATCHOPT_STATS). */
 int tmv_batch_stats(tmv_ctx *ctx, uint64_t *groups, uint64_t *groups_failed);
+/* ValidatorSet.Hash of n_sets validator sets in one launch (SURVEY §8(f)
+ * rank 4): replaces types/validator_set.go:344-350 (merkle.HashFromByteSlices,
+ * crypto/merkle/tree.go:11-27, over Validator.Bytes(), types/validator.go:
+ * 154-170), as the light client checks it per header (light/verifier.go:266).
+ * Set s holds validators [set_off[s], set_off[s+1]) in set order; validator
+ * i: pk + 32*i, key_kind[i] (TMV_KIND_ED25519 / TMV_KIND_SR25519; secp256k1
+ * keys are not supported), power[i].  hash_out: n_sets x 32 bytes (an empty
+ * set hashes to SHA-256(""), as the reference).  set_off[0] must be 0.
+ * Synchronous; 0 or < 0 on error. */
+int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key_kind, const int64_t *power,
+                             const uint32_t *set_off, uint32_t n_sets, uint8_t *hash_out);
 /* Sub-groups of failing groups checked / failed (k_msm_subcheck: a failing
  * group's sub-groups of 8 entries are re-checked with the same equation
  * before entry-by-entry verification; TMV_BATCHOPT_STATS; 0 with

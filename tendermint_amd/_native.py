@@ -43,7 +43,7 @@ EXPORTS = [
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
     "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
-    "tmv_subgroup_stats",
+    "tmv_subgroup_stats", "tmv_validator_set_hashes",
     "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
     "tmv_verify_votes", "tmv_vote_sign_bytes_device",
     # include/tmhost.h
@@ -124,6 +124,8 @@ def lib() -> ctypes.CDLL:
         L.tmv_set_batch_options.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint32]
         L.tmv_batch_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.tmv_subgroup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.tmv_validator_set_hashes.argtypes = [vp, u8p, u8p, ctypes.POINTER(ctypes.c_int64), u32p,
+                                               ctypes.c_uint32, u8p]
         L.tmv_verify_mixed_batch_ex.argtypes = [vp, ctypes.c_uint32, u8p, u8p, u8p, u8p, u32p, ctypes.c_uint32, i8p]
         L.tmv_verify_batch_device_ex.argtypes = [vp, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint32, vp, vp, vp, vp,
                                                  vp, ctypes.c_uint32, vp, vp]
@@ -290,6 +292,20 @@ class Context:
         self._check(self._lib.tmv_set_batch_options(self._h, group_log2, window_bits, sp,
                                                     TMV_BATCHOPT_STATS if stats else 0),
                     "tmv_set_batch_options")
+
+    def validator_set_hashes(self, pk: np.ndarray, kind: np.ndarray, power: np.ndarray,
+                             set_off: np.ndarray) -> np.ndarray:
+        """ValidatorSet.Hash of each set (tmv_validator_set_hashes): (n_sets, 32) uint8."""
+        n_sets = len(set_off) - 1
+        out = np.zeros((max(n_sets, 1), 32), np.uint8)
+        pk = np.ascontiguousarray(pk, np.uint8) if len(pk) else np.zeros(32, np.uint8)
+        kind = np.ascontiguousarray(kind, np.uint8) if len(kind) else np.zeros(1, np.uint8)
+        power = np.ascontiguousarray(power, np.int64) if len(power) else np.zeros(1, np.int64)
+        set_off = np.ascontiguousarray(set_off, np.uint32)
+        self._check(self._lib.tmv_validator_set_hashes(self._h, _p(pk), _p(kind), _p(power, ctypes.c_int64),
+                                                       _p(set_off, ctypes.c_uint32), n_sets, _p(out)),
+                    "tmv_validator_set_hashes")
+        return out[:n_sets]
 
     def batch_stats(self):
         g, f = ctypes.c_uint64(), ctypes.c_uint64()

@@ -11,15 +11,17 @@ signature path one commit at a time:
 Here every commit check of a window of headers/blocks is planned on the host
 and all their signatures go to the GPU in ONE tmv_verify_commits call; the
 per-header / per-block results are then walked in order, so the first error
-returned is the one the sequential reference loop would return.  Header
-hashing (ValidatorSet.Hash merkle, header hash) is outside this engine's
-scope: headers carry those hashes as opaque bytes and are compared as the
-reference compares them.
+returned is the one the sequential reference loop would return.  The
+ValidatorSet.Hash of every supplied set of a window (light/verifier.go:266,
+SURVEY §8(f) rank 4) is computed on the GPU in one tmv_validator_set_hashes
+call; the header hash itself is not (headers carry it as opaque bytes).
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
+
+import numpy as np
 
 from . import host as H
 
@@ -44,9 +46,31 @@ def _after(a: Tuple[int, int], b: Tuple[int, int]) -> bool:
     return a > b
 
 
-def verify_adjacent_checks(trusted: SignedHeader, untrusted: SignedHeader) -> Optional[str]:
+def validator_set_arrays(sets: List[H.ValidatorSet]):
+    """Column arrays of tmv_validator_set_hashes for `sets` (set order kept)."""
+    vals = [v for vs in sets for v in vs.validators]
+    n = len(vals)
+    pk = np.frombuffer(b"".join(v.pub_key for v in vals), np.uint8) if n else np.zeros(0, np.uint8)
+    kind = np.fromiter((v.key_kind for v in vals), np.uint8, count=n)
+    power = np.fromiter((v.voting_power for v in vals), np.int64, count=n)
+    off = np.zeros(len(sets) + 1, np.uint32)
+    off[1:] = np.cumsum([len(vs.validators) for vs in sets])
+    return pk, kind, power, off
+
+
+def validator_set_hashes(ctx, sets: List[H.ValidatorSet]) -> List[bytes]:
+    """ValidatorSet.Hash (types/validator_set.go:344-350) of each set, one GPU call."""
+    if not sets:
+        return []
+    out = ctx.validator_set_hashes(*validator_set_arrays(sets))
+    return [bytes(r) for r in out]
+
+
+def verify_adjacent_checks(trusted: SignedHeader, untrusted: SignedHeader,
+                           untrusted_vals_hash: Optional[bytes] = None) -> Optional[str]:
     """The non-signature checks of light.VerifyAdjacent (light/verifier.go:115-150)
-    that this engine's callers need, in the reference's order and text."""
+    that this engine's callers need, in the reference's order and text;
+    `untrusted_vals_hash` = Hash() of the supplied set (verifier.go:266)."""
     if trusted.height == 0:
         return "height in trusted header must be set (non zero"
     if not trusted.chain_id:
@@ -57,6 +81,10 @@ def verify_adjacent_checks(trusted: SignedHeader, untrusted: SignedHeader) -> Op
         return "headers must be adjacent in height"
     if not _after(untrusted.time, trusted.time):
         return "invalid header: expected new header time to be after old header time"
+    if untrusted_vals_hash is not None and untrusted.validators_hash != untrusted_vals_hash:
+        return ("invalid header: expected new header validators (%s) to match those that were supplied (%s) "
+                "at height %d" % (untrusted.validators_hash.hex().upper(), untrusted_vals_hash.hex().upper(),
+                                  untrusted.height))
     if untrusted.validators_hash != trusted.next_validators_hash:
         return ("invalid header: expected old header's next validators (%s) to match those from new header (%s)"
                 % (trusted.next_validators_hash.hex().upper(), untrusted.validators_hash.hex().upper()))
@@ -74,8 +102,9 @@ def verify_sequential(ctx, trusted: SignedHeader, blocks: List[LightBlock], wind
         jobs = [H.CommitJob(H.MODE_LIGHT, trusted.chain_id, lb.vals, lb.header.commit.block_id, lb.header.height,
                             lb.header.commit) for lb in chunk]
         res = H.verify_commits(ctx, jobs)
-        for lb, err in zip(chunk, res):
-            e = verify_adjacent_checks(trusted, lb.header)
+        vhash = validator_set_hashes(ctx, [lb.vals for lb in chunk])
+        for lb, err, vh in zip(chunk, res, vhash):
+            e = verify_adjacent_checks(trusted, lb.header, vh)
             if e is None and err is not None:
                 e = "invalid header: " + err
             if e is not None:

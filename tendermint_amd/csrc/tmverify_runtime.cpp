@@ -30,6 +30,7 @@
 #include "host/pool.h"
 #include "verify_kernels.h"
 #include "votes.h"
+#include "valset.h"
 
 namespace {
 
@@ -184,6 +185,7 @@ struct Device {
   std::vector<uint8_t> kseen;  // resolve_keys: slots found, per lookup part
   uint64_t kepoch = 0, khits = 0, kmisses = 0;
   DeviceBuf d_kbuild, h_kbuild;
+  DeviceBuf d_valset, h_valset;  // tmv_validator_set_hashes staging
   // host-buffer launches: key slots of the shard and the per-chunk key
   // histograms of the key-merged form's counting sort
   std::vector<uint32_t> slots, key_count;
@@ -1337,7 +1339,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
     return TMV_ERR_ARG;
   }
   if (n_batches == 0 || n_batches > tmv::kMaxBatches || !batches) {
-    set_error("tmv_verify_batches_device: 1..32 batches");
+    set_error("tmv_verify_batches_device: 1..64 batches");
     return TMV_ERR_ARG;
   }
   tmv::BatchRefs r{};
@@ -1389,6 +1391,62 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   if ((e = tmv::launch_scatter(r, gst, s)) != hipSuccess) { set_error("scatter launch", e); return TMV_ERR_LAUNCH; }
   (void)hipEventRecord(ws->done, s);
   return TMV_NOT_ALL;
+}
+
+// ValidatorSet.Hash of many sets in one launch (SURVEY §8(f) rank 4;
+// types/validator_set.go:344-350).  Synchronous, host buffers.
+int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key_kind, const int64_t *power,
+                             const uint32_t *set_off, uint32_t n_sets, uint8_t *hash_out) {
+  if (!ctx || ctx->devs.empty()) { set_error("null context"); return TMV_ERR_ARG; }
+  if (n_sets == 0) return 0;
+  if (!set_off || !hash_out) { set_error("tmv_validator_set_hashes: null pointer"); return TMV_ERR_ARG; }
+  if (set_off[0] != 0) { set_error("tmv_validator_set_hashes: set_off[0] must be 0"); return TMV_ERR_ARG; }
+  for (uint32_t s = 0; s < n_sets; s++)
+    if (set_off[s + 1] < set_off[s]) { set_error("tmv_validator_set_hashes: set_off decreasing"); return TMV_ERR_ARG; }
+  const uint32_t n = set_off[n_sets];
+  if (n && (!pk || !key_kind || !power)) { set_error("tmv_validator_set_hashes: null pointer"); return TMV_ERR_ARG; }
+  if (n > (1u << 26)) { set_error("tmv_validator_set_hashes: too many validators"); return TMV_ERR_ARG; }
+  for (uint32_t i = 0; i < n; i++)
+    if (key_kind[i] != TMV_KIND_ED25519 && key_kind[i] != TMV_KIND_SR25519) {
+      set_error("tmv_validator_set_hashes: key kind must be ed25519 or sr25519");
+      return TMV_ERR_ARG;
+    }
+  Device &d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  hipError_t e = hipSetDevice(d.id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  // staging: power | set_off | pk | kind, then (device only) two node arrays and the roots
+  const size_t o_off = align16(8ull * n), o_pk = o_off + align16(4ull * (n_sets + 1));
+  const size_t o_kind = o_pk + align16(32ull * n), in_bytes = o_kind + align16(n);
+  const size_t o_na = in_bytes, o_nb = o_na + 32ull * n, o_out = o_nb + 32ull * n;
+  const size_t dev_bytes = o_out + 32ull * n_sets;
+  hipStream_t s = d.stream;
+  (void)hipStreamSynchronize(s);  // staging buffers may still feed an earlier call
+  if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  uint8_t *h = static_cast<uint8_t *>(d.h_valset.ptr);
+  if (n) {
+    std::memcpy(h, power, 8ull * n);
+    std::memcpy(h + o_pk, pk, 32ull * n);
+    std::memcpy(h + o_kind, key_kind, n);
+  }
+  std::memcpy(h + o_off, set_off, 4ull * (n_sets + 1));
+  uint8_t *g = static_cast<uint8_t *>(d.d_valset.ptr);
+  if ((e = hipMemcpyAsync(g, h, in_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) {
+    set_error("hipMemcpyAsync(valset)", e);
+    return TMV_ERR_LAUNCH;
+  }
+  e = tmv::launch_valset_hashes(g + o_pk, g + o_kind, reinterpret_cast<const int64_t *>(g), n,
+                                reinterpret_cast<const uint32_t *>(g + o_off), n_sets,
+                                reinterpret_cast<uint32_t *>(g + o_na), reinterpret_cast<uint32_t *>(g + o_nb),
+                                g + o_out, s);
+  if (e != hipSuccess) { set_error("valset hash launch", e); return TMV_ERR_LAUNCH; }
+  if ((e = hipMemcpyAsync(hash_out, g + o_out, 32ull * n_sets, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipStreamSynchronize(s)) != hipSuccess) {
+    set_error("valset hash readback", e);
+    return TMV_ERR_LAUNCH;
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -278,12 +278,36 @@ def make_c1_commit(n_vals: int = 150, chain_id: str = "test_chain_id", height: i
     return vals, hbid, H.Commit(height, 0, hbid, sigs)
 
 
+def _simple_validator_bytes(v) -> bytes:
+    """Validator.Bytes() (types/validator.go:154-170): SimpleValidator protobuf."""
+    pub = bytes([(3 if v.key_kind == 1 else 1) << 3 | 2, 32]) + v.pub_key  # kind 1 = sr25519: oneof field 3
+    out = bytes([0x0A, len(pub)]) + pub
+    if v.voting_power:
+        u, var = v.voting_power & ((1 << 64) - 1), bytearray()
+        while True:
+            var.append((u & 0x7F) | (0x80 if u >> 7 else 0))
+            u >>= 7
+            if not u:
+                break
+        out += b"\x10" + bytes(var)
+    return out
+
+
+def _merkle(items) -> bytes:
+    """merkle.HashFromByteSlices (crypto/merkle/tree.go:11-27)."""
+    if not items:
+        return hashlib.sha256(b"").digest()
+    if len(items) == 1:
+        return hashlib.sha256(b"\x00" + items[0]).digest()
+    k = 1 << (len(items).bit_length() - 1)
+    k = k >> 1 if k == len(items) else k
+    return hashlib.sha256(b"\x01" + _merkle(items[:k]) + _merkle(items[k:])).digest()
+
+
 def _valset_hash(vals) -> bytes:
-    """Stand-in for ValidatorSet.Hash (merkle, out of scope): SHA-256 over the keys and powers."""
-    h = hashlib.sha256()
-    for v in vals.validators:
-        h.update(v.pub_key + v.voting_power.to_bytes(8, "little"))
-    return h.digest()
+    """ValidatorSet.Hash (types/validator_set.go:344-350) of the generated set,
+    so headers carry the hash the light client checks (light/verifier.go:266)."""
+    return _merkle([_simple_validator_bytes(v) for v in vals.validators])
 
 
 def make_light_chain(n_headers: int, n_vals: int = 100, chain_id: str = "test", rotate: int = 1, seed: int = 7):

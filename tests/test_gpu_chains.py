@@ -39,7 +39,13 @@ def test_light_sequential_first_error_matches_single(ctx):
 
 def test_light_broken_validator_chain(ctx):
     trusted, blocks = make_light_chain(10, 10)
+    # header's ValidatorsHash no longer the supplied set's Hash() (light/verifier.go:266)
     blocks[4].header.validators_hash = b"\x00" * 32
+    n, err = chains.verify_sequential(ctx, trusted, blocks)
+    assert n == 4 and "to match those that were supplied" in err
+    # previous header's NextValidatorsHash differs (light/verifier.go:140-145)
+    trusted, blocks = make_light_chain(10, 10)
+    blocks[3].header.next_validators_hash = b"\x00" * 32
     n, err = chains.verify_sequential(ctx, trusted, blocks)
     assert n == 4 and "to match those from new header" in err
 
