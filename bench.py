@@ -169,7 +169,7 @@ def _c2(a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=384)
+    ap.add_argument("--steps", type=int, default=1536)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--batch", type=int, default=10_000)
     ap.add_argument("--per-launch", type=int, default=32,
