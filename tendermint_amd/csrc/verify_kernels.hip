@@ -59,11 +59,11 @@ k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig
 // k_prep_hash (one lane per entry: SHA-512 + Barrett, or the merlin
 // transcript).
 template <bool SR>
-__global__ void __launch_bounds__(kVerifyBlock, SR ? 2 : TMV_DECODE_WAVES)
-k_prep_decode(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
-              const uint32_t *count_ptr, uint32_t n, Ed25519Work w, int aligned) {
+__device__ __forceinline__ void prep_decode_block(uint32_t bx, const uint8_t *__restrict__ pk,
+                                                  const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
+                                                  const uint32_t *count_ptr, uint32_t n, Ed25519Work w, int aligned) {
   const uint32_t m = entry_count(count_ptr, n);
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = bx * blockDim.x + threadIdx.x;
   if (j >= 2 * m) return;
   const bool isA = j < m;
   const uint32_t e = isA ? j : j - m;
@@ -108,12 +108,13 @@ k_prep_decode(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
 }
 
 template <bool SR>
-__global__ void __launch_bounds__(kVerifyBlock)
-k_prep_hash(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
-            const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
-            uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned) {
+__device__ __forceinline__ void prep_hash_block(uint32_t bx, const uint8_t *__restrict__ pk,
+                                                const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
+                                                const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx,
+                                                const uint32_t *count_ptr, uint32_t n, Ed25519Work w,
+                                                const strobe_t *__restrict__ prefix, int aligned) {
   const uint32_t m = entry_count(count_ptr, n);
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t e = bx * blockDim.x + threadIdx.x;
   if (e >= m) return;
   const uint32_t i = idx ? idx[e] : e;
   uint32_t a_w[8], r_w[8];
@@ -136,6 +137,33 @@ k_prep_hash(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, con
   uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
   kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
   kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
+}
+
+template <bool SR>
+__global__ void __launch_bounds__(kVerifyBlock, SR ? 2 : TMV_DECODE_WAVES)
+k_prep_decode(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
+              const uint32_t *count_ptr, uint32_t n, Ed25519Work w, int aligned) {
+  prep_decode_block<SR>(blockIdx.x, pk, sig, idx, count_ptr, n, w, aligned);
+}
+
+template <bool SR>
+__global__ void __launch_bounds__(kVerifyBlock)
+k_prep_hash(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
+            const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+            uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned) {
+  prep_hash_block<SR>(blockIdx.x, pk, sig, msg, msg_off, idx, count_ptr, n, w, prefix, aligned);
+}
+
+// Both halves of the prep in one launch: blocks [0, dblocks) decode, the
+// rest hash, so the hash no longer waits behind the decode's sqrt chains
+// (the two kernels' register budgets are alike, 182 / 192 VGPRs).
+template <bool SR>
+__global__ void __launch_bounds__(kVerifyBlock)
+k_prep_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
+             const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+             uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned, uint32_t dblocks) {
+  if (blockIdx.x < dblocks) prep_decode_block<SR>(blockIdx.x, pk, sig, idx, count_ptr, n, w, aligned);
+  else prep_hash_block<SR>(blockIdx.x - dblocks, pk, sig, msg, msg_off, idx, count_ptr, n, w, prefix, aligned);
 }
 
 constexpr int kQuadSigs = kQuadBlock / 4;
@@ -753,16 +781,33 @@ template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *
                                                const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
                                                hipStream_t, const uint8_t *);
 
+// Decode and hash blocks in one launch (default; TMV_PREP_FUSED=0: two
+// kernels).  Measured in one GPU call (tools/gpu_ab_env.sh): one 10k batch
+// 1.047 -> 0.987 ms through the batch equation, 0.546 -> 0.491 ms per entry;
+// the 32-batch bench unchanged (77.1-77.8 M/s either way).
+static bool prep_fused() {
+  static const bool on = [] {
+    const char *e = getenv("TMV_PREP_FUSED");
+    return !(e && !strcmp(e, "0"));
+  }();
+  return on;
+}
+
 template <bool SR>
 hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                        const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const strobe_t *prefix,
                        Ed25519Work w, int aligned, hipStream_t stream) {
   const uint32_t dblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
+  const uint32_t hblocks = (n + kVerifyBlock - 1) / kVerifyBlock;
+  if (prep_fused()) {
+    hipLaunchKernelGGL(k_prep_fused<SR>, dim3(dblocks + hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off,
+                       idx, count_ptr, n, w, prefix, aligned, dblocks);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_prep_decode<SR>, dim3(dblocks), dim3(kVerifyBlock), 0, stream, pk, sig, idx, count_ptr, n, w,
                      aligned);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint32_t hblocks = (n + kVerifyBlock - 1) / kVerifyBlock;
   hipLaunchKernelGGL(k_prep_hash<SR>, dim3(hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
                      count_ptr, n, w, prefix, aligned);
   return hipGetLastError();
