@@ -94,8 +94,8 @@ __device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &o
 // form): only the m R points are sorted; z_e k_e and the B scalar go to
 // mw.wscal / mw.bscal for k_msm_items, and the key's decode status comes from
 // the key cache.
-template <bool SR, bool KM>
-__global__ void __launch_bounds__(kMsmSortBlock)
+template <bool SR, bool KM, int BS = kMsmSortBlock>
+__global__ void __launch_bounds__(BS)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
            Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned,
            const uint32_t *__restrict__ key_slot, const uint8_t *__restrict__ key_ok) {
@@ -117,10 +117,10 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   const uint32_t mlive = min(p.m(), cnt - e0);
   const uint32_t WH = p.W * p.H;
   uint32_t *hist = smem;                       // WH counters, then cursors
-  uint32_t *red = smem + WH;                   // kMsmSortBlock x 9 words
-  uint32_t *scan = red + kMsmSortBlock * 9;    // kMsmSortBlock + 1
+  uint32_t *red = smem + WH;                   // BS x 9 words
+  uint32_t *scan = red + BS * 9;    // BS + 1
 
-  constexpr int R = 4;  // entries per thread: m <= 4 * kMsmSortBlock
+  constexpr int R = 4;  // entries per thread: m <= 4 * BS
   uint32_t z[R][4], wv[R][8];
   bool live[R];
   uint32_t acc[9];
@@ -133,7 +133,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     for (int t = 0; t < 4; t++) z[r][t] = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) wv[r][t] = 0;
-    const uint32_t j = tid + r * kMsmSortBlock;
+    const uint32_t j = tid + r * BS;
     if (j >= mlive) continue;
     const uint32_t e = e0 + j;
     const uint32_t i = idx ? idx[e] : e;
@@ -187,7 +187,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 #pragma unroll
   for (int t = 0; t < 9; t++) red[tid * 9 + t] = acc[t];
   __syncthreads();
-  for (uint32_t stride = kMsmSortBlock / 2; stride > 0; stride >>= 1) {
+  for (uint32_t stride = BS / 2; stride > 0; stride >>= 1) {
     if (tid < stride) {
       uint64_t c = 0;
       for (int t = 0; t < 9; t++) {
@@ -206,7 +206,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     if (KM)
       for (int t = 0; t < 8; t++) mw.bscal[8ull * g + t] = b[t];
   }
-  for (uint32_t t = tid; t < WH; t += kMsmSortBlock) hist[t] = 0;
+  for (uint32_t t = tid; t < WH; t += BS) hist[t] = 0;
   __syncthreads();
   uint32_t bsc[8];
 #pragma unroll
@@ -223,7 +223,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   __syncthreads();
 
   // exclusive scan: contiguous segments per thread, thread 0 scans the totals
-  const uint32_t seg = (WH + kMsmSortBlock - 1) / kMsmSortBlock;
+  const uint32_t seg = (WH + BS - 1) / BS;
   const uint32_t lo = min(WH, tid * seg), hi = min(WH, lo + seg);
   uint32_t local = 0;
   for (uint32_t t = lo; t < hi; t++) local += hist[t];
@@ -231,12 +231,12 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   __syncthreads();
   if (tid == 0) {
     uint32_t run = 0;
-    for (int t = 0; t < kMsmSortBlock; t++) {
+    for (int t = 0; t < BS; t++) {
       const uint32_t v = scan[t];
       scan[t] = run;
       run += v;
     }
-    scan[kMsmSortBlock] = run;
+    scan[BS] = run;
   }
   __syncthreads();
   const uint32_t gbase = g * p.cap;
@@ -259,7 +259,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (!live[r]) continue;
-    const uint32_t e = e0 + tid + r * kMsmSortBlock;
+    const uint32_t e = e0 + tid + r * BS;
     for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
       ent_pt[pos] = ((KM ? e : 2 * e) << 1) | (neg ? 1u : 0u);
@@ -278,7 +278,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       ent_bk[pos] = bbase + bk;
     });
   }
-  for (uint32_t t = scan[kMsmSortBlock] + tid; t < p.cap; t += kMsmSortBlock) ent_bk[t] = kMsmEmpty;
+  for (uint32_t t = scan[BS] + tid; t < p.cap; t += BS) ent_bk[t] = kMsmEmpty;
 }
 
 // One lane per chunk of L sorted entries: sums each run of equal
@@ -698,6 +698,19 @@ static int subcheck_mode() {
   }();
   return mode;
 }
+// k_msm_sort workgroup size for groups <= 256 entries: 64 by default
+// (TMV_SORT_BLOCK=256: the old 256).  A 64-entry group in a 256-thread
+// workgroup left 3 of 4 waves idle but resident through the sort's LDS
+// phases; C2 bench (3,072 steps, tools/gpu_ab_env.sh): 80.4 / 80.7 ->
+// 84.8 / 84.7 M/s.
+static int sort_block() {
+  static const int bs = [] {
+    const char *e = getenv("TMV_SORT_BLOCK");
+    return (e && !strcmp(e, "256")) ? 256 : 64;
+  }();
+  return bs;
+}
+
 bool subcheck_enabled(uint32_t m_log2) {
   const int mode = subcheck_mode();
   return mode < 0 ? m_log2 >= 8 : mode == 1;
@@ -713,9 +726,17 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   w.niels = mw.pts;
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
-  const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
-  hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx, count_ptr, n,
-                     w, mw, p, seed, btab_q, aligned, nullptr, nullptr);
+  // groups of <= 256 entries: 64-thread workgroups (4 entries per thread at
+  // most), so a 64-entry group no longer parks 192 idle lanes
+  if (p.m_log2 <= 8 && sort_block() == 64) {
+    const size_t smem = ((size_t)p.W * p.H + 64 * 9 + 64 + 1) * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_msm_sort<SR, false, 64>), dim3(p.groups), dim3(64), smem, stream, sig, idx, count_ptr, n,
+                       w, mw, p, seed, btab_q, aligned, nullptr, nullptr);
+  } else {
+    const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx,
+                       count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = launch_buckets(count_ptr, n, mw, p, stream)) != hipSuccess) return e;
   hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
