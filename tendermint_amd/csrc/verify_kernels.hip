@@ -183,14 +183,27 @@ template <bool SR, bool GT>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
-              const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok) {
+              const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok,
+              const uint32_t *__restrict__ fail_list, const uint32_t *__restrict__ fail_count) {
   __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
   const uint32_t m = entry_count(count_ptr, n);
-  if (blockIdx.x * kQuadSigs >= m) return;  // block-uniform
+  // Compacted fallback (fail_list): block b covers the b-th 16-entry block of
+  // the failing groups k_msm_horner listed; every other entry already holds
+  // its pre-check status (written by k_msm_sort).  Otherwise block b covers
+  // entries [16 b, 16 b + 16).
+  uint32_t b0;
+  if (fail_list) {
+    const uint32_t per_log2 = group_log2 - 4;  // 16-entry blocks per group
+    if (blockIdx.x >= (*fail_count << per_log2)) return;  // block-uniform
+    b0 = (fail_list[blockIdx.x >> per_log2] << group_log2) + ((blockIdx.x & ((1u << per_log2) - 1)) << 4);
+  } else {
+    b0 = blockIdx.x * kQuadSigs;
+  }
+  if (b0 >= m) return;  // block-uniform
   const int c = threadIdx.x & 3;
   const int q = threadIdx.x >> 2;
-  const uint32_t raw = blockIdx.x * kQuadSigs + q;
+  const uint32_t raw = b0 + q;
   const bool live = raw < m;
   const uint32_t e = live ? raw : m - 1;
   const uint32_t i = idx ? idx[e] : e;
@@ -201,8 +214,7 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   // passes when every sub-group it covers passed.
   bool pass = false;
   if (group_ok) {
-    const uint32_t b0 = blockIdx.x * kQuadSigs;
-    pass = group_ok[b0 >> group_log2];
+    pass = !fail_list && group_ok[b0 >> group_log2];
     if (!pass && sub_ok) {
       pass = true;
       for (uint32_t s = b0 >> kSubGroupLog2; s <= (b0 + kQuadSigs - 1) >> kSubGroupLog2; s++) pass = pass && sub_ok[s];
@@ -737,13 +749,14 @@ template <bool SR>
 static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig, const uint32_t *idx,
                         const uint32_t *count_ptr, uint32_t n, Ed25519Work w, const fe *btab_q, uint8_t *out,
                         int aligned, const uint8_t *group_ok, uint32_t group_log2,
-                        const uint8_t *sub_ok = nullptr) {
+                        const uint8_t *sub_ok = nullptr, const uint32_t *fail_list = nullptr,
+                        const uint32_t *fail_count = nullptr) {
   if (quad_table_global())
     hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
-                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok);
+                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count);
   else
     hipLaunchKernelGGL((k_verify_quad<SR, false>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
-                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok);
+                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count);
 }
 
 static int is_aligned(const void *a, const void *b) {
@@ -769,17 +782,21 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
 template <bool SR>
 hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                                 const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
-                                uint8_t *out, int aligned, hipStream_t stream, const uint8_t *sub_ok) {
-  const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
-  launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok);
+                                uint8_t *out, int aligned, hipStream_t stream, const uint8_t *sub_ok,
+                                const uint32_t *fail_list, const uint32_t *fail_count) {
+  // compacted: a grid for every group failing (blocks past the failing count exit at once)
+  const uint32_t qblocks = fail_list ? ((((n + (1u << group_log2) - 1) >> group_log2)) << (group_log2 - 4))
+                                     : (n + kQuadSigs - 1) / kQuadSigs;
+  launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok,
+                  fail_list, fail_count);
   return hipGetLastError();
 }
 template hipError_t launch_quad_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
                                                 const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
-                                                hipStream_t, const uint8_t *);
+                                                hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *);
 template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
                                                const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
-                                               hipStream_t, const uint8_t *);
+                                               hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *);
 
 // Decode and hash blocks in one launch (default; TMV_PREP_FUSED=0: two
 // kernels).  Measured in one GPU call (tools/gpu_ab_env.sh): one 10k batch
