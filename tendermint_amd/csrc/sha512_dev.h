@@ -95,6 +95,33 @@ TMV_HD void sha512_pq_msg(uint32_t out[16], const uint32_t P[8], const uint32_t 
         const uint32_t hi = (i + 1) < 8 ? P[i + 1] : Q[i + 1 - 8];
         word = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
       } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // message bytes [off, off + 8) (off is a multiple of 8: P||Q is 64
+        // bytes) from aligned dword loads -- no dword past the one holding
+        // the last message byte is read, so the loads stay inside that
+        // byte's page -- then the 0x80 pad byte and zeros
+        const uint32_t off = (uint32_t)(base - 64);
+        const uint32_t sh = (uint32_t)((uintptr_t)m & 3);
+        const uint32_t *a = reinterpret_cast<const uint32_t *>((uintptr_t)m - sh);
+        const uint32_t d0i = (sh + off) >> 2;
+        const uint32_t last = mlen ? (sh + mlen - 1) >> 2 : 0;
+        const bool any = mlen > off;
+        const uint32_t d0 = any ? a[d0i] : 0u;
+        const uint32_t d1 = (any && d0i + 1 <= last) ? a[d0i + 1] : 0u;
+        const uint32_t d2 = (any && sh && d0i + 2 <= last) ? a[d0i + 2] : 0u;
+        const uint64_t lo64 = ((uint64_t)d1 << 32) | d0, hi64 = ((uint64_t)d2 << 32) | d1;
+        uint32_t b_lo = (uint32_t)(lo64 >> (8 * sh));  // message bytes off .. off+3, little-endian
+        uint32_t b_hi = (uint32_t)(hi64 >> (8 * sh));  // bytes off+4 .. off+7
+        const int v = mlen > off ? (mlen - off >= 8 ? 8 : (int)(mlen - off)) : 0;  // valid bytes here
+        if (v < 8) {
+          const uint64_t keep = v ? ((uint64_t)1 << (8 * v)) - 1 : 0;
+          uint64_t x = (((uint64_t)b_hi << 32) | b_lo) & keep;
+          if (off + v == total - 64) x |= (uint64_t)0x80 << (8 * v);  // pad byte right after the message
+          b_lo = (uint32_t)x;
+          b_hi = (uint32_t)(x >> 32);
+        }
+        word = ((uint64_t)bswap32(b_lo) << 32) | bswap32(b_hi);
+#else
         word = 0;
         for (int b = 0; b < 8; b++) {
           const uint64_t q = base + b;
@@ -111,6 +138,7 @@ TMV_HD void sha512_pq_msg(uint32_t out[16], const uint32_t P[8], const uint32_t 
           }
           word = (word << 8) | byte;
         }
+#endif
         if (blk == nblocks - 1 && t == 15) word = total * 8;  // length (< 2^64 bits)
       }
       w[t] = word;
