@@ -54,44 +54,80 @@ TMV_HD void keccak_f1600_lanes(uint64_t a[25]) {
 
 constexpr int kStrobeR = 166;
 
-// STROBE-128 state as bytes + the three position registers.
+// STROBE-128 state held as the 25 Keccak lanes (state byte p is byte p & 7 of
+// lane p >> 3, little-endian, as Keccak defines it) + the position registers.
+// Absorb/squeeze touch one lane per <= 8 bytes and F runs on the lanes in
+// place: no byte-array pack/unpack around the permutation.
 struct strobe_t {
-  uint8_t st[200];
-  uint8_t pos, pos_begin, cur_flags;
+  uint64_t a[25];
+  uint32_t pos, pos_begin, cur_flags;
 };
 
+TMV_HD void strobe_xor_byte(strobe_t &s, uint32_t p, uint8_t b) { s.a[p >> 3] ^= (uint64_t)b << (8 * (p & 7)); }
+
 TMV_HD void strobe_run_f(strobe_t &s) {
-  s.st[s.pos] ^= s.pos_begin;
-  s.st[s.pos + 1] ^= 0x04;
-  s.st[kStrobeR + 1] ^= 0x80;
-  uint64_t a[25];
-  for (int i = 0; i < 25; i++) {
-    uint64_t v = 0;
-    for (int j = 7; j >= 0; j--) v = (v << 8) | s.st[8 * i + j];
-    a[i] = v;
-  }
-  keccak_f1600_lanes(a);
-  for (int i = 0; i < 25; i++)
-    for (int j = 0; j < 8; j++) s.st[8 * i + j] = (uint8_t)(a[i] >> (8 * j));
+  strobe_xor_byte(s, s.pos, (uint8_t)s.pos_begin);
+  strobe_xor_byte(s, s.pos + 1, 0x04);
+  strobe_xor_byte(s, kStrobeR + 1, 0x80);
+  keccak_f1600_lanes(s.a);
   s.pos = 0;
   s.pos_begin = 0;
 }
 
+// Fresh STROBE-128 instance before any operation: header, version string, F.
+TMV_HD void strobe_init(strobe_t &s) {
+  for (int i = 0; i < 25; i++) s.a[i] = 0;
+  const uint8_t hdr[6] = {1, kStrobeR + 2, 1, 0, 1, 96};
+  for (int i = 0; i < 6; i++) strobe_xor_byte(s, i, hdr[i]);
+  const char *v = "STROBEv1.0.2";
+  for (int i = 0; i < 12; i++) strobe_xor_byte(s, 6 + i, (uint8_t)v[i]);
+  keccak_f1600_lanes(s.a);
+  s.pos = 0; s.pos_begin = 0; s.cur_flags = 0;
+}
+
+// XOR d[0..n) into the rate, a lane-sized chunk at a time.
 TMV_HD void strobe_absorb(strobe_t &s, const uint8_t *d, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++) {
-    s.st[s.pos++] ^= d[i];
+  uint32_t i = 0;
+  while (i < n) {
+    const uint32_t sh = s.pos & 7;
+    uint32_t c = 8 - sh;
+    if (c > kStrobeR - s.pos) c = kStrobeR - s.pos;
+    if (c > n - i) c = n - i;
+    uint64_t v = 0;
+    for (uint32_t j = 0; j < c; j++) v |= (uint64_t)d[i + j] << (8 * j);
+    s.a[s.pos >> 3] ^= v << (8 * sh);
+    s.pos += c;
+    i += c;
     if (s.pos == kStrobeR) strobe_run_f(s);
   }
 }
 TMV_HD void strobe_absorb_byte(strobe_t &s, uint8_t b) {
-  s.st[s.pos++] ^= b;
+  strobe_xor_byte(s, s.pos++, b);
   if (s.pos == kStrobeR) strobe_run_f(s);
+}
+
+// PRF squeeze after begin_op(I|A|C): out = state bytes, which are then zeroed.
+TMV_HD void strobe_prf(strobe_t &s, uint8_t *out, uint32_t n) {
+  uint32_t i = 0;
+  while (i < n) {
+    const uint32_t sh = s.pos & 7;
+    uint32_t c = 8 - sh;
+    if (c > kStrobeR - s.pos) c = kStrobeR - s.pos;
+    if (c > n - i) c = n - i;
+    const uint64_t lane = s.a[s.pos >> 3];
+    for (uint32_t j = 0; j < c; j++) out[i + j] = (uint8_t)(lane >> (8 * (sh + j)));
+    const uint64_t mask = (c == 8) ? ~0ULL : (((1ULL << (8 * c)) - 1) << (8 * sh));
+    s.a[s.pos >> 3] = lane & ~mask;
+    s.pos += c;
+    i += c;
+    if (s.pos == kStrobeR) strobe_run_f(s);
+  }
 }
 
 // begin_op for a fresh (more == false) operation
 TMV_HD void strobe_begin_op(strobe_t &s, uint8_t flags) {
-  const uint8_t old_begin = s.pos_begin;
-  s.pos_begin = (uint8_t)(s.pos + 1);
+  const uint8_t old_begin = (uint8_t)s.pos_begin;
+  s.pos_begin = s.pos + 1;
   s.cur_flags = flags;
   strobe_absorb_byte(s, old_begin);
   strobe_absorb_byte(s, flags);
@@ -122,34 +158,17 @@ TMV_HD void merlin_challenge64(strobe_t &s, const char *label, uint32_t llen, ui
   const uint8_t len[4] = {64, 0, 0, 0};
   strobe_absorb(s, len, 4);
   strobe_begin_op(s, 1 | 2 | 4);  // I | A | C  (prf)
-  for (int i = 0; i < 16; i++) out[i] = 0;
-  for (int i = 0; i < 64; i++) {
-    out[i >> 2] |= (uint32_t)s.st[s.pos] << (8 * (i & 3));
-    s.st[s.pos++] = 0;
-    if (s.pos == kStrobeR) strobe_run_f(s);
-  }
+  uint8_t b[64];
+  strobe_prf(s, b, 64);
+  for (int i = 0; i < 16; i++)
+    out[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+             ((uint32_t)b[4 * i + 3] << 24);
 }
 
 // Transcript state after merlin("SigningContext") + append("", ctx = "")
 // (crypto/sr25519/privkey.go:18): computed once on the host.
 inline void sr25519_context_prefix(strobe_t &s) {
-  for (int i = 0; i < 200; i++) s.st[i] = 0;
-  const uint8_t hdr[6] = {1, kStrobeR + 2, 1, 0, 1, 96};
-  for (int i = 0; i < 6; i++) s.st[i] = hdr[i];
-  const char *v = "STROBEv1.0.2";
-  for (int i = 0; i < 12; i++) s.st[6 + i] = (uint8_t)v[i];
-  s.pos = 0; s.pos_begin = 0; s.cur_flags = 0;
-  {
-    uint64_t a[25];
-    for (int i = 0; i < 25; i++) {
-      uint64_t w = 0;
-      for (int j = 7; j >= 0; j--) w = (w << 8) | s.st[8 * i + j];
-      a[i] = w;
-    }
-    keccak_f1600_lanes(a);
-    for (int i = 0; i < 25; i++)
-      for (int j = 0; j < 8; j++) s.st[8 * i + j] = (uint8_t)(a[i] >> (8 * j));
-  }
+  strobe_init(s);
   // Strobe128::new("Merlin v1.0"): meta_ad(label, false)
   strobe_begin_op(s, 16 | 2);
   strobe_absorb(s, reinterpret_cast<const uint8_t *>("Merlin v1.0"), 11);

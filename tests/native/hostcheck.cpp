@@ -88,18 +88,7 @@ extern "C" void hostcheck_sr25519_status_batch(const uint8_t *pk, const uint8_t 
 extern "C" void hostcheck_merlin_test(uint8_t out[32]) {
   // merlin "test protocol" vector through the same STROBE code
   strobe_t s;
-  for (int i = 0; i < 200; i++) s.st[i] = 0;
-  const uint8_t hdr[6] = {1, kStrobeR + 2, 1, 0, 1, 96};
-  for (int i = 0; i < 6; i++) s.st[i] = hdr[i];
-  const char *v = "STROBEv1.0.2";
-  for (int i = 0; i < 12; i++) s.st[6 + i] = (uint8_t)v[i];
-  s.pos = 0; s.pos_begin = 0; s.cur_flags = 0;
-  {
-    uint64_t a[25];
-    for (int i = 0; i < 25; i++) { uint64_t w = 0; for (int j = 7; j >= 0; j--) w = (w << 8) | s.st[8 * i + j]; a[i] = w; }
-    keccak_f1600_lanes(a);
-    for (int i = 0; i < 25; i++) for (int j = 0; j < 8; j++) s.st[8 * i + j] = (uint8_t)(a[i] >> (8 * j));
-  }
+  strobe_init(s);
   strobe_begin_op(s, 16 | 2);
   strobe_absorb(s, reinterpret_cast<const uint8_t *>("Merlin v1.0"), 11);
   merlin_append(s, "dom-sep", 7, reinterpret_cast<const uint8_t *>("test protocol"), 13);
@@ -109,5 +98,5 @@ extern "C" void hostcheck_merlin_test(uint8_t out[32]) {
   const uint8_t len[4] = {32, 0, 0, 0};
   strobe_absorb(s, len, 4);
   strobe_begin_op(s, 1 | 2 | 4);
-  for (int i = 0; i < 32; i++) { out[i] = s.st[s.pos]; s.st[s.pos++] = 0; }
+  strobe_prf(s, out, 32);
 }
