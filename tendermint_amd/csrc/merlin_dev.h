@@ -61,15 +61,31 @@ constexpr int kStrobeR = 166;
 struct strobe_t {
   uint64_t a[25];
   uint32_t pos, pos_begin, cur_flags;
+  TMV_HD uint64_t &lane(uint32_t i) { return a[i]; }
 };
 
-TMV_HD void strobe_xor_byte(strobe_t &s, uint32_t p, uint8_t b) { s.a[p >> 3] ^= (uint64_t)b << (8 * (p & 7)); }
+// The same state with its lanes in LDS, lane-interleaved (lane i of thread t
+// at base[i * STRIDE + t]: conflict-free, and the dynamically indexed state
+// stays out of scratch).  The kernels' transcript workspace.
+template <int STRIDE>
+struct strobe_lds_t {
+  uint64_t *base;
+  uint32_t pos, pos_begin, cur_flags;
+  TMV_HD uint64_t &lane(uint32_t i) { return base[i * STRIDE]; }
+};
 
-TMV_HD void strobe_run_f(strobe_t &s) {
+template <class S>
+TMV_HD void strobe_xor_byte(S &s, uint32_t p, uint8_t b) { s.lane(p >> 3) ^= (uint64_t)b << (8 * (p & 7)); }
+
+template <class S>
+TMV_HD void strobe_run_f(S &s) {
   strobe_xor_byte(s, s.pos, (uint8_t)s.pos_begin);
   strobe_xor_byte(s, s.pos + 1, 0x04);
   strobe_xor_byte(s, kStrobeR + 1, 0x80);
-  keccak_f1600_lanes(s.a);
+  uint64_t a[25];  // F on registers
+  for (int i = 0; i < 25; i++) a[i] = s.lane(i);
+  keccak_f1600_lanes(a);
+  for (int i = 0; i < 25; i++) s.lane(i) = a[i];
   s.pos = 0;
   s.pos_begin = 0;
 }
@@ -86,7 +102,8 @@ TMV_HD void strobe_init(strobe_t &s) {
 }
 
 // XOR d[0..n) into the rate, a lane-sized chunk at a time.
-TMV_HD void strobe_absorb(strobe_t &s, const uint8_t *d, uint32_t n) {
+template <class S>
+TMV_HD void strobe_absorb(S &s, const uint8_t *d, uint32_t n) {
   uint32_t i = 0;
   while (i < n) {
     const uint32_t sh = s.pos & 7;
@@ -95,29 +112,31 @@ TMV_HD void strobe_absorb(strobe_t &s, const uint8_t *d, uint32_t n) {
     if (c > n - i) c = n - i;
     uint64_t v = 0;
     for (uint32_t j = 0; j < c; j++) v |= (uint64_t)d[i + j] << (8 * j);
-    s.a[s.pos >> 3] ^= v << (8 * sh);
+    s.lane(s.pos >> 3) ^= v << (8 * sh);
     s.pos += c;
     i += c;
     if (s.pos == kStrobeR) strobe_run_f(s);
   }
 }
-TMV_HD void strobe_absorb_byte(strobe_t &s, uint8_t b) {
+template <class S>
+TMV_HD void strobe_absorb_byte(S &s, uint8_t b) {
   strobe_xor_byte(s, s.pos++, b);
   if (s.pos == kStrobeR) strobe_run_f(s);
 }
 
 // PRF squeeze after begin_op(I|A|C): out = state bytes, which are then zeroed.
-TMV_HD void strobe_prf(strobe_t &s, uint8_t *out, uint32_t n) {
+template <class S>
+TMV_HD void strobe_prf(S &s, uint8_t *out, uint32_t n) {
   uint32_t i = 0;
   while (i < n) {
     const uint32_t sh = s.pos & 7;
     uint32_t c = 8 - sh;
     if (c > kStrobeR - s.pos) c = kStrobeR - s.pos;
     if (c > n - i) c = n - i;
-    const uint64_t lane = s.a[s.pos >> 3];
+    const uint64_t lane = s.lane(s.pos >> 3);
     for (uint32_t j = 0; j < c; j++) out[i + j] = (uint8_t)(lane >> (8 * (sh + j)));
     const uint64_t mask = (c == 8) ? ~0ULL : (((1ULL << (8 * c)) - 1) << (8 * sh));
-    s.a[s.pos >> 3] = lane & ~mask;
+    s.lane(s.pos >> 3) = lane & ~mask;
     s.pos += c;
     i += c;
     if (s.pos == kStrobeR) strobe_run_f(s);
@@ -125,7 +144,8 @@ TMV_HD void strobe_prf(strobe_t &s, uint8_t *out, uint32_t n) {
 }
 
 // begin_op for a fresh (more == false) operation
-TMV_HD void strobe_begin_op(strobe_t &s, uint8_t flags) {
+template <class S>
+TMV_HD void strobe_begin_op(S &s, uint8_t flags) {
   const uint8_t old_begin = (uint8_t)s.pos_begin;
   s.pos_begin = s.pos + 1;
   s.cur_flags = flags;
@@ -135,7 +155,8 @@ TMV_HD void strobe_begin_op(strobe_t &s, uint8_t flags) {
 }
 
 // merlin append_message(label, message): meta_ad(label); meta_ad(le32(len), more); ad(message)
-TMV_HD void merlin_append(strobe_t &s, const char *label, uint32_t llen, const uint8_t *m, uint32_t n) {
+template <class S>
+TMV_HD void merlin_append(S &s, const char *label, uint32_t llen, const uint8_t *m, uint32_t n) {
   strobe_begin_op(s, 16 | 2);  // M | A
   strobe_absorb(s, reinterpret_cast<const uint8_t *>(label), llen);
   const uint8_t len[4] = {(uint8_t)n, (uint8_t)(n >> 8), (uint8_t)(n >> 16), (uint8_t)(n >> 24)};
@@ -145,14 +166,16 @@ TMV_HD void merlin_append(strobe_t &s, const char *label, uint32_t llen, const u
 }
 
 // merlin append with the message given as 8 little-endian words (32 bytes)
-TMV_HD void merlin_append_words(strobe_t &s, const char *label, uint32_t llen, const uint32_t w[8]) {
+template <class S>
+TMV_HD void merlin_append_words(S &s, const char *label, uint32_t llen, const uint32_t w[8]) {
   uint8_t b[32];
   for (int i = 0; i < 32; i++) b[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
   merlin_append(s, label, llen, b, 32);
 }
 
 // challenge_bytes(label, 64) -> out (64 bytes as 16 LE words)
-TMV_HD void merlin_challenge64(strobe_t &s, const char *label, uint32_t llen, uint32_t out[16]) {
+template <class S>
+TMV_HD void merlin_challenge64(S &s, const char *label, uint32_t llen, uint32_t out[16]) {
   strobe_begin_op(s, 16 | 2);
   strobe_absorb(s, reinterpret_cast<const uint8_t *>(label), llen);
   const uint8_t len[4] = {64, 0, 0, 0};
@@ -178,10 +201,10 @@ inline void sr25519_context_prefix(strobe_t &s) {
   merlin_append(s, "", 0, reinterpret_cast<const uint8_t *>(""), 0);
 }
 
-// k = challenge mod l for (pk, R, M) starting from the context prefix.
-TMV_HD void sr25519_challenge(uint32_t k[8], const strobe_t &prefix, const uint32_t pk_w[8],
-                              const uint32_t r_w[8], const uint8_t *m, uint32_t mlen) {
-  strobe_t s = prefix;
+// k = challenge mod l for (pk, R, M), s holding the context prefix on entry.
+template <class S>
+TMV_HD void sr25519_challenge_from(uint32_t k[8], S &s, const uint32_t pk_w[8], const uint32_t r_w[8],
+                                   const uint8_t *m, uint32_t mlen) {
   merlin_append(s, "sign-bytes", 10, m, mlen);
   merlin_append(s, "proto-name", 10, reinterpret_cast<const uint8_t *>("Schnorr-sig"), 11);
   merlin_append_words(s, "sign:pk", 7, pk_w);
@@ -189,6 +212,24 @@ TMV_HD void sr25519_challenge(uint32_t k[8], const strobe_t &prefix, const uint3
   uint32_t wide[16];
   merlin_challenge64(s, "sign:c", 6, wide);
   sc_reduce512(k, wide);
+}
+
+TMV_HD void sr25519_challenge(uint32_t k[8], const strobe_t &prefix, const uint32_t pk_w[8],
+                              const uint32_t r_w[8], const uint8_t *m, uint32_t mlen) {
+  strobe_t s = prefix;
+  sr25519_challenge_from(k, s, pk_w, r_w, m, mlen);
+}
+
+// Same, with the transcript state in the caller's LDS slot (base = &lds[0][t]
+// of a uint64_t [25][STRIDE] array).
+template <int STRIDE>
+TMV_HD void sr25519_challenge_lds(uint32_t k[8], const strobe_t &prefix, uint64_t *base, const uint32_t pk_w[8],
+                                      const uint32_t r_w[8], const uint8_t *m, uint32_t mlen) {
+  strobe_lds_t<STRIDE> s;
+  s.base = base;
+  for (int i = 0; i < 25; i++) s.lane(i) = prefix.a[i];
+  s.pos = prefix.pos; s.pos_begin = prefix.pos_begin; s.cur_flags = prefix.cur_flags;
+  sr25519_challenge_from(k, s, pk_w, r_w, m, mlen);
 }
 
 // Signature.UnmarshalBinary checks: schnorrkel marker bit, canonical s.
