@@ -419,8 +419,9 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
     else load_words_unaligned(a_w, pk + 32ull * i);
     uint32_t k[8];
     const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
-    if (SR) {
-      sr25519_challenge(k, *prefix, a_w, r_w, msg + o0, o1 - o0);
+    if constexpr (SR) {
+      __shared__ uint64_t strobe_lanes[25][kVerifyBlock];
+      sr25519_challenge_lds<kVerifyBlock>(k, *prefix, &strobe_lanes[0][threadIdx.x], a_w, r_w, msg + o0, o1 - o0);
     } else {
       uint32_t h[16];
       sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
