@@ -604,8 +604,9 @@ k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict_
       load_words_unaligned(r_w, sig + 64ull * i);
     }
     const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
-    if (SR) {
-      sr25519_challenge(k_w, *prefix, a_w, r_w, msg + o0, o1 - o0);
+    if constexpr (SR) {  // transcript state in LDS, one slot per quad
+      __shared__ uint64_t strobe_lanes[25][kQuadSigs];
+      sr25519_challenge_lds<kQuadSigs>(k_w, *prefix, &strobe_lanes[0][q], a_w, r_w, msg + o0, o1 - o0);
     } else {
       uint32_t h[16];
       sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
