@@ -10,6 +10,9 @@
  *   tmv_vote_sign_bytes types.VoteSignBytes (types/vote.go:149-157)
  *   tmv_verify_commit  types.VerifyCommit / VerifyCommitLight /
  *                      VerifyCommitLightTrusting (types/validation.go:27,61,96)
+ *   tmv_light_verify   light.Verify / VerifyAdjacent / VerifyNonAdjacent
+ *                      (light/verifier.go:33-177)
+ *   tmv_header_hashes  types.Header.Hash (types/block.go:447-478)
  */
 #ifndef TMHOST_H
 #define TMHOST_H
@@ -131,6 +134,80 @@ typedef struct {
 
 int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                        size_t err_stride);
+
+/* ---- light client (light/verifier.go) ---- */
+typedef struct {
+  const uint8_t *p;
+  uint32_t len;
+} tmv_bytes;
+
+/* types.Header (types/block.go:338-366); chain_id NUL-terminated. */
+typedef struct {
+  uint64_t version_block, version_app;
+  const char *chain_id;
+  int64_t height;
+  int64_t time_seconds;
+  int32_t time_nanos;
+  tmv_block_id last_block_id;
+  tmv_bytes last_commit_hash, data_hash, validators_hash, next_validators_hash, consensus_hash, app_hash,
+      last_results_hash, evidence_hash, proposer_address;
+} tmv_header;
+
+/* types.SignedHeader (types/light.go:131-136); NULL members = nil. */
+typedef struct {
+  const tmv_header *header;
+  const tmv_commit *commit;
+} tmv_signed_header;
+
+/* types.ValidatorSet (proposer_index < 0: derived from the priorities). */
+typedef struct {
+  const tmv_validator *vals;
+  uint32_t n_vals;
+  int32_t proposer_index;
+} tmv_validator_set;
+
+/* Header.Hash (types/block.go:447-478) of n headers; has_hash[i] = 0 when the
+ * reference returns nil (empty ValidatorsHash), else hash_out + 32*i holds it.
+ * Many headers go to the device in one tmv_merkle_roots launch.  0 or < 0. */
+int tmv_header_hashes(tmv_ctx *ctx, const tmv_header *headers, uint32_t n, uint8_t *hash_out, uint8_t *has_hash);
+
+#define TMV_LIGHT_VERIFY 0       /* light.Verify (light/verifier.go:158-177) */
+#define TMV_LIGHT_ADJACENT 1     /* light.VerifyAdjacent (light/verifier.go:106-155) */
+#define TMV_LIGHT_NON_ADJACENT 2 /* light.VerifyNonAdjacent (light/verifier.go:33-91) */
+
+/* Result classes (light/errors.go:15-40): the reference's error types. */
+#define TMV_LIGHT_OK 0
+#define TMV_LIGHT_ERR_INVALID_HEADER 1     /* light.ErrInvalidHeader */
+#define TMV_LIGHT_ERR_OLD_HEADER_EXPIRED 2 /* light.ErrOldHeaderExpired */
+#define TMV_LIGHT_ERR_CANT_TRUST 3         /* light.ErrNewValSetCantBeTrusted */
+#define TMV_LIGHT_ERR_OTHER 4              /* a plain error (errors.New / fmt.Errorf) */
+
+/* One light-client verification: the arguments of light.Verify /
+ * VerifyAdjacent / VerifyNonAdjacent.  trusted_vals = the trusted header's
+ * next validators (unused by VerifyAdjacent); times are UTC; trust level
+ * = trust_num / trust_den (tmmath.Fraction). */
+typedef struct {
+  int mode; /* TMV_LIGHT_VERIFY / _ADJACENT / _NON_ADJACENT */
+  const tmv_signed_header *trusted;
+  const tmv_validator_set *trusted_vals;
+  const tmv_signed_header *untrusted;
+  const tmv_validator_set *untrusted_vals;
+  int64_t trusting_period_ns;
+  int64_t now_seconds;
+  int32_t now_nanos;
+  int64_t max_clock_drift_ns;
+  uint64_t trust_num, trust_den;
+} tmv_light_job;
+
+/* Many light verifications in one pass: header and validator-set hashes of
+ * all jobs in one device launch each, every commit check of all jobs in one
+ * signature batch (tmv_verify_commits).  results[j] = TMV_LIGHT_* class,
+ * error text at errs + j*err_stride, each identical to a tmv_light_verify
+ * of job j alone.  Returns the number of failed jobs or < 0 (infrastructure). */
+int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                          size_t err_stride);
+/* One job: returns its TMV_LIGHT_* class (text in err) or < 0. */
+int tmv_light_verify(tmv_ctx *ctx, const tmv_light_job *job, char *err, size_t err_cap);
 
 #ifdef __cplusplus
 }

@@ -137,6 +137,18 @@ int tmv_batch_stats(tmv_ctx *ctx, uint64_t *groups, uint64_t *groups_failed);
  * Synchronous; 0 or < 0 on error. */
 int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key_kind, const int64_t *power,
                              const uint32_t *set_off, uint32_t n_sets, uint8_t *hash_out);
+/* merkle.HashFromByteSlices of n_trees trees in one launch (crypto/merkle/
+ * tree.go:11-27: RFC 6962 leaves SHA-256(0x00 || leaf), inner nodes
+ * SHA-256(0x01 || l || r), split at the largest power of two below n).  The
+ * host layer uses it for Header.Hash (types/block.go:447-478: 14 proto-encoded
+ * fields per header) across a light client's window of headers.
+ * Leaf i = data[leaf_off[i], leaf_off[i+1]) (n_leaves + 1 offsets,
+ * leaf_off[0] = 0); tree t = leaves [tree_off[t], tree_off[t+1]) (n_trees + 1
+ * offsets, tree_off[0] = 0, tree_off[n_trees] = n_leaves; an empty tree
+ * hashes to SHA-256("")).  hash_out: n_trees x 32 bytes.  Synchronous; 0 or
+ * < 0 on error. */
+int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off, uint32_t n_leaves,
+                     const uint32_t *tree_off, uint32_t n_trees, uint8_t *hash_out);
 /* Sub-groups of failing groups checked / failed (k_msm_subcheck: a failing
  * group's sub-groups of 8 entries are re-checked with the same equation
  * before entry-by-entry verification; TMV_BATCHOPT_STATS; 0 with

@@ -593,8 +593,10 @@ def _check_required(sh: SignedHeader) -> Optional[str]:
 
 
 def validate_trust_level(num: int, den: int) -> Optional[str]:
-    if num * 3 < den or num >= den or den == 0:
-        return "trustLevel must be within [1/3, 1], given {%d %d}" % (num, den)
+    """light/verifier.go:183-191 (uint64 arithmetic; %v of a Fraction is its
+    String(), libs/math/fraction.go:20-22)."""
+    if (num * 3) % (1 << 64) < den or num >= den or den == 0:
+        return "trustLevel must be within [1/3, 1], given %d/%d" % (num, den)
     return None
 
 

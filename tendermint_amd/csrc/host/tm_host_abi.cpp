@@ -18,9 +18,10 @@
 #include "../../../include/tmhost.h"
 #include "../../../include/tmverify.h"
 #include "pool.h"
+#include "tm_host_internal.h"
 #include "tm_types.h"
 
-namespace {
+namespace tmh_internal {
 
 void put_err(char *err, size_t cap, const std::string &s) {
   if (!err || cap == 0) return;
@@ -28,6 +29,12 @@ void put_err(char *err, size_t cap, const std::string &s) {
   std::memcpy(err, s.data(), n);
   err[n] = 0;
 }
+
+}  // namespace tmh_internal
+
+using namespace tmh_internal;
+
+namespace {
 
 // Packed entries + GPU verify.
 class GpuBatch : public tmh::BatchVerifier {
@@ -99,6 +106,10 @@ class GpuBatch : public tmh::BatchVerifier {
   int infra_error_ = 0;
 };
 
+}  // namespace
+
+namespace tmh_internal {
+
 tmh::KeyType to_kind(uint8_t k) {
   return k == TMV_KIND_ED25519 ? tmh::KeyType::Ed25519 : k == TMV_KIND_SR25519 ? tmh::KeyType::Sr25519
                                                                              : tmh::KeyType::Other;
@@ -114,7 +125,7 @@ tmh::BlockID block_id_of(const tmv_block_id &b) {
   return r;
 }
 
-}  // namespace
+}  // namespace tmh_internal
 
 struct tmv_batch {
   std::unique_ptr<GpuBatch> impl;
@@ -193,12 +204,6 @@ size_t tmv_vote_template_encode(const char *chain_id, int32_t vote_type, int64_t
 }  // extern "C"
 
 namespace {
-
-// Run fn(i) for i in [0, n) on the host worker pool (serial when small).
-template <class F>
-void parallel_for(size_t n, size_t min_per_thread, F fn) {
-  tmh::parallel_for_n(n, n / std::max<size_t>(1, min_per_thread), fn);
-}
 
 // Phase timing of tmv_verify_commits, printed to stderr when the
 // environment variable TMV_HOST_TIMING is set (profiling aid).
@@ -380,6 +385,10 @@ struct GpuBackend {
   }
 };
 
+}  // namespace
+
+namespace tmh_internal {
+
 std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index) {
   if (!vals) return nullptr;
   auto vs = std::make_unique<tmh::ValidatorSet>();
@@ -414,12 +423,8 @@ std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit) {
   return cm;
 }
 
-}  // namespace
-
-extern "C" {
-
-int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
-                       size_t err_stride) {
+int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                   size_t err_stride, uint8_t *not_enough) {
   if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
   for (uint32_t j = 0; j < n_jobs; j++)
     if (jobs[j].mode < 0 || jobs[j].mode > 2) return TMV_ERR_ARG;
@@ -555,13 +560,24 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
   for (uint32_t j = 0; j < n_jobs; j++) {
     buf.resize(joff[j + 1] - joff[j]);
     for (size_t e = 0; e < buf.size(); e++) buf[e] = st[where[joff[j] + e]];
-    tmh::Error e = tmh::CommitVerifier::Finish(plans[j], buf.data());
+    bool ne = false;
+    tmh::Error e = tmh::CommitVerifier::Finish(plans[j], buf.data(), &ne);
     if (results) results[j] = e ? 1 : 0;
+    if (not_enough) not_enough[j] = ne ? 1 : 0;
     if (errs && err_stride) put_err(errs + (size_t)j * err_stride, err_stride, e ? *e : std::string());
     bad += e ? 1 : 0;
   }
   tm.mark("finish");
   return bad;
+}
+
+}  // namespace tmh_internal
+
+extern "C" {
+
+int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                       size_t err_stride) {
+  return verify_commits(ctx, jobs, n_jobs, results, errs, err_stride, nullptr);
 }
 
 int tmv_verify_commit(tmv_ctx *ctx, int mode, const char *chain_id, const tmv_validator *vals, uint32_t n_vals,

@@ -1,0 +1,34 @@
+// Helpers shared by the host layer's C-ABI translation units
+// (tm_host_abi.cpp: batch verifier and commit checks; tm_light_abi.cpp:
+// light-client verification).  Not part of the public C-ABI.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+#include "../../../include/tmhost.h"
+#include "pool.h"
+#include "tm_types.h"
+
+namespace tmh_internal {
+
+void put_err(char *err, size_t cap, const std::string &s);
+tmh::KeyType to_kind(uint8_t k);
+tmh::Bytes bytes_of(const uint8_t *p, size_t n);
+tmh::BlockID block_id_of(const tmv_block_id &b);
+std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index);
+std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit);
+
+// tmv_verify_commits, plus not_enough[j] = 1 when job j's error is
+// types.ErrNotEnoughVotingPowerSigned (may be NULL).
+int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                   size_t err_stride, uint8_t *not_enough);
+
+// Run fn(i) for i in [0, n) on the host worker pool (serial when small).
+template <class F>
+void parallel_for(size_t n, size_t min_per_thread, F fn) {
+  tmh::parallel_for_n(n, n / std::max<size_t>(1, min_per_thread), fn);
+}
+
+}  // namespace tmh_internal

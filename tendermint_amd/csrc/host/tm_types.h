@@ -585,8 +585,11 @@ struct CommitVerifier {
     }
   }
 
-  // Signature results -> the reference's return value.
-  static Error Finish(const CommitPlan &pl, const int8_t *st) {
+  // Signature results -> the reference's return value.  *not_enough is set
+  // when the error is types.ErrNotEnoughVotingPowerSigned (the light client
+  // maps that type to ErrNewValSetCantBeTrusted, light/verifier.go:72-75).
+  static Error Finish(const CommitPlan &pl, const int8_t *st, bool *not_enough = nullptr) {
+    if (not_enough) *not_enough = false;
     if (pl.early) return pl.early;
     const Commit &commit = *pl.commit;
     if (pl.batch) {
@@ -598,7 +601,10 @@ struct CommitVerifier {
             return pl.deferred_sig[i].empty() ? std::string("sr25519: unable to decode signature") : pl.deferred_sig[i];
         }
       }
-      if (pl.tallied <= pl.needed) return ErrNotEnoughVotingPowerSigned(pl.tallied, pl.needed);
+      if (pl.tallied <= pl.needed) {
+        if (not_enough) *not_enough = true;
+        return ErrNotEnoughVotingPowerSigned(pl.tallied, pl.needed);
+      }
       for (size_t i = 0; i < pl.entries.size(); i++) {
         if (st[i] != 1) {
           const int idx = pl.sig_idx[i];
@@ -615,7 +621,10 @@ struct CommitVerifier {
       }
       if (pl.crosses[i]) return std::nullopt;
     }
-    if (pl.tallied <= pl.needed) return ErrNotEnoughVotingPowerSigned(pl.tallied, pl.needed);
+    if (pl.tallied <= pl.needed) {
+      if (not_enough) *not_enough = true;
+      return ErrNotEnoughVotingPowerSigned(pl.tallied, pl.needed);
+    }
     return std::nullopt;
   }
 

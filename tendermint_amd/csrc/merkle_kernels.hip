@@ -10,7 +10,11 @@
 //   k_valset_leaves  one lane per validator: encode SimpleValidator into a
 //                    single SHA-256 block (<= 48 bytes with the prefix) and
 //                    hash it
-//   k_valset_tree    one workgroup per set: the levels of the tree, pairing
+//   k_merkle_leaves  one lane per leaf of arbitrary length (tmv_merkle_roots:
+//                    the 14 proto-encoded fields of Header.Hash,
+//                    types/block.go:447-478, or any HashFromByteSlices input):
+//                    SHA-256(0x00 || leaf) over as many blocks as it needs
+//   k_merkle_tree    one workgroup per set: the levels of the tree, pairing
 //                    (0,1), (2,3), ... and promoting an odd last node --
 //                    the same tree as the reference's split at the largest
 //                    power of two below n (tree.go:68-99, its iterative form,
@@ -23,7 +27,6 @@
 
 namespace tmv {
 
-constexpr int kTreeBlock = 256;
 
 __global__ void __launch_bounds__(256)
 k_valset_leaves(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ kind, const int64_t *__restrict__ power,
@@ -98,8 +101,48 @@ __device__ __forceinline__ void store_node(uint32_t *p, const uint32_t h[8]) {
   q[1] = make_uint4(h[4], h[5], h[6], h[7]);
 }
 
+// RFC 6962 leaf of an arbitrary byte string, one lane per leaf: the padded
+// message 0x00 || leaf || 0x80 || 0* || bitlen(64) is assembled a block at a
+// time from global memory (leaves are short: header fields, <= 2 blocks).
+__global__ void __launch_bounds__(256)
+k_merkle_leaves(const uint8_t *__restrict__ data, const uint32_t *__restrict__ leaf_off, uint32_t n_leaves,
+                uint32_t *__restrict__ node) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_leaves) return;
+  const uint32_t base = leaf_off[i];
+  const uint32_t total = leaf_off[i + 1] - base + 1;  // with the 0x00 prefix
+  const uint32_t nblk = (total + 72) / 64;            // room for 0x80 and the 8-byte length
+  const uint32_t end = 64 * nblk;
+  const uint64_t bits = (uint64_t)total * 8;
+  uint32_t st[8];
+  sha256_init(st);
+  for (uint32_t k = 0; k < nblk; k++) {
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t pos = 64 * k + 4 * q + j;
+        uint32_t byte = 0;
+        if (pos == 0) byte = 0x00;
+        else if (pos < total) byte = data[base + pos - 1];
+        else if (pos == total) byte = 0x80;
+        else if (pos >= end - 8) byte = (uint32_t)(bits >> (8 * (end - 1 - pos))) & 0xffu;
+        word = (word << 8) | byte;
+      }
+      w[q] = word;
+    }
+    sha256_compress(st, w);
+  }
+  uint4 *o = reinterpret_cast<uint4 *>(node + 8ull * i);
+  o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+  o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+}
+
+template <int kTreeBlock>
 __global__ void __launch_bounds__(kTreeBlock)
-k_valset_tree(const uint32_t *__restrict__ set_off, uint32_t n_sets, uint32_t *node_a, uint32_t *node_b,
+k_merkle_tree(const uint32_t *__restrict__ set_off, uint32_t n_sets, uint32_t *node_a, uint32_t *node_b,
               uint8_t *__restrict__ out) {
   const uint32_t s = blockIdx.x;
   if (s >= n_sets) return;
@@ -156,8 +199,27 @@ hipError_t launch_valset_hashes(const uint8_t *pk, const uint8_t *kind, const in
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (n_sets) hipLaunchKernelGGL(k_valset_tree, dim3(n_sets), dim3(kTreeBlock), 0, stream, set_off, n_sets, node_a,
+  if (n_sets) hipLaunchKernelGGL(k_merkle_tree<256>, dim3(n_sets), dim3(256), 0, stream, set_off, n_sets, node_a,
                                  node_b, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_roots(const uint8_t *data, const uint32_t *leaf_off, uint32_t n_leaves,
+                               const uint32_t *tree_off, uint32_t n_trees, uint32_t max_leaves, uint32_t *node_a,
+                               uint32_t *node_b, uint8_t *out, hipStream_t stream) {
+  if (n_leaves) {
+    hipLaunchKernelGGL(k_merkle_leaves, dim3((n_leaves + 255) / 256), dim3(256), 0, stream, data, leaf_off, n_leaves,
+                       node_a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (!n_trees) return hipGetLastError();
+  // small trees (Header.Hash: 14 leaves) take one wave per tree
+  if (max_leaves <= 128)
+    hipLaunchKernelGGL(k_merkle_tree<64>, dim3(n_trees), dim3(64), 0, stream, tree_off, n_trees, node_a, node_b, out);
+  else
+    hipLaunchKernelGGL(k_merkle_tree<256>, dim3(n_trees), dim3(256), 0, stream, tree_off, n_trees, node_a, node_b,
+                       out);
   return hipGetLastError();
 }
 

@@ -1449,6 +1449,60 @@ int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key
   return 0;
 }
 
+int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off, uint32_t n_leaves,
+                     const uint32_t *tree_off, uint32_t n_trees, uint8_t *hash_out) {
+  if (!ctx || ctx->devs.empty()) { set_error("null context"); return TMV_ERR_ARG; }
+  if (n_trees == 0) return 0;
+  if (!leaf_off || !tree_off || !hash_out) { set_error("tmv_merkle_roots: null pointer"); return TMV_ERR_ARG; }
+  if (leaf_off[0] != 0 || tree_off[0] != 0 || tree_off[n_trees] != n_leaves) {
+    set_error("tmv_merkle_roots: offsets must start at 0 and tree_off must end at n_leaves");
+    return TMV_ERR_ARG;
+  }
+  uint32_t max_leaves = 0;
+  for (uint32_t t = 0; t < n_trees; t++) {
+    if (tree_off[t + 1] < tree_off[t]) { set_error("tmv_merkle_roots: tree_off decreasing"); return TMV_ERR_ARG; }
+    max_leaves = std::max(max_leaves, tree_off[t + 1] - tree_off[t]);
+  }
+  for (uint32_t i = 0; i < n_leaves; i++)
+    if (leaf_off[i + 1] < leaf_off[i]) { set_error("tmv_merkle_roots: leaf_off decreasing"); return TMV_ERR_ARG; }
+  const uint32_t bytes = leaf_off[n_leaves];
+  if (bytes && !data) { set_error("tmv_merkle_roots: null data"); return TMV_ERR_ARG; }
+  if (n_leaves > (1u << 26) || bytes > (1u << 30)) { set_error("tmv_merkle_roots: input too large"); return TMV_ERR_ARG; }
+  Device &d = *ctx->devs[0];
+  std::lock_guard<std::mutex> lk(d.mu);
+  hipError_t e = hipSetDevice(d.id);
+  if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
+  // staging: leaf_off | tree_off | data, then (device only) two node arrays and the roots
+  const size_t o_tree = align16(4ull * (n_leaves + 1)), o_data = o_tree + align16(4ull * (n_trees + 1));
+  const size_t in_bytes = o_data + align16(bytes);
+  const size_t o_na = in_bytes, o_nb = o_na + 32ull * n_leaves, o_out = o_nb + 32ull * n_leaves;
+  const size_t dev_bytes = o_out + 32ull * n_trees;
+  hipStream_t s = d.stream;
+  (void)hipStreamSynchronize(s);  // the staging buffers are shared with tmv_validator_set_hashes
+  if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+  if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  uint8_t *h = static_cast<uint8_t *>(d.h_valset.ptr);
+  std::memcpy(h, leaf_off, 4ull * (n_leaves + 1));
+  std::memcpy(h + o_tree, tree_off, 4ull * (n_trees + 1));
+  if (bytes) std::memcpy(h + o_data, data, bytes);
+  uint8_t *g = static_cast<uint8_t *>(d.d_valset.ptr);
+  if ((e = hipMemcpyAsync(g, h, in_bytes, hipMemcpyHostToDevice, s)) != hipSuccess) {
+    set_error("hipMemcpyAsync(merkle)", e);
+    return TMV_ERR_LAUNCH;
+  }
+  e = tmv::launch_merkle_roots(g + o_data, reinterpret_cast<const uint32_t *>(g), n_leaves,
+                               reinterpret_cast<const uint32_t *>(g + o_tree), n_trees, max_leaves,
+                               reinterpret_cast<uint32_t *>(g + o_na), reinterpret_cast<uint32_t *>(g + o_nb),
+                               g + o_out, s);
+  if (e != hipSuccess) { set_error("merkle launch", e); return TMV_ERR_LAUNCH; }
+  if ((e = hipMemcpyAsync(hash_out, g + o_out, 32ull * n_trees, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipStreamSynchronize(s)) != hipSuccess) {
+    set_error("merkle readback", e);
+    return TMV_ERR_LAUNCH;
+  }
+  return 0;
+}
+
 }  // extern "C"
 
 extern "C" {

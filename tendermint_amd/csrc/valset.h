@@ -15,4 +15,12 @@ hipError_t launch_valset_hashes(const uint8_t *pk, const uint8_t *kind, const in
                                 const uint32_t *set_off, uint32_t n_sets, uint32_t *node_a, uint32_t *node_b,
                                 uint8_t *out, hipStream_t stream);
 
+// merkle.HashFromByteSlices of n_trees trees (tmv_merkle_roots): leaf i is
+// data[leaf_off[i], leaf_off[i+1]); tree t holds leaves [tree_off[t],
+// tree_off[t+1]) and has at most max_leaves of them.  node_a / node_b:
+// n_leaves x 8 words each; out: n_trees x 32 B.
+hipError_t launch_merkle_roots(const uint8_t *data, const uint32_t *leaf_off, uint32_t n_leaves,
+                               const uint32_t *tree_off, uint32_t n_trees, uint32_t max_leaves, uint32_t *node_a,
+                               uint32_t *node_b, uint8_t *out, hipStream_t stream);
+
 }  // namespace tmv

@@ -437,3 +437,223 @@ def verify_commits(ctx, jobs: List[CommitJob]) -> List[Optional[str]]:
     pj = PreparedJobs(jobs)
     run_prepared_jobs(ctx, pj)
     return pj.decode()
+
+
+# ---------------------------------------------------------------- light client
+# light.Verify / VerifyAdjacent / VerifyNonAdjacent (light/verifier.go:33-177)
+# and Header.Hash (types/block.go:447-478) through tmv_light_verify_many /
+# tmv_header_hashes (include/tmhost.h).
+
+LIGHT_VERIFY, LIGHT_ADJACENT, LIGHT_NON_ADJACENT = 0, 1, 2
+LIGHT_OK, LIGHT_ERR_INVALID_HEADER, LIGHT_ERR_OLD_HEADER_EXPIRED, LIGHT_ERR_CANT_TRUST, LIGHT_ERR_OTHER = 0, 1, 2, 3, 4
+BLOCK_PROTOCOL = 11  # version/version.go:27
+
+
+class CBytes(ctypes.Structure):
+    _fields_ = [("p", _u8p), ("len", ctypes.c_uint32)]
+
+
+_HASH_FIELDS = ("last_commit_hash", "data_hash", "validators_hash", "next_validators_hash", "consensus_hash",
+                "app_hash", "last_results_hash", "evidence_hash", "proposer_address")
+
+
+class CHeader(ctypes.Structure):
+    _fields_ = ([("version_block", ctypes.c_uint64), ("version_app", ctypes.c_uint64), ("chain_id", ctypes.c_char_p),
+                 ("height", ctypes.c_int64), ("time_seconds", ctypes.c_int64), ("time_nanos", ctypes.c_int32),
+                 ("last_block_id", CBlockID)] + [(f, CBytes) for f in _HASH_FIELDS])
+
+
+class CSignedHeader(ctypes.Structure):
+    _fields_ = [("header", ctypes.POINTER(CHeader)), ("commit", ctypes.POINTER(CCommit))]
+
+
+class CValidatorSet(ctypes.Structure):
+    _fields_ = [("vals", ctypes.POINTER(CValidator)), ("n_vals", ctypes.c_uint32), ("proposer_index", ctypes.c_int32)]
+
+
+class CLightJob(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("trusted", ctypes.POINTER(CSignedHeader)),
+                ("trusted_vals", ctypes.POINTER(CValidatorSet)), ("untrusted", ctypes.POINTER(CSignedHeader)),
+                ("untrusted_vals", ctypes.POINTER(CValidatorSet)), ("trusting_period_ns", ctypes.c_int64),
+                ("now_seconds", ctypes.c_int64), ("now_nanos", ctypes.c_int32),
+                ("max_clock_drift_ns", ctypes.c_int64), ("trust_num", ctypes.c_uint64),
+                ("trust_den", ctypes.c_uint64)]
+
+
+@dataclass
+class Header:
+    """types.Header (types/block.go:338-366)."""
+    chain_id: str
+    height: int
+    time: Tuple[int, int]
+    last_block_id: BlockID = field(default_factory=BlockID)
+    last_commit_hash: bytes = b""
+    data_hash: bytes = b""
+    validators_hash: bytes = b""
+    next_validators_hash: bytes = b""
+    consensus_hash: bytes = b""
+    app_hash: bytes = b""
+    last_results_hash: bytes = b""
+    evidence_hash: bytes = b""
+    proposer_address: bytes = b""
+    version_block: int = BLOCK_PROTOCOL
+    version_app: int = 0
+
+
+@dataclass
+class SignedHeader:
+    """types.SignedHeader (types/light.go:131-136)."""
+    header: Optional[Header]
+    commit: Optional[Commit]
+
+    @property
+    def height(self) -> int:
+        return self.header.height
+
+
+@dataclass
+class LightBlock:
+    """types.LightBlock: a signed header and the validator set at its height."""
+    signed_header: SignedHeader
+    vals: ValidatorSet
+    next_vals: Optional[ValidatorSet] = None
+
+    @property
+    def height(self) -> int:
+        return self.signed_header.header.height
+
+
+@dataclass
+class LightJob:
+    """One light-client verification (the arguments of light.Verify)."""
+    trusted: SignedHeader
+    trusted_next_vals: Optional[ValidatorSet]
+    untrusted: SignedHeader
+    untrusted_vals: Optional[ValidatorSet]
+    trusting_period_ns: int
+    now: Tuple[int, int]
+    max_clock_drift_ns: int = 10 * 10**9  # light/client.go:52 defaultMaxClockDrift
+    trust: Tuple[int, int] = (1, 3)       # light.DefaultTrustLevel
+    mode: int = LIGHT_VERIFY
+
+
+def _c_bytes(k: _Keep, b: bytes) -> CBytes:
+    p, n = k.buf(b)
+    return CBytes(p, n)
+
+
+def _c_header(k: _Keep, h: Header) -> CHeader:
+    cid = h.chain_id.encode()
+    k.refs.append(cid)
+    c = CHeader(h.version_block, h.version_app, cid, h.height, h.time[0], h.time[1], _c_block_id(k, h.last_block_id),
+                *[_c_bytes(k, getattr(h, f)) for f in _HASH_FIELDS])
+    k.refs.append(c)
+    return c
+
+
+class PreparedLightJobs:
+    """C structs for a list of LightJob, built once; headers, commits and
+    validator sets shared by object identity are passed once (the engine
+    converts and hashes each distinct one once)."""
+
+    def __init__(self, jobs: List[LightJob]):
+        k = _Keep()
+        hcache, ccache, vcache, shcache = {}, {}, {}, {}
+
+        def header(h):
+            if h is None:
+                return None
+            if id(h) not in hcache:
+                hcache[id(h)] = (h, ctypes.pointer(_c_header(k, h)))
+            return hcache[id(h)][1]
+
+        def commit(c):
+            if c is None:
+                return None
+            if id(c) not in ccache:
+                cc = _c_commit(k, c)
+                ccache[id(c)] = (c, ctypes.pointer(cc))
+            return ccache[id(c)][1]
+
+        def signed(sh):
+            if sh is None:
+                return None
+            if id(sh) not in shcache:
+                s = CSignedHeader(header(sh.header), commit(sh.commit))
+                k.refs.append(s)
+                shcache[id(sh)] = (sh, ctypes.pointer(s))
+            return shcache[id(sh)][1]
+
+        def vset(vs):
+            if vs is None:
+                return None
+            if id(vs) not in vcache:
+                s = CValidatorSet(_c_validators(k, vs), len(vs.validators), vs.proposer_index)
+                k.refs.append(s)
+                vcache[id(vs)] = (vs, ctypes.pointer(s))
+            return vcache[id(vs)][1]
+
+        arr = (CLightJob * max(1, len(jobs)))()
+        for j, jb in enumerate(jobs):
+            arr[j] = CLightJob(jb.mode, signed(jb.trusted), vset(jb.trusted_next_vals), signed(jb.untrusted),
+                               vset(jb.untrusted_vals), jb.trusting_period_ns, jb.now[0], jb.now[1],
+                               jb.max_clock_drift_ns, jb.trust[0], jb.trust[1])
+        self.keep = (k, hcache, ccache, vcache, shcache)
+        self.arr, self.n = arr, len(jobs)
+        self.stride = 1024
+        self.errs = ctypes.create_string_buffer(self.stride * max(1, self.n))
+        self.results = (ctypes.c_int32 * max(1, self.n))()
+
+    def decode(self) -> List[Tuple[int, Optional[str]]]:
+        out = []
+        for j in range(self.n):
+            kind = self.results[j]
+            raw = self.errs.raw[j * self.stride:(j + 1) * self.stride].split(b"\0", 1)[0].decode()
+            out.append((kind, raw if kind != LIGHT_OK else None))
+        return out
+
+
+def _setup_light(L):
+    if not getattr(L, "_tmhost_light", False):
+        L.tmv_light_verify_many.argtypes = [ctypes.c_void_p, ctypes.POINTER(CLightJob), ctypes.c_uint32,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_size_t]
+        L.tmv_header_hashes.argtypes = [ctypes.c_void_p, ctypes.POINTER(CHeader), ctypes.c_uint32, _u8p, _u8p]
+        L._tmhost_light = True
+    return L
+
+
+def run_light_jobs(fn, ctx_handle, pj: PreparedLightJobs) -> List[Tuple[int, Optional[str]]]:
+    """fn = tmv_light_verify_many (or the CPU harness's twin)."""
+    rc = fn(ctx_handle, pj.arr, pj.n, pj.results, pj.errs, pj.stride)
+    if rc < 0:
+        raise NativeError(f"tmv_light_verify_many failed ({rc}): {_native.last_error()}")
+    return pj.decode()
+
+
+def light_verify_many(ctx, jobs: List[LightJob]) -> List[Tuple[int, Optional[str]]]:
+    """Each job's (TMV_LIGHT_* class, error text or None), all jobs in one pass."""
+    L = _setup_light(_setup(_native.lib()))
+    return run_light_jobs(L.tmv_light_verify_many, ctx.handle, PreparedLightJobs(jobs))
+
+
+def light_verify(ctx, job: LightJob) -> Tuple[int, Optional[str]]:
+    return light_verify_many(ctx, [job])[0]
+
+
+def header_hashes_call(fn, ctx_handle, headers: List[Header]) -> List[Optional[bytes]]:
+    k = _Keep()
+    arr = (CHeader * max(1, len(headers)))()
+    for i, h in enumerate(headers):
+        arr[i] = _c_header(k, h)
+    out = (ctypes.c_uint8 * (32 * max(1, len(headers))))()
+    has = (ctypes.c_uint8 * max(1, len(headers)))()
+    rc = fn(ctx_handle, arr, len(headers), ctypes.cast(out, _u8p), ctypes.cast(has, _u8p))
+    if rc < 0:
+        raise NativeError(f"tmv_header_hashes failed ({rc})")
+    return [bytes(out[32 * i:32 * i + 32]) if has[i] else None for i in range(len(headers))]
+
+
+def header_hashes(ctx, headers: List[Header]) -> List[Optional[bytes]]:
+    """Header.Hash of each header (None where the reference returns nil)."""
+    L = _setup_light(_setup(_native.lib()))
+    return header_hashes_call(L.tmv_header_hashes, ctx.handle, headers)

@@ -102,6 +102,27 @@ class FakeBackend:
     def batches_made(self):
         return ctypes.c_int.in_dll(self.L, "commitcheck_backend_calls").value
 
+    def real_signatures(self, on: bool):
+        """Switch the test double to the C oracle's ed25519 / sr25519 verification."""
+        self.L.commitcheck_set_real_signatures(1 if on else 0)
+
+    def light_verify_many(self, jobs):
+        L = self.L
+        if not getattr(L, "_light", False):
+            L.commitcheck_light_verify_many.argtypes = [ctypes.POINTER(H.CLightJob), ctypes.c_uint32,
+                                                        ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p,
+                                                        ctypes.c_size_t]
+            L.commitcheck_header_hashes.argtypes = [ctypes.POINTER(H.CHeader), ctypes.c_uint32,
+                                                    ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8)]
+            L._light = True
+        fn = lambda _h, *a: L.commitcheck_light_verify_many(*a)  # noqa: E731
+        return H.run_light_jobs(fn, None, H.PreparedLightJobs(jobs))
+
+    def header_hashes(self, headers):
+        self.light_verify_many([])  # argtypes
+        fn = lambda _h, *a: self.L.commitcheck_header_hashes(*a)  # noqa: E731
+        return H.header_hashes_call(fn, None, headers)
+
 
 class GpuBackend:
     def __init__(self, ctx, scheme="ed25519"):

@@ -79,3 +79,72 @@ def run_driver(case, verify):
         yield inp, r
         if r is None:
             trusted, tnext = inp["signed_header"], inp["next_vals"]
+
+
+# ---------------------------------------------------------------- host (product) types
+def _host():
+    from tendermint_amd import host as H
+    return H
+
+
+def host_block_id(d):
+    H = _host()
+    return H.BlockID(_b(d["hash"]), d["psh_total"], _b(d["psh_hash"]))
+
+
+def host_header(d):
+    H = _host()
+    return H.Header(chain_id=d["chain_id"], height=d["height"], time=tuple(d["time"]),
+                    last_block_id=host_block_id(d["last_block_id"]), version_block=d["version_block"],
+                    version_app=d["version_app"],
+                    **{k: _b(d[k]) for k in ("last_commit_hash", "data_hash", "validators_hash",
+                                             "next_validators_hash", "consensus_hash", "app_hash",
+                                             "last_results_hash", "evidence_hash", "proposer_address")})
+
+
+def host_commit(d):
+    H = _host()
+    return H.Commit(d["height"], d["round"], host_block_id(d["block_id"]),
+                    [H.CommitSig(s["flag"], _b(s["address"]), tuple(s["time"]), _b(s["signature"]))
+                     for s in d["signatures"]])
+
+
+def host_signed_header(d):
+    H = _host()
+    return H.SignedHeader(host_header(d["header"]), host_commit(d["commit"]))
+
+
+def host_valset(d):
+    H = _host()
+    return H.ValidatorSet([H.Validator(_b(v["address"]), _b(v["pub_key"]), v["voting_power"], H.TMV_KIND_ED25519,
+                                       v["proposer_priority"]) for v in d], proposer_index=-1)
+
+
+def load_host_cases():
+    with open(GOLDEN) as f:
+        data = json.load(f)
+    out = []
+    for c in data["cases"]:
+        ini = c["initial"]
+        out.append({"file": c["file"], "trusted": host_signed_header(ini["signed_header"]),
+                    "trusted_next_vals": host_valset(ini["next_validator_set"]),
+                    "trusting_period_ns": ini["trusting_period_ns"],
+                    "inputs": [{"signed_header": host_signed_header(i["signed_header"]),
+                                "vals": host_valset(i["validator_set"]),
+                                "next_vals": host_valset(i["next_validator_set"]), "now": tuple(i["now"]),
+                                "verdict": i["verdict"]} for i in c["input"]]})
+    return out
+
+
+def run_host_driver(case, verify_many):
+    """driver_test.go:42-81 through the host layer: verify_many(list of
+    host.LightJob) -> [(kind, text)].  Yields (input, (kind, text))."""
+    H = _host()
+    trusted, tnext = case["trusted"], case["trusted_next_vals"]
+    for inp in case["inputs"]:
+        job = H.LightJob(trusted, tnext, inp["signed_header"], inp["vals"], case["trusting_period_ns"], inp["now"],
+                         MAX_CLOCK_DRIFT_NS, TRUST_LEVEL)
+        r = verify_many([job])[0]
+        yield inp, r
+        if r[0] == H.LIGHT_OK:
+            trusted, tnext = inp["signed_header"], inp["next_vals"]

@@ -1,8 +1,12 @@
-// CPU test harness for the commit-verification control flow
-// (tendermint_amd/csrc/host/tm_types.h) with a test-double signature scheme,
-// like the reference's mocks: "signature" = SHA-512(pk || 0^32 || msg).
-// sr25519 test keys starting with 0xFF fail to decode (status -1) and
-// sr25519 signatures without the schnorrkel marker are rejected (-2).
+// CPU test harness for the commit-verification and light-client control flow
+// (tendermint_amd/csrc/host/tm_types.h, tm_light.h) with a test-double
+// signature scheme, like the reference's mocks: "signature" =
+// SHA-512(pk || 0^32 || msg).  sr25519 test keys starting with 0xFF fail to
+// decode (status -1) and sr25519 signatures without the schnorrkel marker are
+// rejected (-2).  commitcheck_set_real_signatures(1) switches the double to
+// the C oracle (oracle/c, linked as liboracle.so: test infrastructure) so the
+// reference's own signed fixtures (light/mbt) run through the product's host
+// code on the CPU.
 #include <cstring>
 #include <memory>
 #include <string>
@@ -10,8 +14,15 @@
 
 #include "../../include/tmhost.h"
 #include "../../include/tmverify.h"
+#include "../../tendermint_amd/csrc/host/tm_light.h"
 #include "../../tendermint_amd/csrc/host/tm_types.h"
 #include "../../tendermint_amd/csrc/sha512_dev.h"
+
+extern "C" {
+int oracle_ed25519_verify(const uint8_t *pk, const uint8_t *msg, size_t mlen, const uint8_t *sig);
+int oracle_sr25519_add_check(const uint8_t *pk, const uint8_t *sig);
+int oracle_sr25519_verify(const uint8_t *pk, const uint8_t *msg, size_t mlen, const uint8_t *sig);
+}
 
 namespace {
 
@@ -26,7 +37,17 @@ Bytes fake_sig(const Bytes &pk, const Bytes &msg) {
   return s;
 }
 
+int g_real = 0;  // commitcheck_set_real_signatures
+
 int8_t fake_status(KeyType kind, const Bytes &pk, const Bytes &msg, const Bytes &sig) {
+  if (g_real) {
+    if (kind == KeyType::Sr25519) {
+      const int a = oracle_sr25519_add_check(pk.data(), sig.data());  // 0 ok, -1 key, -2 signature
+      if (a < 0) return (int8_t)a;
+      return (int8_t)oracle_sr25519_verify(pk.data(), msg.data(), msg.size(), sig.data());
+    }
+    return (int8_t)oracle_ed25519_verify(pk.data(), msg.data(), msg.size(), sig.data());
+  }
   if (kind == KeyType::Sr25519) {
     if (!pk.empty() && pk[0] == 0xFF) return -1;
     if (sig.size() != 64 || !(sig[63] & 0x80)) return -2;
@@ -112,7 +133,54 @@ int tmv_verify_votes(tmv_ctx *, uint8_t key_kind, uint32_t, const tmv_vote_templ
   return all ? TMV_ALL_VALID : TMV_NOT_ALL;
 }
 
+// Device hashing entry points (include/tmverify.h) on the host: the light
+// layer sends large windows to them.
+int tmv_merkle_roots(tmv_ctx *, const uint8_t *data, const uint32_t *leaf_off, uint32_t n_leaves,
+                     const uint32_t *tree_off, uint32_t n_trees, uint8_t *hash_out) {
+  commitcheck_backend_calls++;
+  if (tree_off[n_trees] != n_leaves) return TMV_ERR_ARG;
+  for (uint32_t t = 0; t < n_trees; t++)
+    MerkleRootHost(data, leaf_off + tree_off[t], tree_off[t + 1] - tree_off[t], hash_out + 32 * t);
+  return 0;
+}
+
+int tmv_validator_set_hashes(tmv_ctx *, const uint8_t *pk, const uint8_t *key_kind, const int64_t *power,
+                             const uint32_t *set_off, uint32_t n_sets, uint8_t *hash_out) {
+  commitcheck_backend_calls++;
+  for (uint32_t s = 0; s < n_sets; s++) {
+    ValidatorSet vs;
+    for (uint32_t i = set_off[s]; i < set_off[s + 1]; i++) {
+      Validator v;
+      v.pub_key = PubKey{key_kind[i] == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519,
+                         Bytes(pk + 32 * i, pk + 32 * i + 32)};
+      v.voting_power = power[i];
+      vs.validators.push_back(v);
+    }
+    const Bytes h = ValidatorSetHashHost(vs);
+    std::memcpy(hash_out + 32 * s, h.data(), 32);
+  }
+  return 0;
+}
+
 static tmv_ctx g_ctx;
+
+void commitcheck_set_real_signatures(int on) { g_real = on; }
+
+int commitcheck_light_verify_many(const tmv_light_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                                  size_t err_stride) {
+  return tmv_light_verify_many(&g_ctx, jobs, n_jobs, results, errs, err_stride);
+}
+
+int commitcheck_header_hashes(const tmv_header *headers, uint32_t n, uint8_t *hash_out, uint8_t *has_hash) {
+  return tmv_header_hashes(&g_ctx, headers, n, hash_out, has_hash);
+}
+
+size_t commitcheck_go_format(int what, int64_t a, int32_t b, char *out, size_t cap) {
+  std::string s = what == 0 ? GoTime(Timestamp{a, b}) : what == 1 ? GoDuration(a) : GoQuote(std::string(out));
+  std::strncpy(out, s.c_str(), cap - 1);
+  out[cap - 1] = 0;
+  return s.size();
+}
 
 // Same contract as tmv_verify_commits (include/tmhost.h), fake signatures.
 int commitcheck_verify_commits(const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
