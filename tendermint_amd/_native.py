@@ -45,10 +45,11 @@ EXPORTS = [
     "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
     "tmv_subgroup_stats", "tmv_validator_set_hashes",
     "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
-    "tmv_verify_votes", "tmv_vote_sign_bytes_device",
+    "tmv_verify_votes", "tmv_vote_sign_bytes_device", "tmv_merkle_roots",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_vote_template_encode", "tmv_verify_commit", "tmv_verify_commits",
+    "tmv_header_hashes", "tmv_light_verify_many", "tmv_light_verify",
 ]
 
 

@@ -1,53 +1,54 @@
-"""Callers of the commit verifier, driven with cross-commit batching
- — the two reference loops that feed the
-signature path one commit at a time:
+"""Callers of the verification engine, driven with cross-commit batching
+ — the reference loops that feed the
+signature path one header / block at a time:
 
-  * light.Client.verifySequential (light/client.go:554-634) ->
-    light.VerifyAdjacent (light/verifier.go:106-155) -> VerifyCommitLight
+  * light.Client.verifySequential (light/client.go:554-634): VerifyAdjacent
+    per height (light/verifier.go:106-155)
+  * light.Client.verifySkipping (light/client.go:647-727): light.Verify
+    (light/verifier.go:158-177) against a bisection cache of pivots
   * blocksync Reactor.poolRoutine (internal/blocksync/reactor.go:549-645):
-    state.Validators.VerifyCommitLight(second.LastCommit) and then
-    ValidateBlock(first) -> state.LastValidators.VerifyCommit(first.LastCommit)
+    state.Validators.VerifyCommitLight(firstID, second.LastCommit), then
+    ValidateBlock(first) -> state.LastValidators.VerifyCommit(
+    state.LastBlockID, first.Height-1, first.LastCommit)
+    (internal/state/validation.go:86-96)
 
-Here every commit check of a window of headers/blocks is planned on the host
-and all their signatures go to the GPU in ONE tmv_verify_commits call; the
-per-header / per-block results are then walked in order, so the first error
-returned is the one the sequential reference loop would return.  The
-ValidatorSet.Hash of every supplied set of a window (light/verifier.go:266,
-SURVEY §8(f) rank 4) is computed on the GPU in one tmv_validator_set_hashes
-call; the header hash itself is not (headers carry it as opaque bytes).
+The light checks run entirely in the engine's C++ host layer
+(tmv_light_verify_many: Header.Hash and ValidatorSet.Hash of a whole window
+on the device, SignedHeader.ValidateBasic, the trusting period / clock drift
+checks and every commit check of the window in one signature batch); the
+drivers here only decide which checks form a window and walk the results in
+the reference's order, so the first error returned is the one the
+one-at-a-time loop returns.  Primary/witness handling (provider I/O,
+detector) is out of scope (networking).
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Tuple
-
-import numpy as np
+from typing import Callable, Dict, List, Optional, Tuple
 
 from . import host as H
+from .host import LightBlock, LightJob, SignedHeader  # noqa: F401  (re-exported)
+
+# light/client.go:45-46
+SKIPPING_NUM, SKIPPING_DEN = 9, 16
 
 
 @dataclass
-class SignedHeader:
-    chain_id: str
-    height: int
-    time: Tuple[int, int]
-    validators_hash: bytes
-    next_validators_hash: bytes
-    commit: H.Commit
+class VerificationFailed:
+    """light.ErrVerificationFailed (light/errors.go:53-66): the class and text
+    of the wrapped error (TMV_LIGHT_*), the heights it failed between."""
+    from_height: int
+    to_height: int
+    kind: int
+    reason: str
 
-
-@dataclass
-class LightBlock:
-    header: SignedHeader
-    vals: H.ValidatorSet
-
-
-def _after(a: Tuple[int, int], b: Tuple[int, int]) -> bool:
-    return a > b
+    def __str__(self) -> str:
+        return "verify from #%d to #%d failed: %s" % (self.from_height, self.to_height, self.reason)
 
 
 def validator_set_arrays(sets: List[H.ValidatorSet]):
     """Column arrays of tmv_validator_set_hashes for `sets` (set order kept)."""
+    import numpy as np
     vals = [v for vs in sets for v in vs.validators]
     n = len(vals)
     pk = np.frombuffer(b"".join(v.pub_key for v in vals), np.uint8) if n else np.zeros(0, np.uint8)
@@ -66,87 +67,140 @@ def validator_set_hashes(ctx, sets: List[H.ValidatorSet]) -> List[bytes]:
     return [bytes(r) for r in out]
 
 
-def verify_adjacent_checks(trusted: SignedHeader, untrusted: SignedHeader,
-                           untrusted_vals_hash: Optional[bytes] = None) -> Optional[str]:
-    """The non-signature checks of light.VerifyAdjacent (light/verifier.go:115-150)
-    that this engine's callers need, in the reference's order and text;
-    `untrusted_vals_hash` = Hash() of the supplied set (verifier.go:266)."""
-    if trusted.height == 0:
-        return "height in trusted header must be set (non zero"
-    if not trusted.chain_id:
-        return "chain ID in trusted header must be set"
-    if len(trusted.next_validators_hash) == 0:
-        return "next validators hash in trusted header is empty"
-    if untrusted.height != trusted.height + 1:
-        return "headers must be adjacent in height"
-    if not _after(untrusted.time, trusted.time):
-        return "invalid header: expected new header time to be after old header time"
-    if untrusted_vals_hash is not None and untrusted.validators_hash != untrusted_vals_hash:
-        return ("invalid header: expected new header validators (%s) to match those that were supplied (%s) "
-                "at height %d" % (untrusted.validators_hash.hex().upper(), untrusted_vals_hash.hex().upper(),
-                                  untrusted.height))
-    if untrusted.validators_hash != trusted.next_validators_hash:
-        return ("invalid header: expected old header's next validators (%s) to match those from new header (%s)"
-                % (trusted.next_validators_hash.hex().upper(), untrusted.validators_hash.hex().upper()))
-    return None
-
-
-def verify_sequential(ctx, trusted: SignedHeader, blocks: List[LightBlock], window: int = 1000
-                      ) -> Tuple[int, Optional[str]]:
-    """light.Client.verifySequential over `blocks` (heights trusted+1 ...).
-    Returns (number of headers verified, first error or None).  `window`
-    headers share one GPU batch (the light client's prefetch depth)."""
+def verify_sequential(ctx, trusted: LightBlock, blocks: List[LightBlock], trusting_period_ns: int,
+                      now: Tuple[int, int], max_clock_drift_ns: int = 10 * 10**9, window: int = 1000,
+                      verify_many=None) -> Tuple[int, Optional[VerificationFailed]]:
+    """Client.verifySequential over `blocks` (heights trusted+1, ...) with a
+    single primary: VerifyAdjacent(verified, interim) per height, `window`
+    headers per engine call (the light client's prefetch).  Returns (headers
+    verified, first ErrVerificationFailed or None)."""
+    run = verify_many or (lambda jobs: H.light_verify_many(ctx, jobs))
     done = 0
+    prev = trusted
     for lo in range(0, len(blocks), window):
         chunk = blocks[lo:lo + window]
-        jobs = [H.CommitJob(H.MODE_LIGHT, trusted.chain_id, lb.vals, lb.header.commit.block_id, lb.header.height,
-                            lb.header.commit) for lb in chunk]
-        res = H.verify_commits(ctx, jobs)
-        vhash = validator_set_hashes(ctx, [lb.vals for lb in chunk])
-        for lb, err, vh in zip(chunk, res, vhash):
-            e = verify_adjacent_checks(trusted, lb.header, vh)
-            if e is None and err is not None:
-                e = "invalid header: " + err
-            if e is not None:
-                return done, e
-            trusted = lb.header
+        jobs, p = [], prev
+        for lb in chunk:
+            jobs.append(LightJob(p.signed_header, None, lb.signed_header, lb.vals, trusting_period_ns, now,
+                                 max_clock_drift_ns, mode=H.LIGHT_ADJACENT))
+            p = lb
+        for lb, (kind, text) in zip(chunk, run(jobs)):
+            if kind != H.LIGHT_OK:
+                return done, VerificationFailed(prev.height, lb.height, kind, text)
+            prev = lb
             done += 1
     return done, None
 
 
+def schedule(last_verified: int, last_failed: int) -> int:
+    """Client.schedule (light/client.go:721-725)."""
+    return last_verified + (last_failed - last_verified) * SKIPPING_NUM // SKIPPING_DEN
+
+
+def verify_skipping(ctx, trusted: LightBlock, target: LightBlock, provider: Callable[[int], LightBlock],
+                    trusting_period_ns: int, now: Tuple[int, int], max_clock_drift_ns: int = 10 * 10**9,
+                    trust: Tuple[int, int] = (1, 3), speculate: int = 8, verify_many=None
+                    ) -> Tuple[Optional[List[int]], Optional[VerificationFailed]]:
+    """Client.verifySkipping (light/client.go:647-727): bisection from the
+    trusted block towards `target`, pivots from `provider(height)`.  The
+    reference verifies one candidate per step; here every step verifies the
+    current candidate, the rest of the cache and up to `speculate` further
+    pivots (the heights schedule() would request next) in ONE engine call, and
+    the results are consumed in the reference's order, so the trace and the
+    error equal the reference's.  Returns (trace heights, None) or
+    (None, ErrVerificationFailed)."""
+    run = verify_many or (lambda jobs: H.light_verify_many(ctx, jobs))
+    cache = [target]
+    fetched: Dict[int, LightBlock] = {}
+    depth = 0
+    verified = trusted
+    trace = [trusted.height]
+    results: Dict[Tuple[int, int], Tuple[int, Optional[str]]] = {}
+
+    def block_at(h: int) -> LightBlock:
+        if h not in fetched:
+            fetched[h] = provider(h)
+        return fetched[h]
+
+    while True:
+        cand = cache[depth]
+        key = (id(verified), id(cand))
+        if key not in results:
+            batch = list(cache[depth:])
+            last = cache[-1].height
+            for _ in range(speculate):
+                p = schedule(verified.height, last)
+                if p <= verified.height or p >= last:
+                    break
+                batch.append(block_at(p))
+                last = p
+            # the client passes the verified block's own validator set
+            # (light/client.go:680-681)
+            jobs = [LightJob(verified.signed_header, verified.vals, b.signed_header, b.vals,
+                             trusting_period_ns, now, max_clock_drift_ns, trust) for b in batch]
+            for b, r in zip(batch, run(jobs)):
+                results[(id(verified), id(b))] = r
+        kind, text = results[key]
+        if kind == H.LIGHT_OK:
+            if depth == 0:
+                trace.append(target.height)
+                return trace, None
+            verified = cand
+            cache = cache[:depth]
+            depth = 0
+            trace.append(verified.height)
+        elif kind == H.LIGHT_ERR_CANT_TRUST:
+            if depth == len(cache) - 1:
+                cache.append(block_at(schedule(verified.height, cache[depth].height)))
+            depth += 1
+        else:
+            return None, VerificationFailed(verified.height, cand.height, kind, text)
+
+
 @dataclass
 class Block:
+    """The parts of a types.Block blocksync's checks read."""
     height: int
-    block_id: H.BlockID
-    last_commit: Optional[H.Commit]   # commit for height-1 (None at the first height)
-    commit: H.Commit                  # the commit for this block (= next block's LastCommit)
+    block_id: H.BlockID               # BlockID{Hash: block.Hash(), PartSetHeader}
+    last_commit: Optional[H.Commit]   # the commit for height-1 carried by this block
 
 
-def blocksync_replay(ctx, chain_id: str, vals: H.ValidatorSet, blocks: List[Block], window: int = 600
+def blocksync_replay(ctx, chain_id: str, vals: H.ValidatorSet, blocks: List[Block], last_block_id: H.BlockID,
+                     initial_height: int = 1, window: int = 600
                      ) -> Tuple[int, Optional[Tuple[int, str]]]:
-    """poolRoutine's two checks per block pair (first, second):
+    """poolRoutine's checks for each block pair (first, second) over a static
+    validator set (state.Validators == state.LastValidators):
       light: vals.VerifyCommitLight(chainID, first.BlockID, first.Height, second.LastCommit)
-      full:  vals.VerifyCommit(chainID, prev.BlockID, first.Height-1, first.LastCommit)
-    over a static validator set, `window` blocks per GPU batch (the pool
-    buffers up to 600 blocks, internal/blocksync/pool.go:32-35).  A commit
-    checked light at height H and full at H+1 is one tmv_commit, so its
+      full:  ValidateBlock(first): at state.InitialHeight the LastCommit must
+             carry no signatures, else vals.VerifyCommit(chainID,
+             state.LastBlockID, first.Height-1, first.LastCommit)
+    with state.LastBlockID = `last_block_id` for the first block and the
+    previous block's BlockID after it (ApplyBlock).  `window` blocks per
+    engine call (the pool buffers up to 600, internal/blocksync/pool.go:32-35);
+    a commit read light at height H and full at H+1 is the same object, so its
     signatures are verified once.  Returns (blocks applied, (height, error))."""
     applied = 0
+    state_last = last_block_id
     for lo in range(0, len(blocks) - 1, window):
         chunk = blocks[lo:lo + window + 1]
-        jobs, where = [], []
+        jobs, where, early = [], [], {}
         for i in range(len(chunk) - 1):
             first, second = chunk[i], chunk[i + 1]
-            jobs.append(H.CommitJob(H.MODE_LIGHT, chain_id, vals, first.block_id, first.height, first.commit))
-            where.append((first.height, "light"))
-            if first.last_commit is not None:
-                prev = blocks[lo + i - 1] if lo + i >= 1 else None
-                pbid = prev.block_id if prev is not None else first.last_commit.block_id
-                jobs.append(H.CommitJob(H.MODE_FULL, chain_id, vals, pbid, first.height - 1, first.last_commit))
-                where.append((first.height, "full"))
-        res = H.verify_commits(ctx, jobs)
-        for (height, _kind), err in zip(where, res):
+            where.append((first.height, len(jobs)))
+            jobs.append(H.CommitJob(H.MODE_LIGHT, chain_id, vals, first.block_id, first.height, second.last_commit))
+            if first.height == initial_height:
+                if first.last_commit is not None and first.last_commit.signatures:
+                    early[first.height] = "initial block can't have LastCommit signatures"
+                jobs.append(None)
+            else:
+                jobs.append(H.CommitJob(H.MODE_FULL, chain_id, vals, state_last, first.height - 1, first.last_commit))
+            state_last = first.block_id
+        res = H.verify_commits(ctx, [j for j in jobs if j is not None])
+        it = iter(res)
+        flat = [next(it) if j is not None else None for j in jobs]
+        for height, k in where:
+            err = flat[k] or early.get(height) or flat[k + 1]
             if err is not None:
-                return applied + (height - chunk[0].height), (height, err)
-        applied += len(chunk) - 1
+                return applied, (height, err)
+            applied += 1
     return applied, None

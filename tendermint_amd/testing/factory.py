@@ -310,13 +310,66 @@ def _valset_hash(vals) -> bytes:
     return _merkle([_simple_validator_bytes(v) for v in vals.validators])
 
 
+def _uvarint(u: int) -> bytes:
+    u &= (1 << 64) - 1
+    out = bytearray()
+    while u >= 0x80:
+        out.append((u & 0x7F) | 0x80)
+        u >>= 7
+    out.append(u)
+    return bytes(out)
+
+
+def _field(tag: int, b: bytes) -> bytes:
+    return bytes([tag]) + _uvarint(len(b)) + b
+
+
+def header_hash(h) -> bytes:
+    """Header.Hash (types/block.go:447-478) of a host.Header, for generating
+    chains whose commits sign their headers (the engine recomputes and checks
+    it, light/verifier.go:243 -> types/light.go:168)."""
+    ts = (b"\x08" + _uvarint(h.time[0]) if h.time[0] else b"") + (b"\x10" + _uvarint(h.time[1]) if h.time[1] else b"")
+    lb = h.last_block_id
+    psh = (b"\x08" + _uvarint(lb.psh_total) if lb.psh_total else b"") + (_field(0x12, lb.psh_hash) if lb.psh_hash else b"")
+    bz = lambda b: _field(0x0A, b) if b else b""  # noqa: E731
+    leaves = [(b"\x08" + _uvarint(h.version_block) if h.version_block else b"") +
+              (b"\x10" + _uvarint(h.version_app) if h.version_app else b""),
+              bz(h.chain_id.encode()), b"\x08" + _uvarint(h.height) if h.height else b"", ts,
+              (_field(0x0A, lb.hash) if lb.hash else b"") + _field(0x12, psh),
+              bz(h.last_commit_hash), bz(h.data_hash), bz(h.validators_hash), bz(h.next_validators_hash),
+              bz(h.consensus_hash), bz(h.app_hash), bz(h.last_results_hash), bz(h.evidence_hash),
+              bz(h.proposer_address)]
+    return _merkle(leaves)
+
+
+def _signed_header(H, chain_id, height, round_, t, vals, nvals, signers_sorted, last_block_id, rng, sign=True):
+    """A header over (vals, nvals) and the commit of all signers for it."""
+    hdr = H.Header(chain_id=chain_id, height=height, time=t, last_block_id=last_block_id,
+                   last_commit_hash=_rand32(rng), data_hash=_rand32(rng), validators_hash=_valset_hash(vals),
+                   next_validators_hash=_valset_hash(nvals), consensus_hash=_rand32(rng), app_hash=_rand32(rng)[:20],
+                   proposer_address=vals.validators[0].address)
+    hbid = H.BlockID(header_hash(hdr), 1, _rand32(rng))
+    bid = BlockID(hbid.hash, PartSetHeader(hbid.psh_total, hbid.psh_hash))
+    sigs = []
+    for i, s in enumerate(signers_sorted):
+        ts = (t[0], t[1] + i)
+        msg = commit_vote_message(chain_id, height, round_, bid, ts[0], ts[1])
+        sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg) if sign else b""))
+    return H.SignedHeader(hdr, H.Commit(height, round_, hbid, sigs))
+
+
+def _rand32(rng) -> bytes:
+    return bytes(rng.randrange(256) for _ in range(32))
+
+
 def make_light_chain(n_headers: int, n_vals: int = 100, chain_id: str = "test", rotate: int = 1, seed: int = 7):
     """Config 3 shape (light/helpers_test.go:165-216 genLightBlocksWithKeys):
     n_vals validators of power 2, `rotate` keys replaced per height, round 1,
-    every validator signs.  Returns (trusted SignedHeader at height 1,
-    [LightBlock] for heights 2..n_headers+1)."""
+    every validator signs, one header per second.  Returns (trusted
+    LightBlock at height 1, [LightBlock] for heights 2..n_headers+1); every
+    LightBlock carries its validator set and the next one, every header's
+    Hash() is the BlockID its commit signs."""
     from .. import host as H
-    from ..chains import LightBlock, SignedHeader
     rng = random.Random(seed)
     next_key = [n_vals]
     signers = [Ed25519Signer(key_seed(i, "lkey")) for i in range(n_vals)]
@@ -326,41 +379,32 @@ def make_light_chain(n_headers: int, n_vals: int = 100, chain_id: str = "test", 
         return vs, H.ValidatorSet([H.Validator(hashlib.sha256(s.public_key).digest()[:20], s.public_key, 2)
                                    for s in vs], proposer_index=0)
 
-    def header(height, sgs, next_sgs, t):
-        vs, vals = valset(sgs)
-        _, nvals = valset(next_sgs)
-        bid = random_block_id(rng)
-        hbid = H.BlockID(bid.hash, bid.part_set_header.total, bid.part_set_header.hash)
-        sigs = []
-        for i, s in enumerate(vs):
-            ts = (t[0], t[1] + i)
-            msg = commit_vote_message(chain_id, height, 1, bid, ts[0], ts[1])
-            sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
-        commit = H.Commit(height, 1, hbid, sigs)
-        return SignedHeader(chain_id, height, t, _valset_hash(vals), _valset_hash(nvals), commit), vals
-
-    cur = signers
-    t0 = 1577836800
-    nxt = list(cur)
-    for _ in range(rotate):
-        nxt = nxt[1:] + [Ed25519Signer(key_seed(next_key[0], "lkey"))]
-        next_key[0] += 1
-    trusted, _ = header(1, cur, nxt, (t0, 0))
-    blocks = []
-    for h in range(2, n_headers + 2):
-        cur = nxt
+    def rotated(cur):
         nxt = list(cur)
         for _ in range(rotate):
             nxt = nxt[1:] + [Ed25519Signer(key_seed(next_key[0], "lkey"))]
             next_key[0] += 1
-        hd, vals = header(h, cur, nxt, (t0 + h, 0))
-        blocks.append(LightBlock(hd, vals))
-    return trusted, blocks
+        return nxt
+
+    t0 = 1577836800
+    cur = signers
+    nxt = rotated(cur)
+    out = []
+    last_bid = H.BlockID()
+    for h in range(1, n_headers + 2):
+        vs, vals = valset(cur)
+        _, nvals = valset(nxt)
+        sh = _signed_header(H, chain_id, h, 1, (t0 + h, 0), vals, nvals, vs, last_bid, rng)
+        out.append(H.LightBlock(sh, vals, nvals))
+        last_bid = sh.commit.block_id
+        cur, nxt = nxt, rotated(nxt)
+    return out[0], out[1:]
 
 
 def make_block_chain(n_blocks: int, n_vals: int = 175, chain_id: str = "test_chain_id", seed: int = 11):
-    """Config 4 shape: a chain of n_blocks with a static n_vals-validator set;
-    block h carries LastCommit = commit for h-1.  Returns (ValidatorSet, [Block])."""
+    """Config 4 shape: a chain of n_blocks (heights 1..n_blocks, initial height
+    1) with a static n_vals-validator set; block h carries LastCommit = the
+    commit for h-1 (none at height 1).  Returns (ValidatorSet, [Block])."""
     from .. import host as H
     from ..chains import Block
     rng = random.Random(seed)
@@ -373,12 +417,11 @@ def make_block_chain(n_blocks: int, n_vals: int = 175, chain_id: str = "test_cha
     for h in range(1, n_blocks + 1):
         bid = random_block_id(rng)
         hbid = H.BlockID(bid.hash, bid.part_set_header.total, bid.part_set_header.hash)
+        blocks.append(Block(h, hbid, prev_commit))
         sigs = []
         for i, s in enumerate(signers):
             ts = (1577836800 + h, i * 1000)
             msg = commit_vote_message(chain_id, h, 0, bid, ts[0], ts[1])
             sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
-        commit = H.Commit(h, 0, hbid, sigs)
-        blocks.append(Block(h, hbid, prev_commit, commit))
-        prev_commit = commit
+        prev_commit = H.Commit(h, 0, hbid, sigs)
     return vals, blocks

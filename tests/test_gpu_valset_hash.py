@@ -108,12 +108,13 @@ def test_argument_errors(ctx):
 
 def test_light_client_checks_supplied_set(ctx):
     trusted, blocks = make_light_chain(12, 20)
-    n, err = chains.verify_sequential(ctx, trusted, blocks)
+    period, now = 10**15, (blocks[-1].signed_header.header.time[0] + 1, 0)
+    n, err = chains.verify_sequential(ctx, trusted, blocks, period, now)
     assert err is None and n == 12
     # a supplied set that does not hash to the header's ValidatorsHash
     vals = blocks[6].vals
     v0 = vals.validators[0]
     vals.validators[0] = type(v0)(v0.address, v0.pub_key, v0.voting_power + 1, v0.key_kind, v0.proposer_priority)
-    n, err = chains.verify_sequential(ctx, trusted, blocks)
-    assert n == 6 and err.startswith("invalid header: expected new header validators (")
-    assert err.endswith("at height %d" % blocks[6].header.height)
+    n, err = chains.verify_sequential(ctx, trusted, blocks, period, now)
+    assert n == 6 and err.reason.startswith("invalid header: expected new header validators (")
+    assert err.reason.endswith("at height %d" % blocks[6].height)

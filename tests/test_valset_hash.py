@@ -68,6 +68,6 @@ def test_factory_headers_carry_the_set_hash():
     trusted, blocks = factory.make_light_chain(3, 7)
     for lb in blocks:
         vals = [(v.pub_key, v.key_kind, v.voting_power) for v in lb.vals.validators]
-        assert lb.header.validators_hash == M.validator_set_hash(vals)
+        assert lb.signed_header.header.validators_hash == M.validator_set_hash(vals)
     assert isinstance(H.ValidatorSet([]).validators, list)
     assert hashlib.sha256(b"").digest() == M.validator_set_hash([])

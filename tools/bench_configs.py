@@ -3,8 +3,9 @@
 each; the headline line is bench.py's C2).  Single GPU.
 
   C1  types.VerifyCommit, 150 validators: p50/p99 latency, cold + warm key cache
-  C3  light sequential: H headers x 100 validators (VerifyCommitLight, 67
-      signatures read per header), window-batched
+  C3  light sequential: H headers x 100 validators (VerifyAdjacent: header
+      and validator-set hashes + VerifyCommitLight, 67 signatures read per
+      header), window-batched through tmv_light_verify_many
   C4  blocksync replay: B blocks x 175 validators (light + full check per
       block = 292 reference verifications, 175 unique)
   C5  mixed ed25519 + sr25519 batch (kernel path, inputs resident)
@@ -39,18 +40,24 @@ if "1" in only:
 
 if "3" in only:
     trusted, blocks = Fa.make_light_chain(a.headers, 100)
-    chains.verify_sequential(ctx, trusted, blocks[:50])  # warm
+    period, now = 10**15, (blocks[-1].signed_header.header.time[0] + 1, 0)
+    chains.verify_sequential(ctx, trusted, blocks[:50], period, now)  # warm
     t = time.perf_counter()
-    n, err = chains.verify_sequential(ctx, trusted, blocks, window=1000)
+    n, err = chains.verify_sequential(ctx, trusted, blocks, period, now, window=1000)
     dt = time.perf_counter() - t
     assert err is None, err
     # the native part alone: C structs prepared outside the timed region
-    pj = [H.PreparedJobs([H.CommitJob(H.MODE_LIGHT, trusted.chain_id, lb.vals, lb.header.commit.block_id,
-                                      lb.header.height, lb.header.commit) for lb in blocks[lo:lo + 1000]])
-          for lo in range(0, len(blocks), 1000)]
+    pj = []
+    for lo in range(0, len(blocks), 1000):
+        prev = [trusted] + blocks[lo:lo + 999] if lo == 0 else blocks[lo - 1:lo + 999]
+        pj.append(H.PreparedLightJobs([H.LightJob(p.signed_header, None, lb.signed_header, lb.vals, period, now,
+                                                  mode=H.LIGHT_ADJACENT)
+                                       for p, lb in zip(prev, blocks[lo:lo + 1000])]))
+    L = H._setup_light(H._setup(N.lib()))
     t = time.perf_counter()
     for p in pj:
-        H.run_prepared_jobs(ctx, p)
+        res = H.run_light_jobs(L.tmv_light_verify_many, ctx.handle, p)
+        assert all(k == 0 for k, _ in res)
     dn = time.perf_counter() - t
     print(json.dumps({"config": f"C3 light sequential {a.headers} headers x 100 vals", "seconds": round(dt, 4),
                       "headers_per_s": round(n / dt, 1), "verifies_per_s_ref_count": round(67 * n / dt),
@@ -59,15 +66,15 @@ if "3" in only:
 
 if "4" in only:
     vals, blocks = Fa.make_block_chain(a.blocks, 175)
-    chains.blocksync_replay(ctx, "test_chain_id", vals, blocks[:20])  # warm (key table)
+    chains.blocksync_replay(ctx, "test_chain_id", vals, blocks[:20], H.BlockID())  # warm (key table)
     t = time.perf_counter()
-    applied, err = chains.blocksync_replay(ctx, "test_chain_id", vals, blocks, window=600)
+    applied, err = chains.blocksync_replay(ctx, "test_chain_id", vals, blocks, H.BlockID(), window=600)
     dt = time.perf_counter() - t
     assert err is None, err
     jobs = []
     for i in range(1, len(blocks) - 1):
-        f = blocks[i]
-        jobs.append(H.CommitJob(H.MODE_LIGHT, "test_chain_id", vals, f.block_id, f.height, f.commit))
+        f, s2 = blocks[i], blocks[i + 1]
+        jobs.append(H.CommitJob(H.MODE_LIGHT, "test_chain_id", vals, f.block_id, f.height, s2.last_commit))
         jobs.append(H.CommitJob(H.MODE_FULL, "test_chain_id", vals, blocks[i - 1].block_id, f.height - 1,
                                 f.last_commit))
     pj = [H.PreparedJobs(jobs[lo:lo + 1200]) for lo in range(0, len(jobs), 1200)]
