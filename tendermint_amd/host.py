@@ -276,11 +276,13 @@ def verify_commit_light_trusting(ctx, chain_id: str, vals, commit, trust_level=(
 
 
 class BatchVerifier:
-    """crypto.BatchVerifier over tmv_batch_* (crypto/crypto.go:66-76)."""
+    """crypto.BatchVerifier over tmv_batch_* (crypto/crypto.go:66-76).
+    `lib` / a raw context handle select another library exporting the same
+    C-ABI (the CPU test harness)."""
 
-    def __init__(self, ctx, key_kind: int):
-        self._L = _setup(_native.lib())
-        self._h = self._L.tmv_batch_new(ctx.handle, key_kind)
+    def __init__(self, ctx, key_kind: int, lib=None):
+        self._L = _setup(lib or _native.lib())
+        self._h = self._L.tmv_batch_new(getattr(ctx, "handle", ctx), key_kind)
         if not self._h:
             raise NativeError("no batch verifier for this key type")
         self.deferred_add_error: Optional[Tuple[int, str]] = None
@@ -314,11 +316,13 @@ class BatchVerifier:
             pass
 
 
-def create_batch_verifier(ctx, key_kind: int) -> Optional[BatchVerifier]:
-    """batch.CreateBatchVerifier: None for key types without batch support."""
-    if key_kind not in (TMV_KIND_ED25519, TMV_KIND_SR25519):
+def create_batch_verifier(ctx, key_kind: int, lib=None) -> Optional[BatchVerifier]:
+    """batch.CreateBatchVerifier (crypto/batch/batch.go:11-21): None for key
+    types without batch support (the C-ABI returns NULL for them)."""
+    try:
+        return BatchVerifier(ctx, key_kind, lib)
+    except NativeError:
         return None
-    return BatchVerifier(ctx, key_kind)
 
 
 def supports_batch_verifier(key_kind: int) -> bool:

@@ -166,6 +166,8 @@ static tmv_ctx g_ctx;
 
 void commitcheck_set_real_signatures(int on) { g_real = on; }
 
+tmv_ctx *commitcheck_ctx(void) { return &g_ctx; }
+
 int commitcheck_light_verify_many(const tmv_light_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                                   size_t err_stride) {
   return tmv_light_verify_many(&g_ctx, jobs, n_jobs, results, errs, err_stride);

@@ -100,3 +100,18 @@ extern "C" void hostcheck_merlin_test(uint8_t out[32]) {
   strobe_begin_op(s, 1 | 2 | 4);
   strobe_prf(s, out, 32);
 }
+
+// Device ChaCha20 block function (msm.h, row I: the batch weights z_i) on the
+// host: key and nonce as RFC 8439 bytes (little-endian words), one block.
+#include "../../tendermint_amd/csrc/msm.h"
+extern "C" void hostcheck_chacha20_block(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12],
+                                         uint8_t out[64]) {
+  uint32_t k[8], n[3], o[16];
+  load_words(k, key);
+  for (int i = 0; i < 3; i++)
+    n[i] = (uint32_t)nonce[4 * i] | ((uint32_t)nonce[4 * i + 1] << 8) | ((uint32_t)nonce[4 * i + 2] << 16) |
+           ((uint32_t)nonce[4 * i + 3] << 24);
+  chacha20_block(o, k, counter, n);
+  for (int i = 0; i < 16; i++)
+    for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(o[i] >> (8 * j));
+}

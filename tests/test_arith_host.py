@@ -69,3 +69,72 @@ def test_verify_core_vs_oracle(H, golden):
     out = np.zeros(len(ents), np.uint8)
     H.hostcheck_ed25519_verify_batch(p(pk), p(sig), p(msg), p(off, ctypes.c_uint32), len(ents), p(out))
     assert np.array_equal(out, ref)
+
+
+def _chacha20_py(key: bytes, counter: int, nonce: bytes) -> bytes:
+    """RFC 8439 §2.3 block function, restated in Python (checker)."""
+    M = 0xFFFFFFFF
+    rotl = lambda x, n: ((x << n) | (x >> (32 - n))) & M  # noqa: E731
+    st = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574] + [int(x) for x in np.frombuffer(key, "<u4")] + \
+         [counter] + [int(x) for x in np.frombuffer(nonce, "<u4")]
+    s = list(st)
+
+    def qr(a, b, c, d):
+        s[a] = (s[a] + s[b]) & M; s[d] = rotl(s[d] ^ s[a], 16)
+        s[c] = (s[c] + s[d]) & M; s[b] = rotl(s[b] ^ s[c], 12)
+        s[a] = (s[a] + s[b]) & M; s[d] = rotl(s[d] ^ s[a], 8)
+        s[c] = (s[c] + s[d]) & M; s[b] = rotl(s[b] ^ s[c], 7)
+    for _ in range(10):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    return b"".join(int((a + b) & M).to_bytes(4, "little") for a, b in zip(s, st))
+
+
+def _chacha20_openssl(key: bytes, counter: int, nonce: bytes) -> bytes:
+    """One keystream block from OpenSSL's EVP_chacha20 (IV = counter || nonce)."""
+    lib = ctypes.CDLL("libcrypto.so.3")
+    lib.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
+    lib.EVP_chacha20.restype = ctypes.c_void_p
+    lib.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
+                                       ctypes.c_char_p]
+    lib.EVP_EncryptUpdate.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int),
+                                      ctypes.c_char_p, ctypes.c_int]
+    lib.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
+    c = lib.EVP_CIPHER_CTX_new()
+    assert lib.EVP_EncryptInit_ex(c, lib.EVP_chacha20(), None, key, counter.to_bytes(4, "little") + nonce) == 1
+    out = ctypes.create_string_buffer(64)
+    n = ctypes.c_int(0)
+    assert lib.EVP_EncryptUpdate(c, out, ctypes.byref(n), bytes(64), 64) == 1
+    lib.EVP_CIPHER_CTX_free(c)
+    return out.raw
+
+
+def test_chacha20_known_answer(H):
+    """The device ChaCha20 (msm.h chacha20_block, the batch equation's z_i,
+    SURVEY row I) against RFC 8439 §2.3.2's test vector, a Python restatement
+    and OpenSSL's EVP_chacha20 on random keys / counters / nonces: a weight
+    generator bug (zero or low-entropy z_i) would let a bad signature pass its
+    group check."""
+    H.hostcheck_chacha20_block.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p]
+
+    def dev(key, counter, nonce):
+        out = ctypes.create_string_buffer(64)
+        H.hostcheck_chacha20_block(key, counter, nonce, out)
+        return out.raw
+
+    key = bytes(range(32))
+    nonce = bytes.fromhex("000000090000004a00000000")
+    want = bytes.fromhex("10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+                         "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+    assert _chacha20_py(key, 1, nonce) == want
+    assert _chacha20_openssl(key, 1, nonce) == want
+    assert dev(key, 1, nonce) == want
+    rng = np.random.default_rng(8439)
+    for _ in range(200):
+        k = rng.bytes(32)
+        n = rng.bytes(12)
+        ctr = int(rng.integers(0, 2**32))
+        assert dev(k, ctr, n) == _chacha20_openssl(k, ctr, n)
+    # weights for consecutive entries (counter = entry index) are distinct and nonzero
+    z = {dev(key, e, nonce)[:16] for e in range(4096)}
+    assert len(z) == 4096 and bytes(16) not in z
