@@ -28,6 +28,7 @@ oracle "port" on the host's cores; the Go reference cannot be built here).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import statistics
@@ -74,21 +75,31 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
+PMC_DIRS = ("r02", "r01_close")  # newest first
+
+
 def _load_pmc(method: str):
-    """PMC summary of a launch of 32 C2 batches from the committed passes
-    (tools/profile_round.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE; tools/pmc_derived.py: occupancy, VALU issue)."""
-    path = (os.path.join(REPO, "profiles", "r01_close", "pmc_batch.json") if method == "batch"
-            else os.path.join(REPO, "profiles", "r01_msm", "pmc_per_entry.json"))
-    try:
+    """PMC summary of the batch-equation (or per-entry) pipeline from the
+    newest committed passes (tools/profile_round.sh + tools/pmc_summary.py:
+    FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_derived.py:
+    occupancy, VALU issue), normalised to one step (one 10k C2 batch)."""
+    name = "pmc_batch.json" if method == "batch" else "pmc_per_entry.json"
+    for d in PMC_DIRS + ("r01_msm",):
+        path = os.path.join(REPO, "profiles", d, name)
+        if not os.path.exists(path):
+            continue
         with open(path) as f:
-            return json.load(f)
-    except Exception:
-        return {}
-
-
-def _load_traffic(method: str):
-    return _load_pmc(method).get("hbm_bytes_per_launch")
+            pmc = json.load(f)
+        per_launch = pmc.get("batches_per_launch", 32)
+        out = dict(pmc)
+        if "hbm_bytes_per_launch" in pmc:
+            out["hbm_bytes_per_step"] = int(pmc["hbm_bytes_per_launch"] / per_launch)
+            out["note"] = (f"HBM bytes per 10k-signature step from PMC (profiles/{d}/{name}: FETCH_SIZE x2 gfx950 "
+                           f"correction + WRITE_SIZE, launches of {per_launch} batches); algorithmic input bytes per "
+                           "step = 10k x ~222 B = 2.2 MB")
+        out["source"] = f"profiles/{d}/{name}"
+        return out
+    return {}
 
 
 def _pmc_kernels(method: str):
@@ -102,24 +113,57 @@ def _pmc_kernels(method: str):
     return out or None
 
 
-def cpu_baseline(batch, seconds_target: float = 12.0):
-    """Oracle C port on the host cores, bounded sample (rank 0, N=1 only)."""
+def host_cpu_info():
+    """The cores this process may use (affinity and cgroup CPU quota), the
+    machine's CPU count and model."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except Exception:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except Exception:
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except Exception:
+        pass
+    usable = min(n, quota) if quota else n
+    return {"usable_cores": usable, "machine_cpus": os.cpu_count(), "cgroup_quota_cores": quota, "model": model}
+
+
+def cpu_baseline(batch, seconds_target: float = 8.0):
+    """Oracle C port on all the host cores this process may use, bounded
+    sample (rank 0, N=1 only)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_c  # noqa: E402  (test infrastructure; checker/baseline only)
-    threads = int(os.environ.get("TMV_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    info = host_cpu_info()
+    threads = int(os.environ.get("TMV_CPU_THREADS", info["usable_cores"]))
     # calibrate on 1,000 sigs, then size the sample to ~seconds_target of CPU time
     sub = batch.off[:1001]
     t0 = time.perf_counter()
     oracle_c.ed25519_verify_packed(batch.pk[:32000], batch.sig[:64000], batch.msg, sub, threads=1)
     per_sig_cpu = (time.perf_counter() - t0) / 1000
-    reps = max(1, int(seconds_target / (per_sig_cpu * batch.n)))
+    reps = max(1, int(seconds_target * threads / (per_sig_cpu * batch.n)))
     t0 = time.perf_counter()
     for _ in range(reps):
         oracle_c.ed25519_verify_packed(batch.pk, batch.sig, batch.msg, batch.off, threads=threads)
     wall = time.perf_counter() - t0
     out = {"value": round(reps * batch.n / wall, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
-           "sample": f"C2 batch ({batch.n} sigs) x {reps} passes, oracle/c/ed25519_oracle.c, "
-                     f"{threads} pthreads; Go/curve25519-voi not buildable here (no toolchain)"}
+           "host": info,
+           "sample": f"C2 batch ({batch.n} sigs) x {reps} passes, oracle/c/ed25519_oracle.c (plain C, radix 2^51), "
+                     f"{threads} pthreads = every core this process may use; Go/curve25519-voi not buildable here "
+                     "(no Go toolchain, voi absent)"}
     out["openssl_proxy"] = _openssl_proxy(threads)
     return out
 
@@ -166,120 +210,213 @@ def _c2(a):
     return make_c2_batch(a[0], seed=a[1])
 
 
+VALID_KINDS = ("honest", "small_order", "noncanonical_y", "neg_zero")  # factory.make_c2_batch's valid entries
+
+
+class _HostStream:
+    """--cpu-stub stand-in for torch.cuda.Stream (the control flow only)."""
+    cuda_stream = 0
+
+    def wait_stream(self, other):
+        pass
+
+
+class _HostEvent:
+    def __init__(self, **_):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+def plan_launches(steps: int, per_launch: int, inflight: int, max_per_launch: int = 32):
+    """Split `steps` batches into launches: per_launch > 0 fixes the launch
+    size; 0 = auto: enough launches to keep `inflight` streams busy, at most
+    max_per_launch batches each.  Returns the list of launch sizes (sum = steps)."""
+    if per_launch <= 0:
+        per_launch = max(1, min(max_per_launch, -(-steps // max(1, inflight))))
+    sizes = [per_launch] * (steps // per_launch)
+    if steps % per_launch:
+        sizes.append(steps % per_launch)
+    return sizes
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1536)
-    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=1536, help="C2 batches verified in the timed region")
+    ap.add_argument("--warmup", type=int, default=64, help="C2 batches verified before timing")
     ap.add_argument("--batch", type=int, default=10_000)
-    ap.add_argument("--per-launch", type=int, default=32,
-                    help="independent batches per pipeline launch (tmv_verify_batches_device)")
+    ap.add_argument("--per-launch", type=int, default=0,
+                    help="batches per pipeline launch (tmv_verify_batches_device, <= 32); 0 = auto")
     ap.add_argument("--inflight", type=int, default=4, help="launches in flight (streams)")
+    ap.add_argument("--resident", type=int, default=32, help="distinct C2 batches held in HBM per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip latency / end-to-end / C1 measurements")
     ap.add_argument("--method", choices=["batch", "per-entry"], default="batch",
                     help="batch: random-linear-combination group check + per-entry fallback "
                          "(voi's BatchVerifier.Verify); per-entry: every signature verified singly")
     ap.add_argument("--group-log2", type=int, default=0)
     ap.add_argument("--window", type=int, default=0)
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="CI only: run the launch / gather / timing control flow on the CPU (gloo) with a stub "
+                         "engine that writes the known statuses; no GPU, no verification, not a measurement")
     args = ap.parse_args()
+    stub = args.cpu_stub
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    K = max(1, min(64, args.per_launch))
     F = max(1, args.inflight)
-    # K distinct C2 batches per rank (own keys / messages), generated on the
+    R = max(1, min(64, args.resident))
+    sizes = plan_launches(max(1, args.steps), args.per_launch, F)
+    K = max(sizes)
+    # R distinct C2 batches per rank (own keys / messages), generated on the
     # host before this process touches the GPU (worker processes are forked)
-    with ProcessPoolExecutor(min(8, K)) as ex:
-        batches = list(ex.map(_c2, [(args.batch, 0xED25519 + 1000 * rank + j) for j in range(K)]))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
-
-    ctx = N.Context(1 << local_rank)
-    ctx.set_batch_options(group_log2=args.group_log2, window_bits=args.window)
+    with ProcessPoolExecutor(min(8, R)) as ex:
+        batches = list(ex.map(_c2, [(args.batch, 0xED25519 + 1000 * rank + j) for j in range(R)]))
+    if stub:
+        if world > 1:
+            dist.init_process_group("gloo")
+        dev = torch.device("cpu")
+        ctx = None
+        sync = lambda d=None: None  # noqa: E731
+        Stream, Event, stream_ctx = (lambda d: _HostStream()), _HostEvent, (lambda st: contextlib.nullcontext())
+    else:
+        if world > 1:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
+        ctx = N.Context(1 << local_rank)
+        ctx.set_batch_options(group_log2=args.group_log2, window_bits=args.window)
+        sync = torch.cuda.synchronize
+        Stream, Event, stream_ctx = torch.cuda.Stream, torch.cuda.Event, torch.cuda.stream
     flags = N.TMV_FLAG_BATCH_EQUATION if args.method == "batch" else N.TMV_FLAG_PER_ENTRY
     batch = batches[0]
     n = batch.n
+    expect_valid = [sum(k in VALID_KINDS for k in b.kinds) for b in batches]
     d_in = []
     for b in batches:
         d_in.append((torch.from_numpy(b.pk).to(dev), torch.from_numpy(b.sig).to(dev), torch.from_numpy(b.msg).to(dev),
                      torch.from_numpy(b.off.view(np.int32)).to(dev), int(b.off[-1] - b.off[0])))
-    # one contiguous status vector per in-flight launch; batch j is a slice
+    # one contiguous status vector per stream; the j-th batch of a launch is a slice
     d_valid = [torch.zeros(K * n, dtype=torch.int8, device=dev) for _ in range(F)]
-    refs = [[N.BatchRef(pk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(), n, mb,
-                        d_valid[f][j * n:(j + 1) * n].data_ptr()) for j, (pk, sig, msg, off, mb) in enumerate(d_in)]
-            for f in range(F)]
-    streams = [torch.cuda.Stream(dev) for _ in range(F)]
-    comm = torch.cuda.Stream(dev) if world > 1 else None
 
-    def launch(i, kk=K, ev_pair=None):
+    def refs(f, first, kk):
+        out = []
+        for j in range(kk):
+            pk, sig, msg, off, mb = d_in[(first + j) % R]
+            out.append(N.BatchRef(pk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(), n, mb,
+                                  d_valid[f][j * n:(j + 1) * n].data_ptr()))
+        return out
+    streams = [Stream(dev) for _ in range(F)]
+    comm = Stream(dev) if world > 1 else None
+    if stub:  # the statuses the engine would write, per resident batch
+        stub_status = [torch.tensor([1 if k in VALID_KINDS else 0 for k in b.kinds], dtype=torch.int8)
+                       for b in batches]
+    gathered = {}
+
+    def launch(i, first, kk, ev_pair=None):
         f = i % F
         st = streams[f]
         if ev_pair is not None:
             ev_pair[0].record(st)
-        ctx.verify_batches_device(local_rank, N.TMV_KIND_ED25519, flags, refs[f][:kk], st.cuda_stream)
+        if stub:
+            for j in range(kk):
+                d_valid[f][j * n:(j + 1) * n] = stub_status[(first + j) % R]
+        else:
+            ctx.verify_batches_device(local_rank, N.TMV_KIND_ED25519, flags, refs(f, first, kk), st.cuda_stream)
         if ev_pair is not None:
             ev_pair[1].record(st)
         if world > 1:
-            # one collective per launch (the K vectors are contiguous), in
+            # one collective per launch (its kk vectors are contiguous), in
             # issue order on one stream, after this launch
             comm.wait_stream(st)
-            with torch.cuda.stream(comm):
-                all_gather_validity(d_valid[f][:kk * n], [kk * n] * world)
+            with stream_ctx(comm):
+                gathered[f] = all_gather_validity(d_valid[f][:kk * n], [kk * n] * world)
             st.wait_stream(comm)
 
-    # single-batch latency (one batch per launch, one at a time), untimed for value
-    lat_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
-    for _ in range(2):
-        launch(0, 1)
-    torch.cuda.synchronize(dev)
-    for i in range(10):
-        launch(0, 1, lat_ev[i])
-        torch.cuda.synchronize(dev)
-    batch_ms = statistics.median(a.elapsed_time(b) for a, b in lat_ev)
+    def run(sizes_, evs=None):
+        first = 0
+        for i, kk in enumerate(sizes_):
+            launch(i, first, kk, evs[i] if evs else None)
+            first += kk
+        return first
 
-    launches = max(1, (args.steps + K - 1) // K)
-    steps = launches * K
-    # every stream's workspace is allocated by its first launch: warm all of them
-    for i in range(max(2 * F, args.warmup // K)):
-        launch(i)
-    torch.cuda.synchronize(dev)
+    # warmup: every stream's workspace is allocated by its first launch, at
+    # the largest launch size of the timed region
+    run(plan_launches(max(args.warmup, F * K), K, F))
+    sync(dev)
     if world > 1:
         dist.barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-    torch.cuda.synchronize(dev)
+    evs = [(Event(enable_timing=True), Event(enable_timing=True)) for _ in sizes]
+    sync(dev)
     t0 = time.perf_counter()
-    for i in range(launches):
-        launch(i, K, evs[i])
-    torch.cuda.synchronize(dev)
+    steps = run(sizes, evs)
+    sync(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
-    valid = [int((d_valid[f][j * n:(j + 1) * n] == 1).sum().item()) for f in range(min(F, launches)) for j in range(K)]
-    assert all(v == 9950 for v in valid), valid  # C2: 100 edge cases, 50 of them valid (factory.py)
+    # the last launch on each stream left its vectors: every C2 batch has its
+    # factory-known number of valid signatures (9,950 of 10k: 100 edge cases,
+    # 50 of them valid)
+    valid, first = [], 0
+    for i, kk in enumerate(sizes):
+        f = i % F
+        if i >= len(sizes) - F:
+            for j in range(kk):
+                v = int((d_valid[f][j * n:(j + 1) * n] == 1).sum().item())
+                assert v == expect_valid[(first + j) % R], (v, expect_valid[(first + j) % R])
+                valid.append(v)
+            if world > 1:  # the gathered vector holds every rank's copy of this launch
+                assert gathered[f].numel() == world * kk * n
+        first += kk
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    result = None
-    if rank == 0:
-        total = n * world * steps
-        value = total / elapsed
-        gpu_rate = n * steps / elapsed
+    extras = {}
+    if rank == 0 and not args.no_extras and not stub:
+        # one launch of K batches alone on one stream (no overlap): the
+        # pipeline's own duration, HIP events on its stream
+        alone = []
+        for _ in range(5):
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            launch(0, 0, K, e)
+            torch.cuda.synchronize(dev)
+            alone.append(e[0].elapsed_time(e[1]))
+        extras["launch_alone_ms"] = round(statistics.median(alone), 4)
+        # single-batch latency (one batch per launch, one at a time)
+        lat = []
+        for _ in range(12):
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            launch(0, 0, 1, e)
+            torch.cuda.synchronize(dev)
+            lat.append(e[0].elapsed_time(e[1]))
+        batch_ms = statistics.median(lat[2:])
+        extras["batch_latency_ms"] = round(batch_ms, 4)
+        extras["serial_verifies_per_s"] = round(n / (batch_ms * 1e-3), 1)
         # end-to-end through the host C-ABI (pinned staging, H2D, kernels,
         # D2H): the K batches of one launch as one host-resident batch
-        hb = Batch.concat(batches)
+        hb = Batch.concat(batches[:K])
         e2e = []
         for _ in range(5):
             t1 = time.perf_counter()
             ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, hb.pk, hb.sig, hb.msg, hb.off)
             e2e.append(time.perf_counter() - t1)
         e2e_rate = hb.n / statistics.median(e2e)
+        extras["end_to_end_verifies_per_s"] = round(e2e_rate, 1)
+        h2d = hb.pk.nbytes + hb.sig.nbytes + hb.msg.nbytes + hb.off.nbytes
+        extras["end_to_end_h2d_bytes_per_sig"] = round(h2d / hb.n, 1)
+        extras["end_to_end_h2d_GBps"] = round(h2d / statistics.median(e2e) / 1e9, 2)
+        extras["end_to_end_note"] = (f"{hb.n} host-resident signatures per call (pinned staging + PCIe + kernels + "
+                                     "D2H); never the headline value")
         # p50 / p99 of types.VerifyCommit on a 150-validator commit (C1): the
         # C++ L3 path (sign-bytes, tally, batch verifier, error mapping) +
         # H2D + GPU kernels + D2H, through tmv_verify_commit.
@@ -293,10 +430,18 @@ def main():
             lat.append((time.perf_counter() - t1) * 1e3)
             assert err is None
         lat.sort()
+        extras["verify_commit_150_p50_ms"] = round(lat[len(lat) // 2], 4)
+        extras["verify_commit_150_p99_ms"] = round(lat[int(len(lat) * 0.99) - 1], 4)
+        extras["verify_commit_note"] = "types.VerifyCommit (C1: 150 validators) via tmv_verify_commit, host-resident commit"
+
+    result = None
+    if rank == 0:
+        total = n * world * steps
+        value = total / elapsed
+        gpu_rate = n * steps / elapsed  # this rank
         peak = _load_peak()
-        # canonical work per launch of K batches / its average
-        # duration (HIP events on the launch stream)
-        achieved = n * K * MULS_PER_SIG / (launch_ms * 1e-3)
+        achieved = gpu_rate * MULS_PER_SIG
+        pmc = _load_pmc(args.method)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -311,37 +456,32 @@ def main():
             "dtype": "int32",
             "data": "synthetic (deterministic C2 generator, OpenSSL-signed commit-vote sign-bytes)",
             "config": {"workload": "C2: 10k ed25519 ZIP-215 batch, 1% corrupted/edge-case sigs (BASELINE configs[1])",
-                       "batch_per_step": n, "batches_per_launch": K, "launches_in_flight": F,
+                       "step": "one C2 batch (10,000 signatures) verified to its exact validity vector",
+                       "batch_per_step": n, "launch_sizes": sorted(set(sizes)), "launches": len(sizes),
+                       "launches_in_flight": F, "resident_batches": R,
                        "method": args.method, "msg_bytes_avg": round(float(batch.msg.size) / n, 1),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "valid_per_batch": valid[0],
-            "batch_latency_ms": round(batch_ms, 4),
-            "serial_verifies_per_s": round(n / (batch_ms * 1e-3), 1),
-            "end_to_end_verifies_per_s": round(e2e_rate, 1),
-            "end_to_end_note": f"{hb.n} host-resident signatures per call (pinned staging + PCIe + kernels + D2H)",
-            "verify_commit_150_p50_ms": round(lat[len(lat) // 2], 4),
-            "verify_commit_150_p99_ms": round(lat[int(len(lat) * 0.99) - 1], 4),
-            "verify_commit_note": "types.VerifyCommit (C1: 150 validators) via tmv_verify_commit, host-resident commit",
+            **extras,
             "roofline": {"bound": "valu-int-mul", "achieved": round(achieved / 1e12, 4),
                          "peak": round(peak / 1e12, 4), "unit": "Tmul/s", "frac": round(achieved / peak, 4),
-                         "traffic": _load_traffic(args.method) if K == 32 else None,
-                         "traffic_note": "HBM bytes per launch (PMC, profiles/r01_close/pmc_batch.json); algorithmic "
-                                         "input bytes per launch = 32 x 10k x ~222 B = 71 MB",
+                         "achieved_from": "verifies/s of this GPU over the timed region x 2.7e5 canonical int32 "
+                                          "products per verified signature (SURVEY 8(d): single-verify equivalent); "
+                                          "independent of how launches overlap",
+                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d))",
+                         "peak_from": "measured v_mad_i64_i32 rate, 16 waves/SIMD (tools/occbench.hip, "
+                                      "profiles/occbench_r01.json)",
                          "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if args.method == "batch"
                                     else "k_prep + k_verify_quad"),
                          "launch_avg_ms": round(launch_ms, 4),
-                         "aggregate_achieved": round(gpu_rate * MULS_PER_SIG / 1e12, 4),
-                         "aggregate_frac": round(gpu_rate * MULS_PER_SIG / peak, 4),
-                         "aggregate_note": f"{F} launches overlap, so each launch's own duration (above) is longer "
-                                           "than the timed span / launches; aggregate = verifies/s x 2.7e5",
-                         "achieved_from": f"{K} x {n} sigs x 2.7e5 canonical products / average launch "
-                                          "duration (HIP events on the launch stream)",
-                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d), single-verify equivalent)",
-                         "pmc_kernels": _pmc_kernels(args.method) if K == 32 else None,
-                         "pmc_note": "each kernel alone under --pmc: occupancy = mean resident waves per SIMD, "
-                                     "valu_issue_util = share of SIMD cycles issuing VALU (tools/pmc_derived.py)"},
+                         "traffic": pmc.get("hbm_bytes_per_step"),
+                         "traffic_note": pmc.get("note"),
+                         "executed": pmc.get("executed"),
+                         "pmc_kernels": _pmc_kernels(args.method)},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if stub:
+            result["data"] = "CPU STUB (--cpu-stub): control-flow check only, no verification, not a measurement"
+        if world == 1 and not args.no_cpu_baseline and not stub:
             result["cpu_baseline"] = cpu_baseline(batch)
         else:
             result["cpu_baseline"] = None

@@ -17,7 +17,8 @@
  *   TMV_ALL_VALID (1)   n > 0 and every entry verified
  *   TMV_NOT_ALL   (0)   some entry failed, or n == 0 (voi: an empty batch
  *                       verifies false)
- *   < 0                 infrastructure error (no device, allocation, launch);
+ *   < 0                 infrastructure error (no device, allocation, launch,
+ *                       TMV_ERR_TIMEOUT);
  *                       the validity vector is then unspecified and the
  *                       caller must not treat any entry as verified.
  */
@@ -37,6 +38,11 @@ extern "C" {
 #define TMV_ERR_NO_DEVICE (-2)
 #define TMV_ERR_NOMEM (-3)
 #define TMV_ERR_LAUNCH (-4)
+/* A device wait exceeded $TMV_DEVICE_TIMEOUT_MS (default 60000; 0 = wait
+ * forever).  The context's device work is then in an unknown state: the
+ * context refuses further work (every call returns TMV_ERR_TIMEOUT); the
+ * caller verifies on the CPU and may tmv_close / tmv_open a new context. */
+#define TMV_ERR_TIMEOUT (-5)
 
 /* Per-entry sr25519 status (tmv_sr25519_verify_batch, tmv_verify_mixed_batch):
  *   1 valid, 0 invalid, TMV_SR_ADDERR_* = BatchVerifier.Add would have

@@ -28,6 +28,7 @@
 #include "ed25519_core.h"
 #include "merlin_dev.h"
 #include "host/pool.h"
+#include "host/wait.h"
 #include "verify_kernels.h"
 #include "votes.h"
 #include "valset.h"
@@ -190,6 +191,9 @@ struct Device {
   // histograms of the key-merged form's counting sort
   std::vector<uint32_t> slots, key_count;
   std::mutex mu;
+  // a device wait timed out: its work is in an unknown state, so every later
+  // call on this device returns TMV_ERR_TIMEOUT (include/tmverify.h)
+  std::atomic<bool> faulted{false};
 };
 
 // Kernel choice: the quad (4 lanes / signature) path wins while the batch is
@@ -216,6 +220,8 @@ int g_zero_copy = 1;
 uint32_t g_host_chunk = 262144;
 // Lanes the chunks rotate over (TMV_HOST_LANES, 1..kLanes).
 uint32_t g_host_lanes = 2;
+// Bound on every wait for device work (TMV_DEVICE_TIMEOUT_MS, 0 = none).
+int64_t g_timeout_ms = 60000;
 
 void read_env() {
   static std::once_flag once;
@@ -237,7 +243,51 @@ void read_env() {
     if (hl) g_host_lanes = std::min<uint32_t>(kLanes, std::max<uint32_t>(1, (uint32_t)strtoul(hl, nullptr, 10)));
     const char *mc = getenv("TMV_MSM_CHUNK");
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
+    const char *to = getenv("TMV_DEVICE_TIMEOUT_MS");
+    if (to) g_timeout_ms = strtoll(to, nullptr, 10);
   });
+}
+
+// Bounded waits (host/wait.h).  hipErrorNotReady = timed out (the device is
+// then marked faulted); any other error is the device's.
+hipError_t wait_stream(Device &d, hipStream_t s) {
+  read_env();
+  hipError_t err = hipSuccess;
+  const tmh::Poll r = tmh::poll_until([&] {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorNotReady) return 1;
+    err = e;
+    return 2;
+  }, g_timeout_ms);
+  if (r == tmh::Poll::kTimeout) {
+    d.faulted = true;
+    set_error("device wait exceeded TMV_DEVICE_TIMEOUT_MS (" + std::to_string(g_timeout_ms) + " ms)");
+    return hipErrorNotReady;
+  }
+  return err;
+}
+hipError_t wait_event(Device &d, hipEvent_t ev) {
+  read_env();
+  hipError_t err = hipSuccess;
+  const tmh::Poll r = tmh::poll_until([&] {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorNotReady) return 1;
+    err = e;
+    return 2;
+  }, g_timeout_ms);
+  if (r == tmh::Poll::kTimeout) {
+    d.faulted = true;
+    set_error("device wait exceeded TMV_DEVICE_TIMEOUT_MS (" + std::to_string(g_timeout_ms) + " ms)");
+    return hipErrorNotReady;
+  }
+  return err;
+}
+int wait_rc(hipError_t e) { return e == hipErrorNotReady ? TMV_ERR_TIMEOUT : TMV_ERR_LAUNCH; }
+int faulted_rc(Device &d) {
+  set_error("device timed out earlier (TMV_ERR_TIMEOUT); open a new context");
+  return TMV_ERR_TIMEOUT;
 }
 
 // Batch-equation parameters for n entries.  Group size: the caller's, else
@@ -323,12 +373,14 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
   else o.batch_eq = g_msm_min > 0 && n >= g_msm_min;
   if (!o.batch_eq) return o;
   uint8_t key[32];
+  bool fixed;
   {
-    std::lock_guard<std::mutex> lk(ctx->opt_mu);
+    std::lock_guard<std::mutex> lk(ctx->opt_mu);  // tmv_set_batch_options writes these
     o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged);
-    if (ctx->fixed_seed) std::memcpy(key, ctx->seed, 32);
+    fixed = ctx->fixed_seed;
+    if (fixed) std::memcpy(key, ctx->seed, 32);
   }
-  if (!ctx->fixed_seed) {
+  if (!fixed) {
     size_t got = 0;
     while (got < 32) {  // the reference draws z from rand.Reader (crypto/ed25519/ed25519.go:232)
       const ssize_t r = getrandom(key + got, 32 - got, 0);
@@ -538,7 +590,10 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   if (n_miss == 0) return 0;
   // new keys may evict slots: let chunks still in flight on other lanes finish
   for (HostLane &l : d.lane)
-    if (l.n && l.stream != s) (void)hipStreamSynchronize(l.stream);
+    if (l.n && l.stream != s) {
+      const hipError_t we = wait_stream(d, l.stream);
+      if (we != hipSuccess) return wait_rc(we);
+    }
   // 3) misses.  First decide, before touching the index, whether the batch
   //    fits: bailing out after inserting keys whose tables were never built
   //    would leave stale entries behind.
@@ -589,7 +644,7 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     const size_t bytes = 32ull * m + 4ull * m + 64;
     if ((e = d.h_kbuild.ensure(bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
     if (bytes > d.d_kbuild.cap) {
-      (void)hipEventSynchronize(d.work_done);
+      if ((e = wait_event(d, d.work_done)) != hipSuccess) return wait_rc(e);
       if ((e = d.d_kbuild.ensure(bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
     }
     (void)hipStreamWaitEvent(s, d.work_done, 0);
@@ -608,7 +663,7 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     }
     // the pinned staging is reused by the next build: wait for this copy
     (void)hipEventRecord(d.work_done, s);
-    (void)hipEventSynchronize(d.work_done);
+    if ((e = wait_event(d, d.work_done)) != hipSuccess) return wait_rc(e);
   }
   return 0;
 }
@@ -629,8 +684,8 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
   const size_t msm_need = mp ? tmv::MsmWork::bytes(n, *mp) : 0;
   if (need > w.work.cap || (mixed && (need > w.work2.cap || idx_need > w.idx.cap)) || msm_need > w.msm.cap ||
       (mixed && msm_need > w.msm2.cap)) {
-    (void)hipEventSynchronize(w.done);  // old buffers may still be in use
-    hipError_t e;
+    hipError_t e = wait_event(d, w.done);  // old buffers may still be in use
+    if (e != hipSuccess) { *rc = wait_rc(e); return nullptr; }
     if ((e = w.work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
     if (mixed) {
       if ((e = w.work2.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work2)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
@@ -805,6 +860,7 @@ void tmv_close(tmv_ctx *ctx) {
   if (!ctx) return;
   for (auto &d : ctx->devs) {
     (void)hipSetDevice(d->id);
+    if (d->faulted) continue;  // work still running on its buffers: leak them rather than free them under it
     for (HostLane &l : d->lane) {
       if (l.stream) (void)hipStreamSynchronize(l.stream);
       l.d_in.release();
@@ -1054,6 +1110,8 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   std::vector<uint32_t> bounds(shards + 1);
   for (uint32_t s = 0; s <= shards; s++) bounds[s] = (uint32_t)((uint64_t)n * s / shards);
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
+  for (uint32_t s = 0; s < shards; s++)
+    if (ctx->devs[s]->faulted) return faulted_rc(*ctx->devs[s]);
   // each shard is cut into chunks of up to g_host_chunk entries, alternating
   // between the device's lanes
   read_env();
@@ -1072,8 +1130,11 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   EngineTimer tm;
   auto harvest = [&](Device &d, HostLane &ln) {
     if (ln.n == 0) return;
-    hipError_t e = hipStreamSynchronize(ln.stream);
-    if (e != hipSuccess && rc == 0) { set_error("hipStreamSynchronize", e); rc = TMV_ERR_LAUNCH; }
+    hipError_t e = wait_stream(d, ln.stream);
+    if (e != hipSuccess && rc == 0) {
+      if (e != hipErrorNotReady) set_error("hipStreamSynchronize", e);
+      rc = wait_rc(e);
+    }
     if (rc == 0) std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
     if (rc == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
     ln.n = 0;
@@ -1098,7 +1159,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     Device &d = *ctx->devs[s];
     (void)hipSetDevice(d.id);
     for (HostLane &ln : d.lane) {
-      if (rc != 0) { if (ln.n) (void)hipStreamSynchronize(ln.stream); ln.n = 0; continue; }
+      if (rc != 0) { if (ln.n && !d.faulted) (void)wait_stream(d, ln.stream); ln.n = 0; continue; }
       harvest(d, ln);
     }
   }
@@ -1226,6 +1287,7 @@ int64_t tmv_vote_sign_bytes_device(tmv_ctx *ctx, const tmv_vote_template *tmpl, 
   if (msg_cap < total) { set_error("msg_cap too small"); return TMV_ERR_ARG; }
   Device &d = *ctx->devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
+  if (d.faulted) return faulted_rc(d);
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   const size_t v_at = 0, t_at = align16(sizeof(tmv_vote) * n), o_at = t_at + align16(tab.size()),
@@ -1241,11 +1303,11 @@ int64_t tmv_vote_sign_bytes_device(tmv_ctx *ctx, const tmv_vote_template *tmpl, 
                                       reinterpret_cast<const uint32_t *>(dev + o_at), n, dev + m_at, d.stream)) !=
           hipSuccess ||
       (e = hipMemcpyAsync(msg_out, dev + m_at, total, hipMemcpyDeviceToHost, d.stream)) != hipSuccess ||
-      (e = hipStreamSynchronize(d.stream)) != hipSuccess) {
-    set_error("tmv_vote_sign_bytes_device", e);
-    rc = TMV_ERR_LAUNCH;
+      (e = wait_stream(d, d.stream)) != hipSuccess) {
+    if (e != hipErrorNotReady) set_error("tmv_vote_sign_bytes_device", e);
+    rc = wait_rc(e);
   }
-  (void)hipFree(dev);
+  if (!d.faulted) (void)hipFree(dev);
   return rc < 0 ? rc : (int64_t)total;
 }
 
@@ -1299,6 +1361,7 @@ int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kin
                                   int8_t *d_status, void *stream) {
   Device *dev = find_device(ctx, device);
   if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (dev->faulted) return faulted_rc(*dev);
   if (n == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
@@ -1314,6 +1377,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
                                const uint32_t *d_msg_off, uint32_t n, int8_t *d_status, void *stream) {
   Device *dev = find_device(ctx, device);
   if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (dev->faulted) return faulted_rc(*dev);
   if (n == 0) return TMV_NOT_ALL;
   if (key_kind == TMV_KIND_MIXED && !d_kind) { set_error("mixed batch without kinds"); return TMV_ERR_ARG; }
   if (key_kind > TMV_KIND_MIXED) { set_error("unsupported key kind"); return TMV_ERR_ARG; }
@@ -1334,6 +1398,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
                               const tmv_batch_ref *batches, uint32_t n_batches, void *stream) {
   Device *dev = find_device(ctx, device);
   if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (dev->faulted) return faulted_rc(*dev);
   if (key_kind != TMV_KIND_ED25519 && key_kind != TMV_KIND_SR25519) {
     set_error("tmv_verify_batches_device: key_kind must be ed25519 or sr25519");
     return TMV_ERR_ARG;
@@ -1373,7 +1438,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   Layout L(n, (size_t)M);
   const size_t need = L.total + align16(n);
   if (need > ws->gather.cap) {
-    (void)hipEventSynchronize(ws->done);
+    if ((e = wait_event(*dev, ws->done)) != hipSuccess) return wait_rc(e);
     if ((e = ws->gather.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(gather)", e); return TMV_ERR_NOMEM; }
   }
   uint8_t *g = static_cast<uint8_t *>(ws->gather.ptr);
@@ -1413,6 +1478,7 @@ int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key
     }
   Device &d = *ctx->devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
+  if (d.faulted) return faulted_rc(d);
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   // staging: power | set_off | pk | kind, then (device only) two node arrays and the roots
@@ -1421,7 +1487,7 @@ int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key
   const size_t o_na = in_bytes, o_nb = o_na + 32ull * n, o_out = o_nb + 32ull * n;
   const size_t dev_bytes = o_out + 32ull * n_sets;
   hipStream_t s = d.stream;
-  (void)hipStreamSynchronize(s);  // staging buffers may still feed an earlier call
+  if ((e = wait_stream(d, s)) != hipSuccess) return wait_rc(e);  // staging may still feed an earlier call
   if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   uint8_t *h = static_cast<uint8_t *>(d.h_valset.ptr);
@@ -1442,9 +1508,9 @@ int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key
                                 g + o_out, s);
   if (e != hipSuccess) { set_error("valset hash launch", e); return TMV_ERR_LAUNCH; }
   if ((e = hipMemcpyAsync(hash_out, g + o_out, 32ull * n_sets, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipStreamSynchronize(s)) != hipSuccess) {
-    set_error("valset hash readback", e);
-    return TMV_ERR_LAUNCH;
+      (e = wait_stream(d, s)) != hipSuccess) {
+    if (e != hipErrorNotReady) set_error("valset hash readback", e);
+    return wait_rc(e);
   }
   return 0;
 }
@@ -1470,6 +1536,7 @@ int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off
   if (n_leaves > (1u << 26) || bytes > (1u << 30)) { set_error("tmv_merkle_roots: input too large"); return TMV_ERR_ARG; }
   Device &d = *ctx->devs[0];
   std::lock_guard<std::mutex> lk(d.mu);
+  if (d.faulted) return faulted_rc(d);
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   // staging: leaf_off | tree_off | data, then (device only) two node arrays and the roots
@@ -1478,7 +1545,7 @@ int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off
   const size_t o_na = in_bytes, o_nb = o_na + 32ull * n_leaves, o_out = o_nb + 32ull * n_leaves;
   const size_t dev_bytes = o_out + 32ull * n_trees;
   hipStream_t s = d.stream;
-  (void)hipStreamSynchronize(s);  // the staging buffers are shared with tmv_validator_set_hashes
+  if ((e = wait_stream(d, s)) != hipSuccess) return wait_rc(e);  // staging shared with tmv_validator_set_hashes
   if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   uint8_t *h = static_cast<uint8_t *>(d.h_valset.ptr);
@@ -1496,9 +1563,9 @@ int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off
                                g + o_out, s);
   if (e != hipSuccess) { set_error("merkle launch", e); return TMV_ERR_LAUNCH; }
   if ((e = hipMemcpyAsync(hash_out, g + o_out, 32ull * n_trees, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-      (e = hipStreamSynchronize(s)) != hipSuccess) {
-    set_error("merkle readback", e);
-    return TMV_ERR_LAUNCH;
+      (e = wait_stream(d, s)) != hipSuccess) {
+    if (e != hipErrorNotReady) set_error("merkle readback", e);
+    return wait_rc(e);
   }
   return 0;
 }
@@ -1523,6 +1590,7 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
                                     void *stream) {
   Device *dev = find_device(ctx, device);
   if (!dev) { set_error("device not in context"); return TMV_ERR_ARG; }
+  if (dev->faulted) return faulted_rc(*dev);
   if (n == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }

@@ -43,9 +43,27 @@ def unpack_bits(bits: torch.Tensor, n: int) -> torch.Tensor:
     return v.reshape(-1)[:n].to(torch.uint8)
 
 
+def all_gather_statuses(status_local: torch.Tensor, counts: List[int], group=None) -> torch.Tensor:
+    """Gather every rank's int8 status vector unpacked (n bytes): sr25519 and
+    mixed batches, whose statuses -1 / -2 are deferred BatchVerifier.Add
+    errors (crypto/sr25519/batch.go:30-37) that verifyCommitBatch returns
+    verbatim (types/validation.go:211-213) — a bitmap would turn them into
+    plain invalid signatures."""
+    world = len(counts)
+    m = max(counts)
+    st = status_local.reshape(-1).to(torch.int8)
+    if st.numel() < m:
+        st = torch.nn.functional.pad(st, (0, m - st.numel()))
+    out = [torch.empty(m, dtype=torch.int8, device=st.device) for _ in range(world)]
+    dist.all_gather(out, st, group=group)
+    return torch.cat([out[r][:counts[r]] for r in range(world)])
+
+
 def all_gather_validity(valid_local: torch.Tensor, counts: List[int], group=None) -> torch.Tensor:
-    """Gather every rank's validity vector (counts[r] entries on rank r) and
-    return the full Add-order vector on every rank."""
+    """Gather every rank's validity vector (counts[r] entries on rank r) as
+    packed bitmaps (n/8 bytes) and return the full Add-order 0/1 vector on
+    every rank.  ed25519 batches only: use all_gather_statuses where an entry
+    can carry a negative (Add-error) status."""
     world = len(counts)
     nbytes = (max(counts) + 7) // 8
     bits = pack_bits(valid_local)

@@ -111,6 +111,18 @@ class Batch:
         off[1:] = np.cumsum(lens)
         return Batch(pk, sig, msg, off, [k for b in batches for k in b.kinds])
 
+    def take(self, idx) -> "Batch":
+        """Entries idx[0], idx[1], ... (any order, repeats allowed), vectorised."""
+        idx = np.asarray(idx, np.int64)
+        lens = (self.off[1:] - self.off[:-1]).astype(np.int64)[idx]
+        off = np.zeros(len(idx) + 1, np.uint32)
+        off[1:] = np.cumsum(lens)
+        starts = self.off[:-1].astype(np.int64)[idx]
+        pos = np.arange(int(off[-1]), dtype=np.int64) - np.repeat(off[:-1].astype(np.int64), lens) + \
+            np.repeat(starts, lens)
+        return Batch(self.pk.reshape(-1, 32)[idx].reshape(-1), self.sig.reshape(-1, 64)[idx].reshape(-1),
+                     self.msg[pos] if len(pos) else np.zeros(0, np.uint8), off, [self.kinds[i] for i in idx])
+
     def tile(self, n: int) -> "Batch":
         """Repeat entries cyclically up to n (throughput runs on >10k)."""
         idx = np.arange(n) % self.n

@@ -15,7 +15,8 @@ from tendermint_amd.types.canonical import (BlockID as PyBlockID, PartSetHeader,
                                             PRECOMMIT_TYPE)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CHECK_SO = os.path.join(REPO, "oracle", "_build", "libcommitcheck.so")
+# TMV_COMMITCHECK_SO: another build of the harness (the ASan/UBSan one, tests/test_sanitizers.py)
+CHECK_SO = os.environ.get("TMV_COMMITCHECK_SO", os.path.join(REPO, "oracle", "_build", "libcommitcheck.so"))
 
 
 def make_block_id(hash_: bytes, total: int, psh: bytes) -> H.BlockID:
@@ -78,7 +79,8 @@ class FakeBackend:
 
     def __init__(self):
         import subprocess
-        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "native")], check=True)
+        if "TMV_COMMITCHECK_SO" not in os.environ:
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "native")], check=True)
         self.L = ctypes.CDLL(CHECK_SO)
         self.L.commitcheck_verify_commit.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(H.CValidator),
                                                      ctypes.c_uint32, ctypes.c_int32, ctypes.POINTER(H.CBlockID),

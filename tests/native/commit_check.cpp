@@ -7,6 +7,7 @@
 // the C oracle (oracle/c, linked as liboracle.so: test infrastructure) so the
 // reference's own signed fixtures (light/mbt) run through the product's host
 // code on the CPU.
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -15,6 +16,7 @@
 #include "../../include/tmhost.h"
 #include "../../include/tmverify.h"
 #include "../../tendermint_amd/csrc/host/tm_light.h"
+#include "../../tendermint_amd/csrc/host/wait.h"
 #include "../../tendermint_amd/csrc/host/tm_types.h"
 #include "../../tendermint_amd/csrc/sha512_dev.h"
 
@@ -72,11 +74,29 @@ extern "C" {
 int commitcheck_backend_calls = 0;
 int commitcheck_entries_verified = 0;
 int g_skip_hash = 0;  // timing of the host layer alone (tools only)
+int g_fail_next = 0;  // the next device call returns this infrastructure error (e.g. TMV_ERR_TIMEOUT)
+
+void commitcheck_fail_next(int rc) { g_fail_next = rc; }
+
+// tmh::poll_until (host/wait.h, the runtime's bounded device waits) against a
+// query that completes after `ready_after` polls (< 0: never) or fails.
+int commitcheck_poll(int ready_after, int fail, int64_t timeout_ms, double *elapsed_ms) {
+  int polls = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  const tmh::Poll r = tmh::poll_until([&] {
+    polls++;
+    if (fail) return 2;
+    return ready_after >= 0 && polls > ready_after ? 0 : 1;
+  }, timeout_ms);
+  *elapsed_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return (int)r;
+}
 
 const char *tmv_last_error(void) { return "fake device error"; }
 
 int tmv_verify_batch_ex(tmv_ctx *, uint8_t key_kind, uint32_t, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
+  if (g_fail_next) { const int rc = g_fail_next; g_fail_next = 0; return rc; }
   commitcheck_backend_calls++;
   commitcheck_entries_verified += (int)n;
   const Bytes dummy_pk;
@@ -118,6 +138,7 @@ static Bytes vote_message(const tmv_vote_template &t, const tmv_vote &v) {
 
 int tmv_verify_votes(tmv_ctx *, uint8_t key_kind, uint32_t, const tmv_vote_template *tmpl, uint32_t n_tmpl,
                      const tmv_vote *votes, const uint8_t *pk, const uint8_t *sig, uint32_t n, int8_t *status_out) {
+  if (g_fail_next) { const int rc = g_fail_next; g_fail_next = 0; return rc; }
   commitcheck_backend_calls++;
   commitcheck_entries_verified += (int)n;
   bool all = n > 0;

@@ -87,3 +87,53 @@ def test_all_gather_statuses_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == [(0, True, 6006), (1, True, 6006)]
+
+
+def _sr_status_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tendermint_amd.shard import all_gather_statuses
+    counts = [1001, 998]
+    g = torch.Generator().manual_seed(7)
+    full = torch.randint(-2, 2, (sum(counts),), generator=g, dtype=torch.int8)
+    lo = sum(counts[:rank])
+    got = all_gather_statuses(full[lo:lo + counts[rank]].clone(), counts)
+    q.put((rank, bool(torch.equal(got, full)), int((got < 0).sum())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_gather_sr25519_statuses_world2():
+    """sr25519 Add-error statuses (-1 / -2) survive the gather
+    (uneven shards)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sr_status_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert [r[:2] for r in res] == [(0, True), (1, True)] and res[0][2] > 0
+
+
+def test_bench_control_flow_world2():
+    """bench.py's --gpus N path (one process per rank via torch.distributed.run,
+    launches over streams, one validity all-gather per launch, barrier + MAX
+    timing, rank 0's JSON line) executed with gloo and the --cpu-stub engine."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"), "--gpus", "2",
+           "--steps", "7", "--warmup", "2", "--batch", "500", "--resident", "3", "--inflight", "2", "--cpu-stub"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=repo)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
+    assert r["config"]["parallelism"] == "shard2" and sum(r["config"]["launch_sizes"]) >= 1
+    assert "STUB" in r["data"]
