@@ -135,6 +135,40 @@ typedef struct {
 int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                        size_t err_stride);
 
+/* ---- consensus votes (ADR-064 batched vote verification) ---- */
+/* The parts of a types.Vote (types/vote.go:50-62) Vote.Verify reads, with
+ * the signing validator's public key (val.PubKey, looked up by the caller
+ * from ValidatorIndex as VoteSet.addVote does, types/vote_set.go:183-199). */
+typedef struct {
+  int32_t type; /* SignedMsgType: 1 prevote, 2 precommit */
+  int64_t height;
+  int32_t round;
+  const tmv_block_id *block_id; /* NULL (or a nil BlockID) = vote for nil */
+  int64_t ts_seconds;
+  int32_t ts_nanos;
+  const uint8_t *validator_address;
+  uint32_t validator_address_len;
+  const uint8_t *signature;
+  uint32_t signature_len;
+  uint8_t key_kind; /* TMV_KIND_ED25519 / TMV_KIND_SR25519 */
+  const uint8_t *pub_key;
+  uint32_t pub_key_len;
+} tmv_vote_in;
+
+#define TMV_VOTE_OK 0
+#define TMV_VOTE_ERR_INVALID_ADDRESS 1   /* types.ErrVoteInvalidValidatorAddress */
+#define TMV_VOTE_ERR_INVALID_SIGNATURE 2 /* types.ErrVoteInvalidSignature */
+
+/* Vote.Verify(chainID, pubKey) (types/vote.go:226-243: address check, then
+ * PubKey.VerifySignature over VoteSignBytes) of n votes in ONE signature
+ * batch: the batched vote verification ADR-064 describes for consensus
+ * (docs/architecture/adr-064-batch-verification.md:58-64: once 2/3+ of the
+ * votes have arrived they are verified together).  results[i] = TMV_VOTE_*,
+ * identical to verifying vote i alone.  Returns the number of failed votes,
+ * or < 0 on an infrastructure error. */
+int tmv_verify_vote_batch(tmv_ctx *ctx, const char *chain_id, const tmv_vote_in *votes, uint32_t n,
+                          int32_t *results);
+
 /* ---- light client (light/verifier.go) ---- */
 typedef struct {
   const uint8_t *p;

@@ -49,7 +49,7 @@ EXPORTS = [
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_vote_template_encode", "tmv_verify_commit", "tmv_verify_commits",
-    "tmv_header_hashes", "tmv_light_verify_many", "tmv_light_verify",
+    "tmv_header_hashes", "tmv_light_verify_many", "tmv_light_verify", "tmv_verify_vote_batch",
 ]
 
 

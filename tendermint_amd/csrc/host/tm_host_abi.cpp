@@ -19,6 +19,7 @@
 #include "../../../include/tmverify.h"
 #include "pool.h"
 #include "tm_host_internal.h"
+#include "tm_light.h"
 #include "tm_types.h"
 
 namespace tmh_internal {
@@ -578,6 +579,59 @@ extern "C" {
 int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                        size_t err_stride) {
   return verify_commits(ctx, jobs, n_jobs, results, errs, err_stride, nullptr);
+}
+
+int tmv_verify_vote_batch(tmv_ctx *ctx, const char *chain_id, const tmv_vote_in *votes, uint32_t n,
+                          int32_t *results) {
+  if (!ctx || (n && (!votes || !results))) return TMV_ERR_ARG;
+  const std::string chain = chain_id ? chain_id : "";
+  // address check (pubKey.Address() == vote.ValidatorAddress, crypto.AddressHash
+  // = SHA-256(pub key)[:20]), then one batch per key kind over the votes'
+  // canonical sign-bytes; VerifySignature semantics: a wrong signature length
+  // or an undecodable sr25519 key / signature is an invalid signature.
+  std::vector<uint8_t> kind(n, 2);
+  parallel_for(n, 256, [&](size_t i) {
+    const tmv_vote_in &v = votes[i];
+    uint32_t st[8];
+    static const uint8_t none = 0;
+    tmh::Sha256Bytes(st, nullptr, 0, v.pub_key ? v.pub_key : &none, v.pub_key_len);
+    uint8_t addr[20];
+    for (int k = 0; k < 20; k++) addr[k] = (uint8_t)(st[k / 4] >> (24 - 8 * (k % 4)));
+    const bool addr_ok = v.validator_address_len == 20 && v.validator_address &&
+                         std::memcmp(addr, v.validator_address, 20) == 0;
+    if (!addr_ok) { results[i] = TMV_VOTE_ERR_INVALID_ADDRESS; return; }
+    results[i] = TMV_VOTE_ERR_INVALID_SIGNATURE;
+    if (v.pub_key_len != 32 || v.signature_len != 64 || !v.signature) return;
+    if (v.key_kind == TMV_KIND_ED25519 || v.key_kind == TMV_KIND_SR25519) kind[i] = v.key_kind;
+  });
+  for (uint8_t k = 0; k < 2; k++) {
+    std::vector<uint32_t> idx;
+    for (uint32_t i = 0; i < n; i++)
+      if (kind[i] == k) idx.push_back(i);
+    if (idx.empty()) continue;
+    const size_t m = idx.size();
+    std::vector<uint8_t> pk(32 * m), sig(64 * m), msg;
+    std::vector<uint32_t> off(m + 1, 0);
+    std::vector<tmh::BlockID> bids(m);
+    for (size_t t = 0; t < m; t++) {
+      const tmv_vote_in &v = votes[idx[t]];
+      std::memcpy(&pk[32 * t], v.pub_key, 32);
+      std::memcpy(&sig[64 * t], v.signature, 64);
+      if (v.block_id) bids[t] = block_id_of(*v.block_id);
+      tmh::AppendVoteSignBytes(msg, chain, v.type, v.height, v.round, v.block_id ? &bids[t] : nullptr,
+                               tmh::Timestamp{v.ts_seconds, v.ts_nanos});
+      off[t + 1] = (uint32_t)msg.size();
+    }
+    std::vector<int8_t> st(m);
+    const int rc = tmv_verify_batch_ex(ctx, k, TMV_FLAG_KEY_CACHE, pk.data(), sig.data(), msg.data(), off.data(),
+                                       (uint32_t)m, st.data());
+    if (rc < 0) return rc;
+    for (size_t t = 0; t < m; t++)
+      if (st[t] == 1) results[idx[t]] = TMV_VOTE_OK;
+  }
+  int bad = 0;
+  for (uint32_t i = 0; i < n; i++) bad += results[i] != TMV_VOTE_OK;
+  return bad;
 }
 
 int tmv_verify_commit(tmv_ctx *ctx, int mode, const char *chain_id, const tmv_validator *vals, uint32_t n_vals,

@@ -661,3 +661,61 @@ def header_hashes(ctx, headers: List[Header]) -> List[Optional[bytes]]:
     """Header.Hash of each header (None where the reference returns nil)."""
     L = _setup_light(_setup(_native.lib()))
     return header_hashes_call(L.tmv_header_hashes, ctx.handle, headers)
+
+
+# ---------------------------------------------------------------- consensus votes (ADR-064)
+VOTE_OK, VOTE_ERR_INVALID_ADDRESS, VOTE_ERR_INVALID_SIGNATURE = 0, 1, 2
+PREVOTE_TYPE, PRECOMMIT_TYPE = 1, 2
+
+
+class CVoteIn(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("height", ctypes.c_int64), ("round", ctypes.c_int32),
+                ("block_id", ctypes.POINTER(CBlockID)), ("ts_seconds", ctypes.c_int64), ("ts_nanos", ctypes.c_int32),
+                ("validator_address", _u8p), ("validator_address_len", ctypes.c_uint32),
+                ("signature", _u8p), ("signature_len", ctypes.c_uint32), ("key_kind", ctypes.c_uint8),
+                ("pub_key", _u8p), ("pub_key_len", ctypes.c_uint32)]
+
+
+@dataclass
+class Vote:
+    """types.Vote (types/vote.go:50-62), the fields consensus votes carry."""
+    type: int
+    height: int
+    round: int
+    block_id: BlockID
+    timestamp: Tuple[int, int]
+    validator_address: bytes
+    validator_index: int
+    signature: bytes = b""
+
+
+def verify_vote_batch_call(fn, ctx_handle, chain_id: str, votes: List[Vote], keys: List[Tuple[int, bytes]]
+                           ) -> List[int]:
+    """votes[i] checked against keys[i] = (key kind, public key); fn =
+    tmv_verify_vote_batch (or the CPU harness's twin).  Returns TMV_VOTE_* per vote."""
+    k = _Keep()
+    arr = (CVoteIn * max(1, len(votes)))()
+    for i, (v, (kind, pk)) in enumerate(zip(votes, keys)):
+        bid = None
+        if v.block_id is not None and (v.block_id.hash or v.block_id.psh_total or v.block_id.psh_hash):
+            b = _c_block_id(k, v.block_id)
+            k.refs.append(b)
+            bid = ctypes.pointer(b)
+        a, al = k.buf(v.validator_address)
+        s, sl = k.buf(v.signature)
+        p, pl = k.buf(pk)
+        arr[i] = CVoteIn(v.type, v.height, v.round, bid, v.timestamp[0], v.timestamp[1], a, al, s, sl, kind, p, pl)
+    res = (ctypes.c_int32 * max(1, len(votes)))()
+    rc = fn(ctx_handle, chain_id.encode(), arr, len(votes), res)
+    if rc < 0:
+        raise NativeError(f"tmv_verify_vote_batch failed ({rc}): {_native.last_error()}")
+    return [res[i] for i in range(len(votes))]
+
+
+def verify_vote_batch(ctx, chain_id: str, votes: List[Vote], keys: List[Tuple[int, bytes]]) -> List[int]:
+    L = _setup(_native.lib())
+    if not getattr(L, "_tmhost_votes", False):
+        L.tmv_verify_vote_batch.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(CVoteIn),
+                                            ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]
+        L._tmhost_votes = True
+    return verify_vote_batch_call(L.tmv_verify_vote_batch, ctx.handle, chain_id, votes, keys)

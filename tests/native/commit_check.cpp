@@ -189,6 +189,11 @@ void commitcheck_set_real_signatures(int on) { g_real = on; }
 
 tmv_ctx *commitcheck_ctx(void) { return &g_ctx; }
 
+int commitcheck_verify_vote_batch(tmv_ctx *, const char *chain_id, const tmv_vote_in *votes, uint32_t n,
+                                  int32_t *results) {
+  return tmv_verify_vote_batch(&g_ctx, chain_id, votes, n, results);
+}
+
 int commitcheck_light_verify_many(const tmv_light_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                                   size_t err_stride) {
   return tmv_light_verify_many(&g_ctx, jobs, n_jobs, results, errs, err_stride);

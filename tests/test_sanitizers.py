@@ -11,7 +11,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SUITES = ["tests/test_commit_verify.py", "tests/test_light_mbt.py", "tests/test_batch_verifier.py",
-          "tests/test_failure_handling.py", "tests/test_chains.py"]
+          "tests/test_failure_handling.py", "tests/test_chains.py", "tests/test_vote_set.py"]
 
 
 def _runtime(name):
