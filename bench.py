@@ -258,6 +258,8 @@ def main():
     ap.add_argument("--per-launch", type=int, default=0,
                     help="batches per pipeline launch (tmv_verify_batches_device, <= 32); 0 = auto")
     ap.add_argument("--inflight", type=int, default=4, help="launches in flight (streams)")
+    ap.add_argument("--plan", default="", help="explicit launch sizes, comma separated (sum = --steps); "
+                                                "overrides --per-launch")
     ap.add_argument("--resident", type=int, default=32, help="distinct C2 batches held in HBM per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / end-to-end / C1 measurements")
@@ -278,6 +280,9 @@ def main():
     F = max(1, args.inflight)
     R = max(1, min(64, args.resident))
     sizes = plan_launches(max(1, args.steps), args.per_launch, F)
+    if args.plan:
+        sizes = [int(x) for x in args.plan.split(",")]
+        assert sum(sizes) == args.steps and all(0 < x <= 32 for x in sizes), (sizes, args.steps)
     K = max(sizes)
     # R distinct C2 batches per rank (own keys / messages), generated on the
     # host before this process touches the GPU (worker processes are forked)
@@ -462,7 +467,7 @@ def main():
             "data": "synthetic (deterministic C2 generator, OpenSSL-signed commit-vote sign-bytes)",
             "config": {"workload": "C2: 10k ed25519 ZIP-215 batch, 1% corrupted/edge-case sigs (BASELINE configs[1])",
                        "step": "one C2 batch (10,000 signatures) verified to its exact validity vector",
-                       "batch_per_step": n, "launch_sizes": sorted(set(sizes)), "launches": len(sizes),
+                       "batch_per_step": n, "launch_sizes": sizes, "launches": len(sizes),
                        "launches_in_flight": F, "resident_batches": R,
                        "method": args.method, "msg_bytes_avg": round(float(batch.msg.size) / n, 1),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
