@@ -98,7 +98,8 @@ template <bool SR, bool KM, int BS = kMsmSortBlock>
 __global__ void __launch_bounds__(BS)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
            Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned,
-           const uint32_t *__restrict__ key_slot, const uint8_t *__restrict__ key_ok, uint8_t *__restrict__ out) {
+           const uint32_t *__restrict__ key_slot, const uint8_t *__restrict__ key_ok, uint8_t *__restrict__ out,
+           uint32_t e_base) {
   extern __shared__ uint32_t smem[];
   const uint32_t cnt = entry_count(count_ptr, n);
   const uint32_t g = blockIdx.x;
@@ -163,7 +164,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     }
     live[r] = true;
     uint32_t blk[16];
-    chacha20_block(blk, seed.key, e, seed.nonce);
+    chacha20_block(blk, seed.key, e_base + e, seed.nonce);  // counter = the entry's index in the whole launch
 #pragma unroll
     for (int t = 0; t < 4; t++) z[r][t] = blk[t];
     uint32_t k[8];
@@ -733,14 +734,46 @@ bool subcheck_enabled(uint32_t m_log2) {
   return mode < 0 ? m_log2 >= 8 : mode == 1;
 }
 
+// Views of a launch's work arrays for the entries of groups [g0, ...): the
+// throughput stages of one part of a split launch run on these exactly as on
+// a whole batch (indices inside a view are relative), and the whole-launch
+// stages (Horner, fallback) read the same arrays through the full structs.
+static Ed25519Work work_view(Ed25519Work w, uint64_t e0) {
+  w.negA += 4 * e0;
+  w.Rc += 4 * e0;
+  w.k += 8 * e0;
+  w.flags += 4 * e0;
+  w.tabA += 32 * e0;
+  return w;
+}
+static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0) {
+  const uint64_t e0 = g0 << p.m_log2, wh = (uint64_t)p.W * p.H;
+  mw.pts += 2 * e0;
+  mw.n_pts = (uint32_t)(2ull * n - 2 * e0);  // B keeps the launch's slot 2n
+  mw.ent_pt += g0 * p.cap;
+  mw.ent_bk += g0 * p.cap;
+  mw.bk_start += g0 * wh;
+  mw.bk_cnt += g0 * wh;
+  mw.bk_sum += g0 * wh;
+  mw.part_first += g0 * p.chunks_per_group();
+  mw.part_last += g0 * p.chunks_per_group();
+  mw.wpart += g0 * p.W * 2ull * p.P;
+  mw.wsum += g0 * p.W;
+  mw.group_ok += g0;
+  if (mw.sub_ok) mw.sub_ok += (g0 << p.m_log2) / kSubGroup;
+  if (mw.tabR) mw.tabR += 32 * e0;
+  return mw;
+}
+
+// Throughput stages (prep, sort, bucket sums, window sums) of entries
+// [e_base, e_base + n) of a launch; w / mw / out / pk / sig / msg_off are
+// already offset to the part.
 template <bool SR>
-static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                               const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const fe *btab_q,
-                               const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
-                               const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
-  const bool compact = fallback_compact();
+static hipError_t launch_part(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                              const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, uint32_t e_base,
+                              const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned, bool compact,
+                              hipStream_t stream) {
   w.niels = mw.pts;
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
@@ -749,14 +782,54 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   if (p.m_log2 <= 8 && sort_block() == 64) {
     const size_t smem = ((size_t)p.W * p.H + 64 * 9 + 64 + 1) * sizeof(uint32_t);
     hipLaunchKernelGGL((k_msm_sort<SR, false, 64>), dim3(p.groups), dim3(64), smem, stream, sig, idx, count_ptr, n,
-                       w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr);
+                       w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr, e_base);
   } else {
     const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
     hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx,
-                       count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr);
+                       count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr,
+                       e_base);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = launch_buckets(count_ptr, n, mw, p, stream)) != hipSuccess) return e;
+  return launch_buckets(count_ptr, n, mw, p, stream);
+}
+
+template <bool SR>
+static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                               const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const fe *btab_q,
+                               const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                               const MsmSeed &seed, uint8_t *out, hipStream_t stream, const SplitStreams *split) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  const bool compact = fallback_compact();
+  w.niels = mw.pts;
+  hipError_t e;
+  // Split launch: the groups' first and second halves run their throughput
+  // stages on two streams at once (the caller's and a helper forked from
+  // it), then join for one Horner and one fallback over all groups -- two
+  // concurrent halves fill each other's wave-quantisation gaps, and the
+  // launch keeps a single latency tail.  Contiguous batches only.
+  const uint32_t g0 = (p.groups + 1) / 2;
+  const uint64_t e0 = (uint64_t)g0 << p.m_log2;
+  if (split && !idx && !count_ptr && g0 > 0 && e0 < n) {
+    MsmParams p0 = p, p1 = p;
+    p0.groups = g0;
+    p1.groups = p.groups - g0;
+    if ((e = hipEventRecord(split->fork, stream)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(split->helper, split->fork, 0)) != hipSuccess) return e;
+    e = launch_part<SR>(pk, sig, msg, msg_off, nullptr, nullptr, (uint32_t)e0, 0u, btab_q, prefix, w, mw, p0, seed,
+                        out, aligned, compact, stream);
+    if (e != hipSuccess) return e;
+    e = launch_part<SR>(pk + 32 * e0, sig + 64 * e0, msg, msg_off + e0, nullptr, nullptr, (uint32_t)(n - e0),
+                        (uint32_t)e0, btab_q, prefix, work_view(w, e0), msm_view(mw, p, n, g0), p1, seed,
+                        out ? out + e0 : nullptr, aligned, compact, split->helper);
+    if (e != hipSuccess) return e;
+    if ((e = hipEventRecord(split->join, split->helper)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(stream, split->join, 0)) != hipSuccess) return e;
+  } else {
+    e = launch_part<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, 0u, btab_q, prefix, w, mw, p, seed, out, aligned,
+                        compact, stream);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
                      nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -851,7 +924,7 @@ static hipError_t launch_km(const uint8_t *pk, const uint8_t *sig, const uint8_t
   if (e != hipSuccess) return e;
   const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
   hipLaunchKernelGGL((k_msm_sort<SR, true>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, runs.order, nullptr,
-                     n, w, mw, p, seed, nullptr, aligned, key_slot, kt.ok, nullptr);
+                     n, w, mw, p, seed, nullptr, aligned, key_slot, kt.ok, nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = launch_buckets(nullptr, n, mw, p, stream)) != hipSuccess) return e;
   const uint32_t n_items = runs.n_runs + p.groups;
@@ -875,9 +948,13 @@ hipError_t launch_key_merged_check(bool sr, const uint8_t *pk, const uint8_t *si
 hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                               const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                               const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
-                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
-  if (sr) return launch_check<true>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream);
-  return launch_check<false>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream);
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream,
+                              const SplitStreams *split) {
+  if (sr)
+    return launch_check<true>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream,
+                              split);
+  return launch_check<false>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream,
+                             split);
 }
 
 hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
@@ -891,10 +968,10 @@ hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, cons
   hipError_t e = launch_partition(kind, n, counts, idx_ed, idx_sr, out, stream);
   if (e != hipSuccess) return e;
   e = launch_check<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, m_ed, p, seed_ed, out,
-                          stream);
+                          stream, nullptr);
   if (e != hipSuccess) return e;
   return launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p, seed_sr,
-                            out, stream);
+                            out, stream, nullptr);
 }
 
 }  // namespace tmv

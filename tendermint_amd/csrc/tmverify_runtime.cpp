@@ -144,6 +144,9 @@ struct KeyIndex {
 struct Workspace {
   DeviceBuf work, work2, idx, msm, msm2, gather;
   hipEvent_t done = nullptr;
+  // helper stream + fork/join events of split batch-equation launches
+  // (created on first use)
+  tmv::SplitStreams split{nullptr, nullptr, nullptr};
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
   const uint8_t *sub_ok[2] = {nullptr, nullptr};  // sub-group verdicts (k_msm_subcheck), if it ran
@@ -222,6 +225,10 @@ uint32_t g_host_chunk = 262144;
 uint32_t g_host_lanes = 2;
 // Bound on every wait for device work (TMV_DEVICE_TIMEOUT_MS, 0 = none).
 int64_t g_timeout_ms = 60000;
+// Batch-equation launches of at least this many contiguous entries run
+// their throughput stages as two concurrent halves (tmv::SplitStreams) and
+// keep one latency tail (TMV_SPLIT_MIN, 0 = never).
+uint32_t g_split_min = 0;
 
 void read_env() {
   static std::once_flag once;
@@ -245,6 +252,8 @@ void read_env() {
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
     const char *to = getenv("TMV_DEVICE_TIMEOUT_MS");
     if (to) g_timeout_ms = strtoll(to, nullptr, 10);
+    const char *sm = getenv("TMV_SPLIT_MIN");
+    if (sm) g_split_min = (uint32_t)strtoul(sm, nullptr, 10);
   });
 }
 
@@ -711,8 +720,17 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   if (!ws) return rc;
   tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
   tmv::MsmWork mw = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
+  read_env();
+  const tmv::SplitStreams *split = nullptr;
+  if (g_split_min && n >= g_split_min) {
+    tmv::SplitStreams &sp = ws->split;
+    if (!sp.helper && hipStreamCreateWithFlags(&sp.helper, hipStreamNonBlocking) != hipSuccess) sp.helper = nullptr;
+    if (sp.helper && !sp.fork && hipEventCreateWithFlags(&sp.fork, hipEventDisableTiming) != hipSuccess) sp.fork = nullptr;
+    if (sp.helper && !sp.join && hipEventCreateWithFlags(&sp.join, hipEventDisableTiming) != hipSuccess) sp.join = nullptr;
+    if (sp.helper && sp.fork && sp.join) split = &sp;  // else: one stream
+  }
   hipError_t e = tmv::launch_batch_check(sr, pk, sig, msg, off, nullptr, nullptr, n, d.d_btab_q, d.d_prefix, w, mw,
-                                         o.p, o.seed[sr ? 1 : 0], out, s);
+                                         o.p, o.seed[sr ? 1 : 0], out, s, split);
   if (e != hipSuccess) { set_error("batch check launch", e); return TMV_ERR_LAUNCH; }
   ws->group_ok[0] = mw.group_ok;
   ws->group_ok[1] = nullptr;
@@ -877,6 +895,11 @@ void tmv_close(tmv_ctx *ctx) {
       kv.second->msm2.release();
       kv.second->gather.release();
       if (kv.second->done) (void)hipEventDestroy(kv.second->done);
+      const tmv::SplitStreams &sp = kv.second->split;
+      if (sp.helper) (void)hipStreamSynchronize(sp.helper);
+      if (sp.fork) (void)hipEventDestroy(sp.fork);
+      if (sp.join) (void)hipEventDestroy(sp.join);
+      if (sp.helper) (void)hipStreamDestroy(sp.helper);
     }
     d->ws.clear();
     d->d_kbuild.release();
@@ -1414,6 +1437,10 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
     const tmv_batch_ref &x = batches[b];
     if (x.n && (!x.pk || !x.sig || !x.msg_off || !x.status || (!x.msg && x.msg_bytes))) {
       set_error("tmv_verify_batches_device: null pointer in a non-empty batch");
+      return TMV_ERR_ARG;
+    }
+    if (!x.n && x.msg_bytes) {
+      set_error("tmv_verify_batches_device: message bytes in an empty batch");
       return TMV_ERR_ARG;
     }
     r.pk[b] = x.pk; r.sig[b] = x.sig; r.msg[b] = x.msg; r.off[b] = x.msg_off; r.out[b] = x.status;

@@ -68,10 +68,18 @@ hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uin
 // Batch-equation pipeline (msm.h): k_prep -> k_msm_sort -> k_msm_accum ->
 // k_msm_group -> k_verify_quad over the failed groups only.  Single key kind
 // (sr = false: ed25519, true: sr25519); idx/count_ptr as for the mixed path.
+// split (optional, contiguous batches): a helper stream and two events; the
+// two halves of the groups run their throughput stages concurrently, forked
+// from and joined back into `stream`, before one Horner and one fallback.
+struct SplitStreams {
+  hipStream_t helper;
+  hipEvent_t fork, join;
+};
 hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                               const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                               const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
-                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream);
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream,
+                              const SplitStreams *split = nullptr);
 // Mixed batch through the batch equation: partition, then one pipeline per kind.
 hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                     const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,

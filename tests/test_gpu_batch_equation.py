@@ -220,14 +220,15 @@ def test_device_resident_entry_point(bctx):
 @pytest.mark.parametrize("flags", [BEQ, N.TMV_FLAG_PER_ENTRY])
 def test_multi_batch_launch(bctx, flags):
     """tmv_verify_batches_device: several independent batches (different
-    sizes, one empty, one unaligned) in one launch equal separate checks."""
+    sizes, one empty, one unaligned, one whose message offsets do not start
+    at 0) in one launch equal separate checks."""
     import torch
     dev = torch.device("cuda:0")
-    specs = [(make_c2_batch(700, seed=41, edge_scale=8.0), 0), (make_c2_batch(0, seed=42), 0),
-             (make_c2_batch(1300, seed=43, edge_scale=4.0), 3), (make_sr25519_batch(0), 0),
-             (make_c2_batch(65, seed=44, edge_scale=20.0), 1)]
+    specs = [(make_c2_batch(700, seed=41, edge_scale=8.0), 0, 0), (make_c2_batch(0, seed=42), 0, 0),
+             (make_c2_batch(1300, seed=43, edge_scale=4.0), 3, 0), (make_sr25519_batch(0), 0, 0),
+             (make_c2_batch(65, seed=44, edge_scale=20.0), 1, 0), (make_c2_batch(300, seed=45, edge_scale=10.0), 2, 7)]
     keep, refs, want = [], [], []
-    for b, shift in specs:
+    for b, shift, base in specs:
         if b.n == 0:
             refs.append(N.BatchRef(0, 0, 0, 0, 0, 0, 0))
             continue
@@ -237,11 +238,11 @@ def test_multi_batch_launch(bctx, flags):
             buf = torch.zeros(len(a) + 16, dtype=torch.uint8, device=dev)
             buf[shift:shift + len(a)] = torch.from_numpy(a).to(dev)
             raw[k] = buf
-        off = torch.from_numpy(b.off.view(np.int32)).to(dev)
+        off = torch.from_numpy((b.off + base).view(np.int32)).to(dev)
         out = torch.full((b.n,), -7, dtype=torch.int8, device=dev)
         keep += [raw, off, out]
         refs.append(N.BatchRef(raw["pk"].data_ptr() + shift, raw["sig"].data_ptr() + shift,
-                               raw["msg"].data_ptr() + shift, off.data_ptr(), b.n, int(b.off[-1] - b.off[0]),
+                               raw["msg"].data_ptr() + shift - base, off.data_ptr(), b.n, int(b.off[-1] - b.off[0]),
                                out.data_ptr()))
         _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
         want.append((out, ref))
