@@ -123,6 +123,12 @@ struct MsmWork {
   uint32_t *fail_list;   // groups: ids of the failing groups
   uint8_t *sub_ok;       // groups x m / kSubGroup: verdict of each sub-group of a failing group
   fe *tabR;              // n x 8 x 4 fe: k_msm_subcheck's tables of -R (its -A tables use Ed25519Work::tabA)
+  // located fallback (msm_kernels.hip, k_loc_*): failing group f's sums T
+  // and T' = sum (j+1) z_j Delta_j, the entries left to verify one by one
+  fe *fail_T;            // groups x 8 fe: [8f .. 8f+3] T (P3Q lanes), [8f+4 .. 8f+7] T'
+  uint32_t *loc_count;   // failing groups x m: entry count of the locate MSM (device)
+  uint32_t *fb_count;    // entries in fb_list
+  uint32_t *fb_list;     // n: work indices verified one by one
   // key-merged form only (null otherwise)
   uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
   uint32_t *bscal;     // groups x 8 words: B scalar of the group
@@ -137,7 +143,8 @@ struct MsmWork {
     size_t b = (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
                2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 16 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
-    else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16;
+    else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
+              G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16;
     return b;
   }
   static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
@@ -164,11 +171,17 @@ struct MsmWork {
     w.fail_count = w.fail_list = nullptr;
     w.sub_ok = nullptr;
     w.tabR = nullptr;
+    w.fail_T = nullptr;
+    w.loc_count = w.fb_count = w.fb_list = nullptr;
     if (!p.merged) {
       w.fail_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
       w.fail_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
       w.sub_ok = b + o; o = up(o + (G << p.m_log2) / kSubGroup);
       w.tabR = reinterpret_cast<fe *>(b + o); o = up(o + (size_t)n * 32 * sizeof(fe));
+      w.fail_T = reinterpret_cast<fe *>(b + o); o = up(o + G * 8 * sizeof(fe));
+      w.loc_count = reinterpret_cast<uint32_t *>(b + o);
+      w.fb_count = w.loc_count + 1; o = up(o + 16);
+      w.fb_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4ull * n);
     }
     if (p.merged) {
       w.wscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32ull * n);

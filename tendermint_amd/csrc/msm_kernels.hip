@@ -93,8 +93,11 @@ __device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &o
 // of the 2m+1 points into the group's slots of ent_pt/ent_bk.  KM (key-merged
 // form): only the m R points are sorted; z_e k_e and the B scalar go to
 // mw.wscal / mw.bscal for k_msm_items, and the key's decode status comes from
-// the key cache.
-template <bool SR, bool KM, int BS = kMsmSortBlock>
+// the key cache.  LOC (located fallback): block f sorts the f-th FAILING
+// group into slot f with every weight multiplied by (j + 1), j the entry's
+// index in its group, so the same bucket stages compute
+// T'_f = sum (j+1) z_j Delta_j (z_j (j+1) < 2^136: ceil(136/c) R windows).
+template <bool SR, bool KM, int BS = kMsmSortBlock, bool LOC = false>
 __global__ void __launch_bounds__(BS)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
            Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned,
@@ -102,10 +105,20 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
            uint32_t e_base) {
   extern __shared__ uint32_t smem[];
   const uint32_t cnt = entry_count(count_ptr, n);
-  const uint32_t g = blockIdx.x;
   const uint32_t tid = threadIdx.x;
+  uint32_t g = blockIdx.x;  // LOC: the slot; the group is fail_list[slot]
+  if (LOC) {
+    const uint32_t nf = *mw.fail_count;
+    if (g == 0 && tid == 0) {
+      *mw.loc_count = nf << p.m_log2;  // the bucket stages' entry count: nf slots
+      *mw.fb_count = 0;                // k_loc_search appends the entries left to verify
+    }
+    if (g >= nf) return;  // block-uniform
+  }
+  const uint32_t slot = g;
+  if (LOC) g = mw.fail_list[slot];
   const uint32_t e0 = g << p.m_log2;
-  if (!KM && g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
+  if (!KM && !LOC && g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
     niels_pt bp;
     bp.ymx = btab_q[0];
     bp.ypx = btab_q[1];
@@ -122,7 +135,9 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   uint32_t *scan = red + BS * 9;    // BS + 1
 
   constexpr int R = 4;  // entries per thread: m <= 4 * BS
-  uint32_t z[R][4], wv[R][8];
+  constexpr int ZW = LOC ? 5 : 4;  // words of the R weight (LOC: z (j + 1) < 2^136)
+  const uint32_t WRz = LOC ? (136 + p.c - 1) / p.c : p.WR;
+  uint32_t z[R][ZW], wv[R][8];
   bool live[R];
   uint32_t acc[9];
 #pragma unroll
@@ -131,7 +146,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   for (int r = 0; r < R; r++) {
     live[r] = false;
 #pragma unroll
-    for (int t = 0; t < 4; t++) z[r][t] = 0;
+    for (int t = 0; t < ZW; t++) z[r][t] = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) wv[r][t] = 0;
     const uint32_t j = tid + r * BS;
@@ -150,7 +165,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       s_ok = sc_is_canonical(s);
     }
     const bool a_ok = KM ? key_ok[key_slot[i]] != 0 : w.flags[4 * e] != 0;
-    if (!KM && out) {  // pre-check status; the compacted fallback rewrites failing groups' entries
+    if (!KM && !LOC && out) {  // pre-check status; the compacted fallback rewrites failing groups' entries
       const bool r_ok = w.flags[4 * e + 1] != 0;
       const int st = SR ? (!a_ok ? -1 : (!s_ok ? -2 : (r_ok ? 1 : 0))) : ((a_ok && r_ok && s_ok) ? 1 : 0);
       out[i] = (uint8_t)(int8_t)st;
@@ -173,13 +188,28 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w;
     k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
     sc_mul_mod(wv[r], z[r], 4, k);
+    if (LOC) {  // weights times (j + 1): z (j + 1) exactly, z k (j + 1) mod l
+      const uint32_t jj = j + 1;
+      uint64_t cy = 0;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        cy += (uint64_t)z[r][t] * jj;
+        z[r][t] = (uint32_t)cy;
+        cy >>= 32;
+      }
+      z[r][4] = (uint32_t)cy;
+      uint32_t t8[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) t8[t] = wv[r][t];
+      sc_mul_mod(wv[r], &jj, 1, t8);
+    }
     if (KM) {
       uint4 *wd = reinterpret_cast<uint4 *>(mw.wscal + 8ull * e);
       wd[0] = make_uint4(wv[r][0], wv[r][1], wv[r][2], wv[r][3]);
       wd[1] = make_uint4(wv[r][4], wv[r][5], wv[r][6], wv[r][7]);
     }
     uint32_t u[8];
-    sc_mul_mod(u, z[r], 4, s);
+    sc_mul_mod(u, z[r], ZW, s);  // LOC: (z (j + 1)) s mod l
     uint64_t c = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
@@ -222,7 +252,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (!live[r]) continue;
-    for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
+    for_each_digit<ZW>(z[r], WRz, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
     if (!KM) for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
   }
   if (!KM && tid == 0) for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool) { atomicAdd(&hist[bk], 1u); });
@@ -245,8 +275,8 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     scan[BS] = run;
   }
   __syncthreads();
-  const uint32_t gbase = g * p.cap;
-  const uint32_t bbase = g * WH;
+  const uint32_t gbase = slot * p.cap;
+  const uint32_t bbase = slot * WH;
   {
     uint32_t off = scan[tid];
     for (uint32_t t = lo; t < hi; t++) {
@@ -266,7 +296,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   for (int r = 0; r < R; r++) {
     if (!live[r]) continue;
     const uint32_t e = e0 + tid + r * BS;
-    for_each_digit<4>(z[r], p.WR, p, [&](uint32_t bk, bool neg) {
+    for_each_digit<ZW>(z[r], WRz, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
       ent_pt[pos] = ((KM ? e : 2 * e) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
@@ -416,7 +446,10 @@ k_msm_wsum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 // Group verdicts: one quad per group (lane c holds coordinate c), 16 groups
 // per wave; T_g = sum_w 2^(c w) S_w by Horner, then
 //   ed25519: [8] T_g == O;  sr25519: T_g is the Ristretto identity.
-template <bool SR, bool KM>
+// A failing group's T_g goes to mw.fail_T at its place in the failing list.
+// LOC: the same Horner over the locate MSM's slots (count_ptr = loc_count),
+// T'_f to mw.fail_T, no verdict.
+template <bool SR, bool KM, bool LOC = false>
 __global__ void __launch_bounds__(64)
 k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, const uint32_t *__restrict__ group_run0,
              uint32_t n_runs) {
@@ -448,6 +481,10 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
       quad::p1p1_to_p3(acc, r);
     }
   }
+  if (LOC) {
+    if (live) mw.fail_T[8ull * g + 4 + c] = acc;
+    return;
+  }
   bool ok;
   if (SR) {
     fe id;
@@ -456,10 +493,85 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
   } else {
     ok = quad::is_identity_times8(acc);
   }
+  int f = -1;
   if (live && c == 0) {
     mw.group_ok[g] = ok ? 1 : 0;
-    if (!ok && mw.fail_list) mw.fail_list[atomicAdd(mw.fail_count, 1u)] = g;
+    if (!ok && mw.fail_list) {
+      f = (int)atomicAdd(mw.fail_count, 1u);
+      mw.fail_list[f] = g;
+    }
   }
+  f = __builtin_amdgcn_mov_dpp(f, quad::qp(0, 0, 0, 0), 0xF, 0xF, false);  // the quad's lane 0
+  if (f >= 0 && mw.fail_T) mw.fail_T[8ull * f + c] = acc;
+}
+
+// Located fallback, search stage: one wave per failing group (slot f).  With
+// M = [8] T_f and M' = [8] T'_f (sr25519: T and T' themselves, compared as
+// Ristretto points), the group holds exactly one entry j whose term is not
+// torsion iff M' = [j + 1] M: M has prime order l and (j + 1) < l, so j is
+// unique; with two or more such entries a match needs the random weights to
+// satisfy a fixed linear relation (probability ~2^-128 per candidate).
+// Quad q tries j = q, q + 16, ...: [q + 1] M, then + [16] M each step.  One
+// match: only entry j is verified one by one (every other entry keeps its
+// pre-check status); otherwise every entry of the group is.
+template <bool SR>
+__global__ void __launch_bounds__(64)
+k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  __shared__ int s_cnt, s_j;
+  __shared__ uint32_t s_base;
+  const uint32_t f = blockIdx.x;
+  if (f >= *mw.fail_count) return;  // block-uniform
+  const int c = (int)(threadIdx.x & 3), q = (int)(threadIdx.x >> 2);
+  if (threadIdx.x == 0) {
+    s_cnt = 0;
+    s_j = -1;
+  }
+  fe M = mw.fail_T[8ull * f + c], Mp = mw.fail_T[8ull * f + 4 + c], r;
+  if (!SR) {
+    for (int i = 0; i < 3; i++) {
+      quad::dbl(r, M);
+      quad::p1p1_to_p3(M, r);
+      quad::dbl(r, Mp);
+      quad::p1p1_to_p3(Mp, r);
+    }
+  }
+  fe Mc, Dc, P = M, D = M;
+  quad::to_cached(Mc, M);
+  const int k = q + 1;  // <= 16; quad-uniform
+  for (int b = 30 - __builtin_clz((unsigned)k); b >= 0; b--) {
+    quad::dbl(r, P);
+    quad::p1p1_to_p3(P, r);
+    if ((k >> b) & 1) {
+      quad::add(r, P, Mc);
+      quad::p1p1_to_p3(P, r);
+    }
+  }
+  for (int i = 0; i < 4; i++) {
+    quad::dbl(r, D);
+    quad::p1p1_to_p3(D, r);
+  }
+  quad::to_cached(Dc, D);
+  __syncthreads();  // s_cnt / s_j initialised
+  const uint32_t m = p.m();
+  for (uint32_t j = (uint32_t)q; j < m; j += 16) {
+    const bool eq = SR ? quad::ristretto_equal(P, Mp) : quad::p3_equal(P, Mp);
+    if (eq && c == 0) {
+      atomicAdd(&s_cnt, 1);
+      s_j = (int)j;
+    }
+    quad::add(r, P, Dc);
+    quad::p1p1_to_p3(P, r);
+  }
+  __syncthreads();
+  const uint32_t e0 = mw.fail_list[f] << p.m_log2;
+  const uint32_t mlive = min(m, entry_count(count_ptr, n) - e0);
+  if (s_cnt == 1 && (uint32_t)s_j < mlive) {  // block-uniform
+    if (threadIdx.x == 0) mw.fb_list[atomicAdd(mw.fb_count, 1u)] = e0 + (uint32_t)s_j;
+    return;
+  }
+  if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < mlive; t += 64) mw.fb_list[s_base + t] = e0 + t;
 }
 
 // Sub-group bisection (row H, before the per-entry fallback): a failing group
@@ -729,6 +841,22 @@ static bool fallback_compact() {
   return on;
 }
 
+// Located fallback (k_msm_sort<LOC> .. k_loc_search): for launches of at
+// least this many entries (TMV_LOCATE_MIN, 0 = never) a failing group gets a
+// second, index-weighted MSM that names its one bad entry, so one entry is
+// verified instead of the whole group; two bad entries in a group still
+// fall back to all of them.  Less work (the second MSM costs about one
+// group's share of the pipeline, the per-entry fallback ~64 verifications),
+// a longer chain (a second Horner), so it pays where throughput, not the
+// launch's latency, sets the rate.
+static uint32_t locate_min() {
+  static const uint32_t v = [] {
+    const char *e = getenv("TMV_LOCATE_MIN");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 150000u;
+  }();
+  return v;
+}
+
 bool subcheck_enabled(uint32_t m_log2) {
   const int mode = subcheck_mode();
   return mode < 0 ? m_log2 >= 8 : mode == 1;
@@ -833,6 +961,31 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
                      nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint32_t lmin = locate_min();
+  if (compact && lmin && n >= lmin && !subcheck_enabled(p.m_log2) && (136 + p.c - 1) / p.c <= p.W) {
+    // second MSM over the failing groups (slot f = f-th failing group), then
+    // the search, then one-by-one verification of the listed entries only
+    if (p.m_log2 <= 8 && sort_block() == 64) {
+      const size_t smem = ((size_t)p.W * p.H + 64 * 9 + 64 + 1) * sizeof(uint32_t);
+      hipLaunchKernelGGL((k_msm_sort<SR, false, 64, true>), dim3(p.groups), dim3(64), smem, stream, sig, idx,
+                         count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
+    } else {
+      const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+      hipLaunchKernelGGL((k_msm_sort<SR, false, kMsmSortBlock, true>), dim3(p.groups), dim3(kMsmSortBlock), smem,
+                         stream, sig, idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr,
+                         0u);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t n_slots = p.groups << p.m_log2;
+    if ((e = launch_buckets(mw.loc_count, n_slots, mw, p, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
+                       mw.loc_count, n_slots, mw, p, nullptr, 0u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream,
+                                    nullptr, nullptr, nullptr, mw.fb_list, mw.fb_count);
+  }
   const uint8_t *sub_ok = nullptr;
   if (subcheck_enabled(p.m_log2)) {
     // grid for every group failing; blocks past the failing count exit at once

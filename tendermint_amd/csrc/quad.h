@@ -163,6 +163,28 @@ TMV_DEV bool is_identity_times8(const fe &p) {
   return (z0 & z1) != 0;
 }
 
+// Equality of two P3Q points: X1 Z2 == X2 Z1 and Y1 Z2 == Y2 Z1.  Quad
+// verdict on every lane.
+TMV_DEV bool p3_equal(const fe &a, const fe &b) {
+  const int c = lane4();
+  fe ta, tb, za, zb, o1, o2, p, d;
+  fe_dpp<qp(0, 1, 0, 1)>(ta, a);            // X1, Y1, X1, Y1
+  fe_dpp<qp(0, 1, 0, 1)>(tb, b);            // X2, Y2, X2, Y2
+  fe_dpp<qp(2, 2, 2, 2)>(za, a);            // Z1
+  fe_dpp<qp(2, 2, 2, 2)>(zb, b);            // Z2
+  o1 = ta;
+  fe_cmov(o1, tb, c >= 2);                  // X1, Y1, X2, Y2
+  o2 = zb;
+  fe_cmov(o2, za, c >= 2);                  // Z2, Z2, Z1, Z1
+  fe_mul(p, o1, o2);
+  fe_dpp<qp(2, 3, 0, 1)>(d, p);
+  fe_sub(d, p, d);                          // lane 0: X1 Z2 - X2 Z1, lane 1: Y1 Z2 - Y2 Z1
+  const int zero = fe_is_zero(d) ? 1 : 0;
+  const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
+  const int z1 = __builtin_amdgcn_mov_dpp(zero, qp(1, 1, 1, 1), 0xF, 0xF, false);
+  return (z0 & z1) != 0;
+}
+
 // Ristretto equality of two P3Q points a (acc) and b (R):
 // X1 Y2 == Y1 X2 or Y1 Y2 == X1 X2.  Quad verdict on every lane.
 TMV_DEV bool ristretto_equal(const fe &a, const fe &b) {

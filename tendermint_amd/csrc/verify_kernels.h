@@ -97,7 +97,8 @@ template <bool SR>
 hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                                 const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
                                 uint8_t *out, int aligned, hipStream_t stream, const uint8_t *sub_ok = nullptr,
-                                const uint32_t *fail_list = nullptr, const uint32_t *fail_count = nullptr);
+                                const uint32_t *fail_list = nullptr, const uint32_t *fail_count = nullptr,
+                                const uint32_t *fb_list = nullptr, const uint32_t *fb_count = nullptr);
 // k_msm_subcheck runs before the per-entry fallback for groups of 2^m_log2
 // (default m >= 256; TMV_SUBCHECK=0 never, =1 always).
 bool subcheck_enabled(uint32_t m_log2);

@@ -185,28 +185,39 @@ __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
               const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok,
-              const uint32_t *__restrict__ fail_list, const uint32_t *__restrict__ fail_count) {
+              const uint32_t *__restrict__ fail_list, const uint32_t *__restrict__ fail_count,
+              const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count) {
   __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
   __shared__ int8_t dig[kQuadSigs][2][64];
   const uint32_t m = entry_count(count_ptr, n);
-  // Compacted fallback (fail_list): block b covers the b-th 16-entry block of
-  // the failing groups k_msm_horner listed; every other entry already holds
-  // its pre-check status (written by k_msm_sort).  Otherwise block b covers
-  // entries [16 b, 16 b + 16).
-  uint32_t b0;
-  if (fail_list) {
-    const uint32_t per_log2 = group_log2 - 4;  // 16-entry blocks per group
-    if (blockIdx.x >= (*fail_count << per_log2)) return;  // block-uniform
-    b0 = (fail_list[blockIdx.x >> per_log2] << group_log2) + ((blockIdx.x & ((1u << per_log2) - 1)) << 4);
-  } else {
-    b0 = blockIdx.x * kQuadSigs;
-  }
-  if (b0 >= m) return;  // block-uniform
   const int c = threadIdx.x & 3;
   const int q = threadIdx.x >> 2;
-  const uint32_t raw = b0 + q;
-  const bool live = raw < m;
-  const uint32_t e = live ? raw : m - 1;
+  // Entry list (fb_list, the located fallback): quad q of block b verifies
+  // entry fb_list[16 b + q].  Compacted fallback (fail_list): block b covers
+  // the b-th 16-entry block of the failing groups k_msm_horner listed.  In
+  // both, every other entry already holds its pre-check status (written by
+  // k_msm_sort).  Otherwise block b covers entries [16 b, 16 b + 16).
+  uint32_t b0 = 0, e;
+  bool live;
+  if (fb_list) {
+    const uint32_t nl = *fb_count;
+    if (blockIdx.x * kQuadSigs >= nl) return;  // block-uniform
+    const uint32_t t = blockIdx.x * kQuadSigs + q;
+    live = t < nl;
+    e = fb_list[live ? t : nl - 1];
+  } else {
+    if (fail_list) {
+      const uint32_t per_log2 = group_log2 - 4;  // 16-entry blocks per group
+      if (blockIdx.x >= (*fail_count << per_log2)) return;  // block-uniform
+      b0 = (fail_list[blockIdx.x >> per_log2] << group_log2) + ((blockIdx.x & ((1u << per_log2) - 1)) << 4);
+    } else {
+      b0 = blockIdx.x * kQuadSigs;
+    }
+    if (b0 >= m) return;  // block-uniform
+    const uint32_t raw = b0 + q;
+    live = raw < m;
+    e = live ? raw : m - 1;
+  }
   const uint32_t i = idx ? idx[e] : e;
   // Batch equation held for this block's group (groups are >= 32 entries, so
   // the test is block-uniform): every entry that passed decoding and the S
@@ -214,7 +225,7 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   // With the sub-group verdicts (k_msm_subcheck) a block of a failing group
   // passes when every sub-group it covers passed.
   bool pass = false;
-  if (group_ok) {
+  if (group_ok && !fb_list) {
     pass = !fail_list && group_ok[b0 >> group_log2];
     if (!pass && sub_ok) {
       pass = true;
@@ -753,13 +764,16 @@ static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig
                         const uint32_t *count_ptr, uint32_t n, Ed25519Work w, const fe *btab_q, uint8_t *out,
                         int aligned, const uint8_t *group_ok, uint32_t group_log2,
                         const uint8_t *sub_ok = nullptr, const uint32_t *fail_list = nullptr,
-                        const uint32_t *fail_count = nullptr) {
+                        const uint32_t *fail_count = nullptr, const uint32_t *fb_list = nullptr,
+                        const uint32_t *fb_count = nullptr) {
   if (quad_table_global())
     hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
-                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count);
+                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count, fb_list,
+                       fb_count);
   else
     hipLaunchKernelGGL((k_verify_quad<SR, false>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
-                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count);
+                       w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count, fb_list,
+                       fb_count);
 }
 
 static int is_aligned(const void *a, const void *b) {
@@ -786,20 +800,25 @@ template <bool SR>
 hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                                 const fe *btab_q, Ed25519Work w, const uint8_t *group_ok, uint32_t group_log2,
                                 uint8_t *out, int aligned, hipStream_t stream, const uint8_t *sub_ok,
-                                const uint32_t *fail_list, const uint32_t *fail_count) {
-  // compacted: a grid for every group failing (blocks past the failing count exit at once)
-  const uint32_t qblocks = fail_list ? ((((n + (1u << group_log2) - 1) >> group_log2)) << (group_log2 - 4))
-                                     : (n + kQuadSigs - 1) / kQuadSigs;
+                                const uint32_t *fail_list, const uint32_t *fail_count, const uint32_t *fb_list,
+                                const uint32_t *fb_count) {
+  // compacted / entry list: a grid for every group failing (blocks past the
+  // failing count exit at once)
+  const uint32_t qblocks = fb_list ? (n + kQuadSigs - 1) / kQuadSigs
+                           : fail_list ? ((((n + (1u << group_log2) - 1) >> group_log2)) << (group_log2 - 4))
+                                       : (n + kQuadSigs - 1) / kQuadSigs;
   launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok,
-                  fail_list, fail_count);
+                  fail_list, fail_count, fb_list, fb_count);
   return hipGetLastError();
 }
 template hipError_t launch_quad_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
                                                 const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
-                                                hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *);
+                                                hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *,
+                                                const uint32_t *, const uint32_t *);
 template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,
                                                const fe *, Ed25519Work, const uint8_t *, uint32_t, uint8_t *, int,
-                                               hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *);
+                                               hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *,
+                                               const uint32_t *, const uint32_t *);
 
 // Decode and hash blocks in one launch (default; TMV_PREP_FUSED=0: two
 // kernels).  Measured in one GPU call (tools/gpu_ab_env.sh): one 10k batch

@@ -252,3 +252,32 @@ def test_multi_batch_launch(bctx, flags):
     torch.cuda.synchronize()
     for out, ref in want:
         assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref)
+
+
+@pytest.mark.parametrize("kind", [ED, SR])
+def test_located_fallback_placements(bctx, kind):
+    """Launches of >= 150k entries (TMV_LOCATE_MIN) re-check a failing group
+    with index weights (j + 1) z_j and verify only the entry that locates;
+    groups with two or more bad entries fall back to every entry.  One bad
+    entry at each group edge (j = 0, 31, 63), pairs, a whole bad group and a
+    ragged tail: the vector equals the oracle's."""
+    n = 150_000 + 37
+    base = make_commit_batch(1500, seed=21) if kind == ED else make_sr25519_batch(1500, seed=22, bad_frac=0.0)
+    b = base.tile(n)
+    sig = b.sig.copy()
+    bad = [0, 64 + 31, 128 + 63, 640 + 5, 640 + 6, 1280 + 1, 1280 + 40, 1280 + 62] + list(range(1920, 1984))
+    bad += [n - 1, n - 30, 77_777, 149_999]
+    for i in bad:
+        sig[64 * i + 5] ^= 0x10  # R byte: R mostly still decodes, the equation fails
+    bb = _B(b.pk, sig, b.msg, b.off)
+    ok, st, groups, failed = _run(bctx, kind, bb)
+    if kind == ED:
+        ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
+        assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
+        pre = C.ed25519_prechecks(b.pk, sig)
+    else:
+        ref = C.sr25519_status_packed(b.pk, sig, b.msg, b.off, threads=16)
+        assert np.array_equal(st, ref)
+        pre = C.sr25519_prechecks(b.pk, sig)
+    assert groups == (n + 63) // 64
+    assert failed == C.failing_groups(pre, ref == 1, 64) and failed >= 3
