@@ -28,6 +28,7 @@
 #include "ed25519_core.h"
 #include "merlin_dev.h"
 #include "host/pool.h"
+#include "host/shard_plan.h"
 #include "host/wait.h"
 #include "verify_kernels.h"
 #include "votes.h"
@@ -1126,29 +1127,13 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     set_error("null argument");
     return TMV_ERR_ARG;
   }
-  const uint32_t ndev = (uint32_t)ctx->devs.size();
-  // tiny batches stay on one device
-  const uint32_t shards = std::max<uint32_t>(1, std::min<uint32_t>(ndev, n / 1024));
+  read_env();
+  const tmh::ShardPlan plan = tmh::plan_shards(n, (uint32_t)ctx->devs.size(), g_host_chunk);
+  const uint32_t shards = plan.shards;
   std::vector<std::unique_lock<std::mutex>> locks;
-  std::vector<uint32_t> bounds(shards + 1);
-  for (uint32_t s = 0; s <= shards; s++) bounds[s] = (uint32_t)((uint64_t)n * s / shards);
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
   for (uint32_t s = 0; s < shards; s++)
     if (ctx->devs[s]->faulted) return faulted_rc(*ctx->devs[s]);
-  // each shard is cut into chunks of up to g_host_chunk entries, alternating
-  // between the device's lanes
-  read_env();
-  // (chunks of at least g_host_chunk / 2 entries: at least 4 once there is
-  // room, then g_host_chunk each; fewer, larger chunks keep the key-merged
-  // form's per-chunk sort and launch chain cheap)
-  const uint32_t chunk = std::max<uint32_t>(2048, g_host_chunk);
-  std::vector<uint32_t> nchunks(shards);
-  uint32_t max_chunks = 0;
-  for (uint32_t s = 0; s < shards; s++) {
-    const uint32_t len = bounds[s + 1] - bounds[s];
-    nchunks[s] = std::max<uint32_t>(1, std::min<uint32_t>(len / (chunk / 2), std::max<uint32_t>(4, len / chunk)));
-    max_chunks = std::max(max_chunks, nchunks[s]);
-  }
   int rc = 0;
   EngineTimer tm;
   auto harvest = [&](Device &d, HostLane &ln) {
@@ -1162,13 +1147,12 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     if (rc == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
     ln.n = 0;
   };
-  for (uint32_t k = 0; k < max_chunks && rc == 0; k++) {
+  // chunk k of every shard, then chunk k + 1: the devices work side by side
+  for (uint32_t k = 0; k < plan.max_chunks && rc == 0; k++) {
     for (uint32_t s = 0; s < shards && rc == 0; s++) {
-      if (k >= nchunks[s]) continue;
+      if (k >= plan.nchunks[s]) continue;
       Device &d = *ctx->devs[s];
-      const uint32_t len = bounds[s + 1] - bounds[s];
-      const uint32_t c0 = bounds[s] + (uint32_t)((uint64_t)len * k / nchunks[s]);
-      const uint32_t c1 = bounds[s] + (uint32_t)((uint64_t)len * (k + 1) / nchunks[s]);
+      const uint32_t c0 = plan.chunk_lo(s, k), c1 = plan.chunk_lo(s, k + 1);
       HostLane &ln = d.lane[k % g_host_lanes];
       (void)hipSetDevice(d.id);
       harvest(d, ln);  // the lane's previous chunk

@@ -16,6 +16,7 @@
 #include "../../include/tmhost.h"
 #include "../../include/tmverify.h"
 #include "../../tendermint_amd/csrc/host/tm_light.h"
+#include "../../tendermint_amd/csrc/host/shard_plan.h"
 #include "../../tendermint_amd/csrc/host/wait.h"
 #include "../../tendermint_amd/csrc/host/tm_types.h"
 #include "../../tendermint_amd/csrc/sha512_dev.h"
@@ -230,4 +231,25 @@ size_t commitcheck_canonical_time(int64_t secs, int32_t nanos, char *out, size_t
   out[cap - 1] = 0;
   return s.size();
 }
+}
+
+// The runtime's shard / chunk plan of a host-buffer batch (host/shard_plan.h,
+// used by run_batch), in launch order: (device, lo, hi, chunk k) per chunk.
+// Returns the number of chunks written (or needed, if cap is short).
+extern "C" uint32_t commitcheck_shard_plan(uint32_t n, uint32_t ndev, uint32_t host_chunk, uint32_t *out,
+                                           uint32_t cap) {
+  const tmh::ShardPlan p = tmh::plan_shards(n, ndev, host_chunk);
+  uint32_t w = 0;
+  for (uint32_t k = 0; k < p.max_chunks; k++)
+    for (uint32_t s = 0; s < p.shards; s++) {
+      if (k >= p.nchunks[s]) continue;
+      if (w < cap) {
+        out[4 * w] = s;
+        out[4 * w + 1] = p.chunk_lo(s, k);
+        out[4 * w + 2] = p.chunk_lo(s, k + 1);
+        out[4 * w + 3] = k;
+      }
+      w++;
+    }
+  return w;
 }
