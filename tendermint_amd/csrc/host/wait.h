@@ -14,19 +14,21 @@ namespace tmh {
 enum class Poll { kReady = 0, kError = 1, kTimeout = 2 };
 
 // query() returns 0 when done, 1 while pending, anything else on error.
-// Spins (yielding) for the first ~200 us so short kernels keep their latency,
-// then sleeps 20 us between polls.
+// Spins (yielding) for the first 5 ms so short and medium launches keep
+// their latency -- a sleep rounds up to the timer slack (~50 us), which a
+// 200 us spin phase put on every ~0.2 ms VerifyCommit (C1 p50 0.24 ->
+// 0.30 ms) -- then sleeps 20 us between polls.
 template <class Q>
 Poll poll_until(Q query, int64_t timeout_ms) {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
-  for (uint32_t spin = 0;; spin++) {
+  for (;;) {
     const int q = query();
     if (q == 0) return Poll::kReady;
     if (q != 1) return Poll::kError;
     const auto el = clk::now() - t0;
     if (timeout_ms > 0 && el > std::chrono::milliseconds(timeout_ms)) return Poll::kTimeout;
-    if (el < std::chrono::microseconds(200)) std::this_thread::yield();
+    if (el < std::chrono::milliseconds(5)) std::this_thread::yield();
     else std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }
