@@ -3,22 +3,24 @@
 
   python bench.py --gpus N --steps K --warmup W
 
-A *step* = one pass of the hot path over one synthetic C2 batch
-(BASELINE.json configs[1]: 10,000 ed25519 signatures over commit-vote
-sign-bytes, 1% corrupted / ZIP-215 edge cases) already resident in HBM,
-producing that batch's exact validity vector.  Each rank holds K distinct
-C2 batches; a launch (tmv_verify_batches_device) verifies several of them at
-once (`plan_launches`: up to 32 per launch, at least 8 when --steps is small;
-`--per-launch` / `--plan` override): the batches are gathered on the device,
-run through one pipeline and each gets its own vector, as a node draining a
-queue of batches does (a single 10k batch fills about one wave per SIMD and
-is latency-bound).  `--inflight F` keeps F launches in flight
-on F streams (default 4, the HIP hardware queues per process).  `--method batch` (default) uses the random-linear-combination
-group check with per-entry fallback (voi's BatchVerifier.Verify, SURVEY rows
-G-I); `--method per-entry` verifies every signature singly.  With N > 1 (one
-process per GPU, torchrun) every rank verifies its own batches (weak
-scaling) and the packed validity bitmaps are all-gathered over RCCL on one
-communication stream, the only cross-GPU exchange the path has.
+A *step* = one device launch (tmv_verify_batches_device) that verifies
+`--batches-per-step` (default 32) synthetic C2 batches (BASELINE.json
+configs[1]: 10,000 ed25519 signatures over commit-vote sign-bytes, 1%
+corrupted / ZIP-215 edge cases each) already resident in HBM, producing every
+batch's exact validity vector: the batches are gathered on the device, run
+through one pipeline and each gets its own vector, as a node draining a queue
+of batches does.  A single 10k batch fills about one wave per SIMD and ends
+in two latency chains (Horner, per-entry fallback), so its
+latency is reported beside the throughput (`batch_latency_ms`), not as it.
+`--steps K` times exactly K such launches; `--inflight F` keeps F launches in
+flight on F streams (default 4, the HIP hardware queues per process), so
+the driver's `--steps 20` already measures the steady state.  `--method batch`
+(default) uses the random-linear-combination group check with per-entry
+fallback (voi's BatchVerifier.Verify); `--method per-entry`
+verifies every signature singly.  With N > 1 (one process per GPU, torchrun)
+every rank verifies its own batches (weak scaling) and the packed validity
+bitmaps are all-gathered over RCCL on one communication stream, the only
+cross-GPU exchange the path has.
 
 Printed (rank 0, one JSON line): value = verifies/s of the whole job
 (kernel path, inputs resident), the single-batch latency and serial rate,
@@ -79,11 +81,12 @@ def _load_peak() -> float:
 PMC_DIRS = ("r02", "r01_close")  # newest first
 
 
-def _load_pmc(method: str):
+def _load_pmc(method: str, batches_per_step: int = 32):
     """PMC summary of the batch-equation (or per-entry) pipeline from the
     newest committed passes (tools/profile_round.sh + tools/pmc_summary.py:
     FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/pmc_derived.py:
-    occupancy, VALU issue), normalised to one step (one 10k C2 batch)."""
+    occupancy, VALU issue), normalised to one step (one launch of
+    `batches_per_step` 10k C2 batches)."""
     name = "pmc_batch.json" if method == "batch" else "pmc_per_entry.json"
     for d in PMC_DIRS + ("r01_msm",):
         path = os.path.join(REPO, "profiles", d, name)
@@ -94,10 +97,10 @@ def _load_pmc(method: str):
         per_launch = pmc.get("batches_per_launch", 32)
         out = dict(pmc)
         if "hbm_bytes_per_launch" in pmc:
-            out["hbm_bytes_per_step"] = int(pmc["hbm_bytes_per_launch"] / per_launch)
-            out["note"] = (f"HBM bytes per 10k-signature step from PMC (profiles/{d}/{name}: FETCH_SIZE x2 gfx950 "
-                           f"correction + WRITE_SIZE, launches of {per_launch} batches); algorithmic input bytes per "
-                           "step = 10k x ~222 B = 2.2 MB")
+            out["hbm_bytes_per_step"] = int(pmc["hbm_bytes_per_launch"] * batches_per_step / per_launch)
+            out["note"] = (f"HBM bytes per step ({batches_per_step} x 10k signatures) from PMC (profiles/{d}/{name}: "
+                           f"FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, launches of {per_launch} batches); "
+                           f"algorithmic input bytes per step = {batches_per_step} x 10k x ~222 B")
         out["source"] = f"profiles/{d}/{name}"
         return out
     return {}
@@ -233,34 +236,16 @@ class _HostEvent:
         return (other.t - self.t) * 1e3
 
 
-def plan_launches(steps: int, per_launch: int, inflight: int, max_per_launch: int = 32):
-    """Split `steps` batches into launches: per_launch > 0 fixes the launch
-    size; 0 = auto: at most max_per_launch batches per launch and at most
-    `inflight` launches, each of at least 8 batches when there are few steps
-    (every launch carries a latency tail -- Horner and the per-entry fallback
-    chains -- so small launches waste the chip; measured at 20 steps: 1 x 20
-    56.7, 2 x 10 60.5, 4 x 5 56.2, 7 x 3 46.7 M/s, profiles/r02/bench_sweep.txt).
-    Returns the list of launch sizes (sum = steps)."""
-    if per_launch <= 0:
-        lanes = max(1, min(inflight, steps // 8))
-        per_launch = max(1, min(max_per_launch, -(-steps // lanes)))
-    sizes = [per_launch] * (steps // per_launch)
-    if steps % per_launch:
-        sizes.append(steps % per_launch)
-    return sizes
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1536, help="C2 batches verified in the timed region")
-    ap.add_argument("--warmup", type=int, default=64, help="C2 batches verified before timing")
+    ap.add_argument("--steps", type=int, default=48, help="timed steps (device launches of --batches-per-step "
+                                                           "C2 batches)")
+    ap.add_argument("--warmup", type=int, default=8, help="untimed steps before timing (at least --inflight)")
     ap.add_argument("--batch", type=int, default=10_000)
-    ap.add_argument("--per-launch", type=int, default=0,
-                    help="batches per pipeline launch (tmv_verify_batches_device, <= 32); 0 = auto")
+    ap.add_argument("--batches-per-step", "--per-launch", dest="per_step", type=int, default=32,
+                    help="C2 batches per step (one tmv_verify_batches_device launch, <= 64)")
     ap.add_argument("--inflight", type=int, default=4, help="launches in flight (streams)")
-    ap.add_argument("--plan", default="", help="explicit launch sizes, comma separated (sum = --steps); "
-                                                "overrides --per-launch")
     ap.add_argument("--resident", type=int, default=32, help="distinct C2 batches held in HBM per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / end-to-end / C1 measurements")
@@ -280,11 +265,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     F = max(1, args.inflight)
     R = max(1, min(64, args.resident))
-    sizes = plan_launches(max(1, args.steps), args.per_launch, F)
-    if args.plan:
-        sizes = [int(x) for x in args.plan.split(",")]
-        assert sum(sizes) == args.steps and all(0 < x <= 32 for x in sizes), (sizes, args.steps)
-    K = max(sizes)
+    K = max(1, min(64, args.per_step))
+    sizes = [K] * max(1, args.steps)
     # R distinct C2 batches per rank (own keys / messages), generated on the
     # host before this process touches the GPU (worker processes are forked)
     with ProcessPoolExecutor(min(8, R)) as ex:
@@ -360,14 +342,15 @@ def main():
 
     # warmup: every stream's workspace is allocated by its first launch, at
     # the largest launch size of the timed region
-    run(plan_launches(max(args.warmup, F * K), K, F))
+    run([K] * max(args.warmup, F))
     sync(dev)
     if world > 1:
         dist.barrier()
     evs = [(Event(enable_timing=True), Event(enable_timing=True)) for _ in sizes]
     sync(dev)
     t0 = time.perf_counter()
-    steps = run(sizes, evs)
+    n_batches = run(sizes, evs)
+    steps = len(sizes)
     sync(dev)
     if world > 1:
         dist.barrier()
@@ -450,12 +433,12 @@ def main():
 
     result = None
     if rank == 0:
-        total = n * world * steps
+        total = n * world * n_batches
         value = total / elapsed
-        gpu_rate = n * steps / elapsed  # this rank
+        gpu_rate = n * n_batches / elapsed  # this rank
         peak = _load_peak()
         achieved = gpu_rate * MULS_PER_SIG
-        pmc = _load_pmc(args.method)
+        pmc = _load_pmc(args.method, K)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -470,8 +453,9 @@ def main():
             "dtype": "int32",
             "data": "synthetic (deterministic C2 generator, OpenSSL-signed commit-vote sign-bytes)",
             "config": {"workload": "C2: 10k ed25519 ZIP-215 batch, 1% corrupted/edge-case sigs (BASELINE configs[1])",
-                       "step": "one C2 batch (10,000 signatures) verified to its exact validity vector",
-                       "batch_per_step": n, "launch_sizes": sizes, "launches": len(sizes),
+                       "step": f"one device launch verifying {K} C2 batches ({n:,} signatures each) to their exact "
+                               "validity vectors",
+                       "batch": n, "batches_per_step": K, "signatures_per_step": K * n,
                        "launches_in_flight": F, "resident_batches": R,
                        "method": args.method, "msg_bytes_avg": round(float(batch.msg.size) / n, 1),
                        "parallelism": f"shard{world}" if world > 1 else "single"},

@@ -863,7 +863,7 @@ bool subcheck_enabled(uint32_t m_log2) {
 }
 
 // Views of a launch's work arrays for the entries of groups [g0, ...): the
-// throughput stages of one part of a split launch run on these exactly as on
+// throughput stages of one part of a launch run on these exactly as on
 // a whole batch (indices inside a view are relative), and the whole-launch
 // stages (Horner, fallback) read the same arrays through the full structs.
 static Ed25519Work work_view(Ed25519Work w, uint64_t e0) {
@@ -897,14 +897,11 @@ static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0)
 // [e_base, e_base + n) of a launch; w / mw / out / pk / sig / msg_off are
 // already offset to the part.
 template <bool SR>
-static hipError_t launch_part(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                              const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, uint32_t e_base,
-                              const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
-                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned, bool compact,
-                              hipStream_t stream) {
-  w.niels = mw.pts;
-  hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
-  if (e != hipSuccess) return e;
+static hipError_t launch_sort_buckets(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                                      uint32_t e_base, const fe *btab_q, Ed25519Work w, MsmWork mw,
+                                      const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned,
+                                      bool compact, hipStream_t stream) {
+  hipError_t e;
   // groups of <= 256 entries: 64-thread workgroups (4 entries per thread at
   // most), so a 64-entry group no longer parks 192 idle lanes
   if (p.m_log2 <= 8 && sort_block() == 64) {
@@ -922,42 +919,26 @@ static hipError_t launch_part(const uint8_t *pk, const uint8_t *sig, const uint8
 }
 
 template <bool SR>
-static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                               const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const fe *btab_q,
-                               const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
-                               const MsmSeed &seed, uint8_t *out, hipStream_t stream, const SplitStreams *split) {
-  if (n == 0) return hipSuccess;
-  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
-  const bool compact = fallback_compact();
+static hipError_t launch_part(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                              const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, uint32_t e_base,
+                              const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned, bool compact,
+                              hipStream_t stream) {
   w.niels = mw.pts;
+  hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
+  if (e != hipSuccess) return e;
+  return launch_sort_buckets<SR>(sig, idx, count_ptr, n, e_base, btab_q, w, mw, p, seed, out, aligned, compact,
+                                 stream);
+}
+
+// Latency stages of a whole launch: Horner over every group, then the
+// located fallback (large launches) or the per-entry fallback of the failing
+// groups.
+template <bool SR>
+static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                              const fe *btab_q, Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
+                              uint8_t *out, int aligned, bool compact, hipStream_t stream) {
   hipError_t e;
-  // Split launch: the groups' first and second halves run their throughput
-  // stages on two streams at once (the caller's and a helper forked from
-  // it), then join for one Horner and one fallback over all groups -- two
-  // concurrent halves fill each other's wave-quantisation gaps, and the
-  // launch keeps a single latency tail.  Contiguous batches only.
-  const uint32_t g0 = (p.groups + 1) / 2;
-  const uint64_t e0 = (uint64_t)g0 << p.m_log2;
-  if (split && !idx && !count_ptr && g0 > 0 && e0 < n) {
-    MsmParams p0 = p, p1 = p;
-    p0.groups = g0;
-    p1.groups = p.groups - g0;
-    if ((e = hipEventRecord(split->fork, stream)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(split->helper, split->fork, 0)) != hipSuccess) return e;
-    e = launch_part<SR>(pk, sig, msg, msg_off, nullptr, nullptr, (uint32_t)e0, 0u, btab_q, prefix, w, mw, p0, seed,
-                        out, aligned, compact, stream);
-    if (e != hipSuccess) return e;
-    e = launch_part<SR>(pk + 32 * e0, sig + 64 * e0, msg, msg_off + e0, nullptr, nullptr, (uint32_t)(n - e0),
-                        (uint32_t)e0, btab_q, prefix, work_view(w, e0), msm_view(mw, p, n, g0), p1, seed,
-                        out ? out + e0 : nullptr, aligned, compact, split->helper);
-    if (e != hipSuccess) return e;
-    if ((e = hipEventRecord(split->join, split->helper)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(stream, split->join, 0)) != hipSuccess) return e;
-  } else {
-    e = launch_part<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, 0u, btab_q, prefix, w, mw, p, seed, out, aligned,
-                        compact, stream);
-    if (e != hipSuccess) return e;
-  }
   hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
                      nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -997,6 +978,69 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
   }
   return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream,
                                   sub_ok, compact ? mw.fail_list : nullptr, compact ? mw.fail_count : nullptr);
+}
+
+template <bool SR>
+static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
+                               const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const fe *btab_q,
+                               const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                               const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  const bool compact = fallback_compact();
+  w.niels = mw.pts;
+  hipError_t e = launch_part<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, 0u, btab_q, prefix, w, mw, p, seed, out,
+                                 aligned, compact, stream);
+  if (e != hipSuccess) return e;
+  return launch_tail<SR>(sig, idx, count_ptr, n, btab_q, w, mw, p, seed, out, aligned, compact, stream);
+}
+
+hipError_t launch_batch_check_part(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                   const uint32_t *msg_off, uint32_t n, uint32_t e0, uint32_t e1, const fe *btab_q,
+                                   const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                                   const MsmSeed &seed, uint8_t *out, hipStream_t stream, bool prep_only) {
+  // a part is whole groups: it starts on a group edge and ends on one or at n
+  if (e0 >= e1 || e1 > n || (e0 & (p.m() - 1)) || (e1 != n && (e1 & (p.m() - 1)))) return hipErrorInvalidValue;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  const uint32_t g0 = e0 >> p.m_log2;
+  MsmParams pp = p;
+  pp.groups = ((e1 - e0) + p.m() - 1) >> p.m_log2;
+  w.niels = mw.pts;
+  const uint64_t E = e0;
+  if (prep_only) {  // the sort and bucket stages run later over the whole launch
+    Ed25519Work v = work_view(w, E);
+    v.niels = mw.pts + 2 * E;
+    if (sr) return launch_prep<true>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, prefix,
+                                     v, aligned, stream);
+    return launch_prep<false>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, prefix, v,
+                              aligned, stream);
+  }
+  if (sr)
+    return launch_part<true>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, e0, btab_q,
+                             prefix, work_view(w, E), msm_view(mw, p, n, g0), pp, seed, out ? out + E : nullptr,
+                             aligned, fallback_compact(), stream);
+  return launch_part<false>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, e0, btab_q,
+                            prefix, work_view(w, E), msm_view(mw, p, n, g0), pp, seed, out ? out + E : nullptr,
+                            aligned, fallback_compact(), stream);
+}
+
+hipError_t launch_batch_check_tail(bool sr, const uint8_t *pk, const uint8_t *sig, uint32_t n, const fe *btab_q,
+                                   Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
+                                   uint8_t *out, hipStream_t stream, bool after_prep) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  w.niels = mw.pts;
+  if (after_prep) {  // parts ran their prep only: sort and bucket stages over the whole launch first
+    hipError_t e = sr ? launch_sort_buckets<true>(sig, nullptr, nullptr, n, 0u, btab_q, w, mw, p, seed, out, aligned,
+                                                  fallback_compact(), stream)
+                      : launch_sort_buckets<false>(sig, nullptr, nullptr, n, 0u, btab_q, w, mw, p, seed, out, aligned,
+                                                   fallback_compact(), stream);
+    if (e != hipSuccess) return e;
+  }
+  if (sr) return launch_tail<true>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(),
+                                   stream);
+  return launch_tail<false>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(),
+                            stream);
 }
 
 // Key-merged form: one quad per item.  Items [0, n_runs) are runs of one key
@@ -1101,13 +1145,9 @@ hipError_t launch_key_merged_check(bool sr, const uint8_t *pk, const uint8_t *si
 hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                               const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                               const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
-                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream,
-                              const SplitStreams *split) {
-  if (sr)
-    return launch_check<true>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream,
-                              split);
-  return launch_check<false>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream,
-                             split);
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (sr) return launch_check<true>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream);
+  return launch_check<false>(pk, sig, msg, msg_off, idx, count_ptr, n, btab_q, prefix, w, mw, p, seed, out, stream);
 }
 
 hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
@@ -1121,10 +1161,10 @@ hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, cons
   hipError_t e = launch_partition(kind, n, counts, idx_ed, idx_sr, out, stream);
   if (e != hipSuccess) return e;
   e = launch_check<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, m_ed, p, seed_ed, out,
-                          stream, nullptr);
+                          stream);
   if (e != hipSuccess) return e;
   return launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p, seed_sr,
-                            out, stream, nullptr);
+                            out, stream);
 }
 
 }  // namespace tmv

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -54,6 +55,28 @@ void par_memcpy(void *dst, const void *src, size_t n) {
   tmh::parallel_for_n(chunks, 8, [&](size_t c) {
     const size_t lo = c * kChunk, len = std::min(n, lo + kChunk) - lo;
     std::memcpy(static_cast<char *>(dst) + lo, static_cast<const char *>(src) + lo, len);
+  });
+}
+
+// Several staging copies at once, cut into pieces spread over the host pool.
+struct CopySpan {
+  void *dst;
+  const void *src;
+  size_t n;
+};
+void par_memcpy_spans(const CopySpan *sp, size_t count) {
+  const size_t kPiece = size_t(512) << 10;
+  std::vector<std::pair<size_t, size_t>> pieces;  // (span, offset)
+  for (size_t i = 0; i < count; i++)
+    for (size_t o = 0; o < sp[i].n; o += kPiece) pieces.emplace_back(i, o);
+  if (pieces.size() < 4) {
+    for (size_t i = 0; i < count; i++) std::memcpy(sp[i].dst, sp[i].src, sp[i].n);
+    return;
+  }
+  tmh::parallel_for_n(pieces.size(), 16, [&](size_t k) {
+    const CopySpan &c = sp[pieces[k].first];
+    const size_t o = pieces[k].second, len = std::min(c.n, o + kPiece) - o;
+    std::memcpy(static_cast<char *>(c.dst) + o, static_cast<const char *>(c.src) + o, len);
   });
 }
 
@@ -145,9 +168,6 @@ struct KeyIndex {
 struct Workspace {
   DeviceBuf work, work2, idx, msm, msm2, gather;
   hipEvent_t done = nullptr;
-  // helper stream + fork/join events of split batch-equation launches
-  // (created on first use)
-  tmv::SplitStreams split{nullptr, nullptr, nullptr};
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
   const uint8_t *sub_ok[2] = {nullptr, nullptr};  // sub-group verdicts (k_msm_subcheck), if it ran
@@ -163,6 +183,11 @@ struct HostLane {
   hipStream_t stream = nullptr;
   DeviceBuf h_in, d_in, h_out, d_out;
   uint32_t lo = 0, n = 0;  // chunk in flight (n == 0: idle)
+  // streamed batch-equation chunks: the parts' H2D copies run on `copy`,
+  // each followed by an event the kernels of its part wait for (created on
+  // first use)
+  hipStream_t copy = nullptr;
+  std::vector<hipEvent_t> part_ready;
 };
 constexpr int kLanes = 4;  // streams per device; TMV_HOST_LANES of them carry chunks
 
@@ -226,10 +251,17 @@ uint32_t g_host_chunk = 262144;
 uint32_t g_host_lanes = 2;
 // Bound on every wait for device work (TMV_DEVICE_TIMEOUT_MS, 0 = none).
 int64_t g_timeout_ms = 60000;
-// Batch-equation launches of at least this many contiguous entries run
-// their throughput stages as two concurrent halves (tmv::SplitStreams) and
-// keep one latency tail (TMV_SPLIT_MIN, 0 = never).
-uint32_t g_split_min = 0;
+// Streamed host batches (uncached batch equation, one key kind): a chunk's
+// inputs are staged and copied in parts -- the first of g_stream_first
+// entries, then g_stream_part each (rounded to whole groups) -- and each
+// part's throughput kernels start as soon as its copy lands, so one
+// pipeline covers the chunk (one latency tail) while the rest is still
+// being staged (TMV_STREAM_FIRST, TMV_STREAM_PART; TMV_STREAM=0 turns it
+// off).  Such batches are cut into chunks of up to g_stream_chunk entries
+// per device (TMV_STREAM_CHUNK).
+int g_stream = 1;
+bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
+uint32_t g_stream_first = 16384, g_stream_part = 65536, g_stream_chunk = 1u << 21;
 
 void read_env() {
   static std::once_flag once;
@@ -253,8 +285,16 @@ void read_env() {
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
     const char *to = getenv("TMV_DEVICE_TIMEOUT_MS");
     if (to) g_timeout_ms = strtoll(to, nullptr, 10);
-    const char *sm = getenv("TMV_SPLIT_MIN");
-    if (sm) g_split_min = (uint32_t)strtoul(sm, nullptr, 10);
+    const char *st = getenv("TMV_STREAM");
+    if (st) g_stream = atoi(st);
+    const char *smd = getenv("TMV_STREAM_MODE");
+    if (smd) g_stream_prep_only = !strcmp(smd, "prep");
+    const char *sf = getenv("TMV_STREAM_FIRST");
+    if (sf) g_stream_first = std::max<uint32_t>(1, (uint32_t)strtoul(sf, nullptr, 10));
+    const char *sp = getenv("TMV_STREAM_PART");
+    if (sp) g_stream_part = std::max<uint32_t>(1, (uint32_t)strtoul(sp, nullptr, 10));
+    const char *sc = getenv("TMV_STREAM_CHUNK");
+    if (sc) g_stream_chunk = std::max<uint32_t>(2048, (uint32_t)strtoul(sc, nullptr, 10));
   });
 }
 
@@ -714,24 +754,46 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
   return &w;
 }
 
+// Stages the inputs of entries [e0, e1) of a streamed launch and makes the
+// launch stream wait for their copy (stage_and_launch); 0 or < 0.
+using PartFeeder = std::function<int(uint32_t e0, uint32_t e1)>;
+
+// Part boundaries of a streamed launch of n entries: whole groups, the first
+// part g_stream_first entries, then g_stream_part each.
+static std::vector<uint32_t> stream_parts(uint32_t n, uint32_t m) {
+  std::vector<uint32_t> b{0};
+  uint32_t want = g_stream_first;
+  while (b.back() < n) {
+    const uint64_t e1 = std::min<uint64_t>(n, ((uint64_t)b.back() + want + m - 1) / m * m);
+    b.push_back((uint32_t)e1);
+    want = g_stream_part;
+  }
+  return b;
+}
+
 static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *pk, const uint8_t *sig,
-                       const uint8_t *msg, const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s) {
+                       const uint8_t *msg, const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s,
+                       const PartFeeder *feed = nullptr) {
   int rc;
   Workspace *ws = reserve_work(d, n, false, s, &rc, &o.p);
   if (!ws) return rc;
   tmv::Ed25519Work w = tmv::Ed25519Work::carve(ws->work.ptr, n);
   tmv::MsmWork mw = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
-  read_env();
-  const tmv::SplitStreams *split = nullptr;
-  if (g_split_min && n >= g_split_min) {
-    tmv::SplitStreams &sp = ws->split;
-    if (!sp.helper && hipStreamCreateWithFlags(&sp.helper, hipStreamNonBlocking) != hipSuccess) sp.helper = nullptr;
-    if (sp.helper && !sp.fork && hipEventCreateWithFlags(&sp.fork, hipEventDisableTiming) != hipSuccess) sp.fork = nullptr;
-    if (sp.helper && !sp.join && hipEventCreateWithFlags(&sp.join, hipEventDisableTiming) != hipSuccess) sp.join = nullptr;
-    if (sp.helper && sp.fork && sp.join) split = &sp;  // else: one stream
+  hipError_t e;
+  if (feed) {  // parts as their inputs land, then one tail
+    const std::vector<uint32_t> b = stream_parts(n, o.p.m());
+    for (size_t j = 0; j + 1 < b.size(); j++) {
+      if ((rc = (*feed)(b[j], b[j + 1])) != 0) return rc;
+      e = tmv::launch_batch_check_part(sr, pk, sig, msg, off, n, b[j], b[j + 1], d.d_btab_q, d.d_prefix, w, mw, o.p,
+                                       o.seed[sr ? 1 : 0], out, s, g_stream_prep_only);
+      if (e != hipSuccess) { set_error("batch check part launch", e); return TMV_ERR_LAUNCH; }
+    }
+    e = tmv::launch_batch_check_tail(sr, pk, sig, n, d.d_btab_q, w, mw, o.p, o.seed[sr ? 1 : 0], out, s,
+                                     g_stream_prep_only);
+  } else {
+    e = tmv::launch_batch_check(sr, pk, sig, msg, off, nullptr, nullptr, n, d.d_btab_q, d.d_prefix, w, mw, o.p,
+                                o.seed[sr ? 1 : 0], out, s);
   }
-  hipError_t e = tmv::launch_batch_check(sr, pk, sig, msg, off, nullptr, nullptr, n, d.d_btab_q, d.d_prefix, w, mw,
-                                         o.p, o.seed[sr ? 1 : 0], out, s, split);
   if (e != hipSuccess) { set_error("batch check launch", e); return TMV_ERR_LAUNCH; }
   ws->group_ok[0] = mw.group_ok;
   ws->group_ok[1] = nullptr;
@@ -882,6 +944,11 @@ void tmv_close(tmv_ctx *ctx) {
     if (d->faulted) continue;  // work still running on its buffers: leak them rather than free them under it
     for (HostLane &l : d->lane) {
       if (l.stream) (void)hipStreamSynchronize(l.stream);
+      if (l.copy) (void)hipStreamSynchronize(l.copy);
+      for (hipEvent_t ev : l.part_ready) (void)hipEventDestroy(ev);
+      l.part_ready.clear();
+      if (l.copy) (void)hipStreamDestroy(l.copy);
+      l.copy = nullptr;
       l.d_in.release();
       l.d_out.release();
       l.h_in.release();
@@ -896,11 +963,6 @@ void tmv_close(tmv_ctx *ctx) {
       kv.second->msm2.release();
       kv.second->gather.release();
       if (kv.second->done) (void)hipEventDestroy(kv.second->done);
-      const tmv::SplitStreams &sp = kv.second->split;
-      if (sp.helper) (void)hipStreamSynchronize(sp.helper);
-      if (sp.fork) (void)hipEventDestroy(sp.fork);
-      if (sp.join) (void)hipEventDestroy(sp.join);
-      if (sp.helper) (void)hipStreamDestroy(sp.helper);
     }
     d->ws.clear();
     d->d_kbuild.release();
@@ -984,6 +1046,61 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     if ((uint64_t)distinct + o.p.groups > n / 2) merged = false;
   }
   if (cached && !merged) o.batch_eq = false;  // key-cached per-entry path
+  read_env();
+  if (g_stream && !cached && !vs && (sch == Scheme::Ed25519 || sch == Scheme::Sr25519) && o.batch_eq &&
+      n > g_stream_first) {
+    // streamed: stage and copy part by part, each part's kernels behind its copy
+    if ((e = ln.h_in.ensure(L.total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+    if ((e = ln.d_in.ensure(L.total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+    if ((e = ln.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+    if ((e = ln.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+    if (!ln.copy && (e = hipStreamCreateWithFlags(&ln.copy, hipStreamNonBlocking)) != hipSuccess) {
+      ln.copy = nullptr;
+      set_error("hipStreamCreate", e);
+      return TMV_ERR_NO_DEVICE;
+    }
+    uint8_t *h = static_cast<uint8_t *>(ln.h_in.ptr), *dd = static_cast<uint8_t *>(ln.d_in.ptr);
+    uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
+    const uint32_t base = msg_off[lo];
+    size_t part = 0;
+    const PartFeeder feed = [&](uint32_t a, uint32_t b) -> int {
+      for (uint32_t i = a; i <= b; i++) off[i] = msg_off[lo + i] - base;
+      const size_t m0 = off[a], m1 = off[b];
+      const CopySpan sp[3] = {{h + L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a)},
+                              {h + L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a)},
+                              {h + L.msg + m0, msg + base + m0, m1 - m0}};
+      par_memcpy_spans(sp, 3);
+      if (part >= ln.part_ready.size()) {
+        hipEvent_t ev;
+        hipError_t ce = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (ce != hipSuccess) { set_error("hipEventCreate", ce); return TMV_ERR_NO_DEVICE; }
+        ln.part_ready.push_back(ev);
+      }
+      hipEvent_t ev = ln.part_ready[part++];
+      hipError_t ce;
+      const size_t offs[4][2] = {{L.pk + 32ull * a, 32ull * (b - a)}, {L.sig + 64ull * a, 64ull * (b - a)},
+                                 {L.off + 4ull * a, 4ull * (b - a + 1)}, {L.msg + m0, m1 - m0}};
+      for (const auto &c : offs)
+        if (c[1] && (ce = hipMemcpyAsync(dd + c[0], h + c[0], c[1], hipMemcpyHostToDevice, ln.copy)) != hipSuccess) {
+          set_error("hipMemcpyAsync(H2D)", ce);
+          return TMV_ERR_LAUNCH;
+        }
+      if ((ce = hipEventRecord(ev, ln.copy)) != hipSuccess || (ce = hipStreamWaitEvent(ln.stream, ev, 0)) != hipSuccess) {
+        set_error("part event", ce);
+        return TMV_ERR_LAUNCH;
+      }
+      return 0;
+    };
+    tm.mark("stage", n);
+    const int rc = batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off),
+                               n, static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed);
+    if (rc != 0) return rc;
+    if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
+      set_error("hipMemcpyAsync(D2H)", e);
+      return TMV_ERR_LAUNCH;
+    }
+    return 0;
+  }
   const uint32_t G = merged ? o.p.groups : 0;
   const size_t kind_at = L.total;
   const size_t votes_at = L.total + (sch == Scheme::Mixed ? align16(n) : 0) + (cached ? align16(4ull * n) : 0);
@@ -1057,7 +1174,6 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
   // Small key-cached batches (the VerifyCommit latency path) skip both
   // copies: the fused kernel reads the pinned staging and writes the
   // statuses to pinned memory over PCIe (coherent host memory).
-  read_env();
   const bool zero_copy = g_zero_copy && cached && !merged && !vs && n <= g_cached_fused_max && ln.h_in.dev &&
                          ln.h_out.dev;
   uint8_t *dd = static_cast<uint8_t *>(zero_copy ? ln.h_in.dev : ln.d_in.ptr);
@@ -1128,7 +1244,14 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     return TMV_ERR_ARG;
   }
   read_env();
-  const tmh::ShardPlan plan = tmh::plan_shards(n, (uint32_t)ctx->devs.size(), g_host_chunk);
+  // streamed batch-equation chunks are large (one pipeline, one tail each);
+  // other paths alternate smaller chunks over the lanes
+  const uint32_t per_dev = n / (uint32_t)ctx->devs.size();
+  const bool streamable = g_stream && !vs && (sch == Scheme::Ed25519 || sch == Scheme::Sr25519) &&
+                          !(flags & TMV_FLAG_PER_ENTRY) &&
+                          ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
+  const tmh::ShardPlan plan =
+      tmh::plan_shards(n, (uint32_t)ctx->devs.size(), streamable ? g_stream_chunk : g_host_chunk);
   const uint32_t shards = plan.shards;
   std::vector<std::unique_lock<std::mutex>> locks;
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);

@@ -66,20 +66,29 @@ hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uin
                                uint32_t *idx_sr, int8_t *status, hipStream_t stream);
 
 // Batch-equation pipeline (msm.h): k_prep -> k_msm_sort -> k_msm_accum ->
-// k_msm_group -> k_verify_quad over the failed groups only.  Single key kind
-// (sr = false: ed25519, true: sr25519); idx/count_ptr as for the mixed path.
-// split (optional, contiguous batches): a helper stream and two events; the
-// two halves of the groups run their throughput stages concurrently, forked
-// from and joined back into `stream`, before one Horner and one fallback.
-struct SplitStreams {
-  hipStream_t helper;
-  hipEvent_t fork, join;
-};
+// k_msm_wpart -> k_msm_wsum -> k_msm_horner -> k_verify_quad over the failed
+// groups only.  Single key kind (sr = false: ed25519, true: sr25519);
+// idx/count_ptr as for the mixed path.
 hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                               const uint32_t *msg_off, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                               const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
-                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream,
-                              const SplitStreams *split = nullptr);
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream);
+// The same launch in pieces, for inputs that arrive in parts (the streamed
+// host path): the throughput stages (prep, sort, bucket and window sums) of
+// entries [e0, e1) of a contiguous n-entry launch -- e0 a multiple of the
+// group size, e1 too unless e1 = n -- once those entries are in device
+// memory, then, after every part, the latency stages of the whole launch
+// (Horner, located / per-entry fallback).  Parts may be enqueued on the
+// stream one by one, each behind its own copy.  prep_only: a part runs its
+// prep only, and the tail (after_prep) runs the sort and bucket stages over
+// the whole launch before Horner.
+hipError_t launch_batch_check_part(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                   const uint32_t *msg_off, uint32_t n, uint32_t e0, uint32_t e1, const fe *btab_q,
+                                   const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                                   const MsmSeed &seed, uint8_t *out, hipStream_t stream, bool prep_only = false);
+hipError_t launch_batch_check_tail(bool sr, const uint8_t *pk, const uint8_t *sig, uint32_t n, const fe *btab_q,
+                                   Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
+                                   uint8_t *out, hipStream_t stream, bool after_prep = false);
 // Mixed batch through the batch equation: partition, then one pipeline per kind.
 hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                     const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,

@@ -1,7 +1,10 @@
 """Host-buffer pipeline: batches of at least two chunks (TMV_HOST_CHUNK)
 alternate between two staging lanes, so chunk k+1's staging and copy overlap
-chunk k's kernels.  Every path must still give the oracle's vector, in
-order, across chunk edges, with key builds and evictions between chunks."""
+chunk k's kernels; uncached batch-equation batches are streamed instead (one
+pipeline per chunk, inputs staged and copied in parts, each part's kernels
+behind its copy: TMV_STREAM_FIRST / TMV_STREAM_PART).  Every path must still
+give the oracle's vector, in order, across chunk and part edges, with key
+builds and evictions between chunks."""
 import os
 import subprocess
 import sys
@@ -45,6 +48,8 @@ ok, st = ctx.verify_batch_ex(SR, N.TMV_FLAG_KEY_CACHE, s.pk, s.sig, s.msg, s.off
 assert np.array_equal(st, sref)
 ok, st = ctx.sr25519_verify_batch(s.pk, s.sig, s.msg, s.off)
 assert np.array_equal(st, sref)
+ok, st = ctx.verify_batch_ex(SR, N.TMV_FLAG_BATCH_EQUATION, s.pk, s.sig, s.msg, s.off)
+assert np.array_equal(st, sref)
 
 # device-built vote messages, chunked
 rng = random.Random(84)
@@ -68,12 +73,44 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("chunk,capacity", [("2048", "4096"), ("3000", "100")])
-def test_chunked_host_batches(chunk, capacity):
+@pytest.mark.parametrize("chunk,capacity,extra", [
+    ("2048", "4096", {}),
+    ("3000", "100", {"TMV_STREAM": "0"}),  # batch equation chunked over the lanes
+    ("2048", "4096", {"TMV_STREAM_FIRST": "1000", "TMV_STREAM_PART": "3000"}),  # streamed in parts
+], ids=["default", "lanes", "streamed"])
+def test_chunked_host_batches(chunk, capacity, extra):
     """Capacity 100 < the keyed batch's 150 keys: that batch takes the
     uncached path; the votes' 61 keys fit and evict slots between calls."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, TMV_HOST_CHUNK=chunk, TMV_KEY_CACHE_CAPACITY=capacity)
+    env = dict(os.environ, TMV_HOST_CHUNK=chunk, TMV_KEY_CACHE_CAPACITY=capacity, **extra)
     out = subprocess.run([sys.executable, "-c", CODE], env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "ok" in out.stdout
+
+
+BIG = r"""
+import json, sys, numpy as np
+sys.path.insert(0, '.')
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import Batch, make_c2_batch
+gold = json.load(open('tests/golden/c2_expected.json'))
+bits = np.unpackbits(np.frombuffer(bytes.fromhex(gold['valid_bits_hex']), np.uint8), bitorder='little')[:10000]
+b = make_c2_batch(10000)
+ctx = N.Context(1)
+for reps in (20, 3):  # 200k: parts of 16k + 3 x 64k + a ragged tail; 30k: two parts
+    hb = Batch.concat([b] * reps)
+    for _ in range(2):
+        ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, hb.pk, hb.sig, hb.msg, hb.off)
+        assert np.array_equal(st.astype(np.uint8), np.tile(bits, reps)), reps
+print("ok")
+"""
+
+
+def test_streamed_c2_host_batches():
+    """The driver-sized host batch (BASELINE C2 tiled to 200k and 30k entries)
+    streamed with the default parts: the vector equals the committed C2
+    bitmap repeated, twice in a row on the same lane."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", BIG], cwd=root, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "ok" in out.stdout

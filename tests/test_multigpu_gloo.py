@@ -128,12 +128,15 @@ def test_bench_control_flow_world2():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"), "--gpus", "2",
-           "--steps", "7", "--warmup", "2", "--batch", "500", "--resident", "3", "--inflight", "2", "--cpu-stub"]
+           "--steps", "7", "--warmup", "2", "--batch", "500", "--resident", "3", "--inflight", "2",
+           "--batches-per-step", "3", "--cpu-stub"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=repo)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
-    assert r["config"]["parallelism"] == "shard2" and sum(r["config"]["launch_sizes"]) >= 1
+    assert r["config"]["parallelism"] == "shard2" and r["config"]["batches_per_step"] == 3
+    # value = every rank's signatures: 2 ranks x 7 steps x 3 batches x 500
+    assert abs(r["value"] * r["ms_per_step"] * 7e-3 / (2 * 7 * 3 * 500) - 1) < 1e-3
     assert "STUB" in r["data"]
