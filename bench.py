@@ -117,6 +117,56 @@ def _pmc_kernels(method: str):
     return out or None
 
 
+TIMED_KERNELS = ("k_msm_accum", "k_msm_wpart", "k_prep_fused")
+# k_msm_accum's algorithmic work: one mixed (Niels) addition per bucket entry,
+# 7 field multiplications (ge_madd 3 + p1p1->p3 4) x 100 int32 products.
+ACCUM_PRODUCTS_PER_ENTRY = 7 * 100
+
+
+def accum_entries_per_sig(m: int = 64, c: int = 5, samples: int = 4000, seed: int = 1) -> float:
+    """Expected bucket entries per signature of the batch equation (msm.h):
+    the nonzero signed c-bit digits of a uniform 128-bit weight z (R term, 129
+    bits of windows) and of a uniform scalar mod l (A term, 254 bits), plus
+    the group's B scalar shared by m signatures -- simulated with the device's
+    recoding (msm_kernels.hip window_digit)."""
+    import random
+    l_order = 2**252 + 27742317777372353535851937790883648493
+    rng = random.Random(seed)
+
+    def nonzero(x, windows):
+        cnt, carry = 0, 0
+        for w in range(windows):
+            d = ((x >> (w * c)) & ((1 << c) - 1)) + carry
+            if w + 1 < windows and d >= 1 << (c - 1):
+                d -= 1 << c
+                carry = 1
+            else:
+                carry = 0
+            cnt += d != 0
+        return cnt
+    wr, w = -(-129 // c), -(-254 // c)
+    tot = 0
+    for _ in range(samples):
+        tot += nonzero(rng.getrandbits(128), wr) + nonzero(rng.randrange(l_order), w)
+    return tot / samples + nonzero(rng.randrange(l_order), w) / m
+
+
+def _rocprof_avg_ms(kernel_prefix: str):
+    """Average duration of a kernel in the committed rocprofv3 --stats summary
+    of the bench (newest round first)."""
+    import csv
+    for d in ("r03", "r02"):
+        path = os.path.join(REPO, "profiles", d, "bench_kernel_stats.csv")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Name"].replace("void ", "").replace("tmv::", "").startswith(kernel_prefix):
+                    return {"avg_ms": round(float(row["AverageNs"]) / 1e6, 4), "calls": int(row["Calls"]),
+                            "source": f"profiles/{d}/bench_kernel_stats.csv"}
+    return None
+
+
 def host_cpu_info():
     """The cores this process may use (affinity and cgroup CPU quota), the
     machine's CPU count and model."""
@@ -348,10 +398,18 @@ def main():
         dist.barrier()
     evs = [(Event(enable_timing=True), Event(enable_timing=True)) for _ in sizes]
     sync(dev)
+    if ctx is not None:  # live HIP-event timing of the hot kernels (roofline.dominant_kernel)
+        for k in TIMED_KERNELS:
+            ctx.kernel_timing_read(k)  # drop earlier records
+        ctx.kernel_timing(True)
     t0 = time.perf_counter()
     n_batches = run(sizes, evs)
     steps = len(sizes)
     sync(dev)
+    ktimes = {}
+    if ctx is not None:
+        ctx.kernel_timing(False)
+        ktimes = {k: ctx.kernel_timing_read(k) for k in TIMED_KERNELS}
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -376,15 +434,19 @@ def main():
         elapsed = float(t.item())
 
     extras = {}
+    ktimes_alone = {}
     if rank == 0 and not args.no_extras and not stub:
         # one launch of K batches alone on one stream (no overlap): the
         # pipeline's own duration, HIP events on its stream
         alone = []
+        ctx.kernel_timing(True)
         for _ in range(5):
             e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             launch(0, 0, K, e)
             torch.cuda.synchronize(dev)
             alone.append(e[0].elapsed_time(e[1]))
+        ctx.kernel_timing(False)
+        ktimes_alone.update({k: ctx.kernel_timing_read(k) for k in TIMED_KERNELS})
         extras["launch_alone_ms"] = round(statistics.median(alone), 4)
         # single-batch latency (one batch per launch, one at a time)
         lat = []
@@ -477,6 +539,47 @@ def main():
                          "executed": pmc.get("executed"),
                          "pmc_kernels": _pmc_kernels(args.method)},
         }
+        ex = pmc.get("executed") or {}
+        if ex.get("int64_lane_ops_per_sig"):
+            result["roofline"]["executed_frac"] = round(gpu_rate * ex["int64_lane_ops_per_sig"] / peak, 4)
+            result["roofline"]["executed_frac_note"] = (
+                "verifies/s x PMC SQ_INSTS_VALU_INT64 lane-ops per signature / peak v_mad_i64_i32 rate: the 64-bit "
+                "VALU ops executed (multiply products plus 64-bit carry adds/shifts) as a share of the multiply peak; "
+                "an upper bound on the multiply share, independent of the canonical work figure")
+        if ktimes.get("k_msm_accum", (0, 0))[1] and args.method == "batch":
+            ms, cnt = ktimes["k_msm_accum"]
+            avg = ms / cnt
+            per_launch = K * n * accum_entries_per_sig(c=args.window or 5) * ACCUM_PRODUCTS_PER_ENTRY
+            acc = per_launch / (avg * 1e-3)
+            kp = pmc.get("kernels", {}).get("tmv::k_msm_accum<16>", {})
+            alone = ktimes_alone.get("k_msm_accum", (0, 0))
+            dk = {"kernel": "k_msm_accum<16> (bucket sums; the largest share of the pipeline's VALU work)",
+                  "avg_launch_ms": round(avg, 4), "launches": cnt,
+                  "timing": "HIP events on the launch's stream around every k_msm_accum launch of the timed region "
+                            "(tmv_kernel_timing); launches in flight share the chip, so this is the kernel's "
+                            "duration under the bench's overlap",
+                  "avg_launch_ms_alone": round(alone[0] / alone[1], 4) if alone[1] else None,
+                  "algorithmic_products_per_launch": round(per_launch),
+                  "algorithmic_note": f"{K} x {n} signatures x expected bucket entries per signature (nonzero signed "
+                                      "5-bit digits of z and z k mod l, + the group's B scalar; simulated recoding) x "
+                                      "7 field multiplications x 100 int32 products",
+                  "achieved": round(acc / 1e12, 4), "peak": round(peak / 1e12, 4), "unit": "Tmul/s",
+                  "frac": round(acc / peak, 4),
+                  "frac_alone": round(per_launch / (alone[0] / alone[1] * 1e-3) / peak, 4) if alone[1] else None,
+                  "other_kernels_avg_ms": {k: round(v[0] / v[1], 4) for k, v in ktimes.items()
+                                           if v[1] and k != "k_msm_accum"},
+                  "rocprof": _rocprof_avg_ms("k_msm_accum")}
+            if kp.get("SQ_INSTS_VALU_INT64"):
+                scale = K / pmc.get("batches_per_launch", 32)
+                dk["executed_int64_lane_ops_per_launch"] = int(kp["SQ_INSTS_VALU_INT64"] * 64 * scale)
+                dk["executed_frac"] = round(dk["executed_int64_lane_ops_per_launch"] / (avg * 1e-3) / peak, 4)
+                if alone[1]:
+                    dk["executed_frac_alone"] = round(
+                        dk["executed_int64_lane_ops_per_launch"] / (alone[0] / alone[1] * 1e-3) / peak, 4)
+                dk["traffic_bytes_per_launch"] = int((kp.get("hbm_read_bytes", 0) + kp.get("hbm_write_bytes", 0)) *
+                                                     scale)
+                dk["traffic_GBps"] = round(dk["traffic_bytes_per_launch"] / (avg * 1e-3) / 1e9, 1)
+            result["roofline"]["dominant_kernel"] = dk
         if stub:
             result["data"] = "CPU STUB (--cpu-stub): control-flow check only, no verification, not a measurement"
         if world == 1 and not args.no_cpu_baseline and not stub:

@@ -166,6 +166,17 @@ int tmv_verify_mixed_batch_ex(tmv_ctx *ctx, uint32_t flags, const uint8_t *kind,
                               const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off, uint32_t n,
                               int8_t *status_out);
 
+/* Live kernel timing (profiling aid; bench.py's roofline object).  enable != 0:
+ * every later launch of the timed kernels -- "k_msm_accum" (batch-equation
+ * bucket sums), "k_msm_wpart" (window running sums), "k_prep_fused" (decode +
+ * challenge) -- is bracketed by HIP timing events on the stream it runs on
+ * (process-wide, two event records per launch); 0 turns it off.
+ * tmv_kernel_timing_read waits for the recorded launches of `kernel`, returns
+ * their summed duration and count, and forgets them.  No reference
+ * counterpart (Go's benchmarks time whole calls). */
+int tmv_kernel_timing(tmv_ctx *ctx, int enable);
+int tmv_kernel_timing_read(tmv_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches);
+
 /* Cumulative key-cache counters over the context's devices. */
 int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t *used, uint32_t *capacity);
 

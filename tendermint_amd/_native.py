@@ -46,6 +46,7 @@ EXPORTS = [
     "tmv_subgroup_stats", "tmv_validator_set_hashes",
     "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
     "tmv_verify_votes", "tmv_vote_sign_bytes_device", "tmv_merkle_roots",
+    "tmv_kernel_timing", "tmv_kernel_timing_read",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_vote_template_encode", "tmv_verify_commit", "tmv_verify_commits",
@@ -124,6 +125,9 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.tmv_set_batch_options.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p, ctypes.c_uint32]
         L.tmv_batch_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.tmv_kernel_timing.argtypes = [vp, ctypes.c_int]
+        L.tmv_kernel_timing_read.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_uint64)]
         L.tmv_subgroup_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.tmv_validator_set_hashes.argtypes = [vp, u8p, u8p, ctypes.POINTER(ctypes.c_int64), u32p,
                                                ctypes.c_uint32, u8p]
@@ -278,6 +282,19 @@ class Context:
                                                              _p(off, ctypes.c_uint32), n, _p(out, ctypes.c_int8)),
                          "tmv_verify_mixed_batch_ex")
         return rc == TMV_ALL_VALID, out[:n]
+
+    def kernel_timing(self, enable: bool) -> None:
+        """Bracket later launches of the timed kernels with HIP timing events
+        on their streams (tmv_kernel_timing)."""
+        self._check(self._lib.tmv_kernel_timing(self._h, 1 if enable else 0), "tmv_kernel_timing")
+
+    def kernel_timing_read(self, kernel: str) -> tuple[float, int]:
+        """(summed duration in ms, launches) of `kernel` since the last read
+        (tmv_kernel_timing_read; waits for the recorded launches)."""
+        ms, cnt = ctypes.c_double(0), ctypes.c_uint64(0)
+        self._check(self._lib.tmv_kernel_timing_read(self._h, kernel.encode(), ctypes.byref(ms), ctypes.byref(cnt)),
+                    "tmv_kernel_timing_read")
+        return ms.value, cnt.value
 
     def set_batch_options(self, group_log2: int = 0, window_bits: int = 0, seed: bytes | None = None,
                           stats: bool = False) -> None:

@@ -22,7 +22,8 @@
 //   k_msm_wpart  one lane per (group, window, part): running sums over the
 //                part's H/P buckets (bucket values merge chunk partials)
 //   k_msm_wsum   one lane per (group, window): joins the P parts into the
-//                window sum S_w = sum_j (j+1) bucket_j
+//                window sum S_w = sum_j (j+1) bucket_j (P > 1 only: with one
+//                lane per window its T is S_w)
 //   k_msm_horner one quad per group: T_g = sum_w 2^(c w) S_w (Horner, quad-lane
 //                arithmetic) and the group verdict
 //
@@ -45,6 +46,7 @@
 
 namespace tmv {
 
+constexpr uint32_t kMsmWideRows = 65536;     // (group, window) rows from which k_msm_wpart runs one lane per window
 constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 8, 16 or 32
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
@@ -99,6 +101,12 @@ struct MsmParams {
       const uint32_t chain = 2 * (p.H / P) + 3 * P + lg;
       if (chain < best) { best = chain; p.P = P; }
     }
+    // a launch with this many (group, window) rows is throughput-bound: one
+    // lane per window does the fewest additions (2 H, no joins; the parts
+    // cost 2 H + ~3 P + log2(H / P) per window) and the window sums are the
+    // lanes' T, so k_msm_wsum is skipped.  C2 bench: 82.9 / 84.1 (P = 4) ->
+    // 85.0 / 86.2 M/s (P = 1), profiles/r03/ab_parts.txt
+    if ((uint64_t)p.groups * p.W >= kMsmWideRows) p.P = 1;
     return p;
   }
 };

@@ -12,9 +12,86 @@
 #include "kernel_util.h"
 #include "comb.h"
 #include "quad.h"
+#include "ktimer.h"
 #include "verify_kernels.h"
 
+#include <atomic>
+#include <mutex>
+#include <vector>
+
 namespace tmv {
+
+namespace ktimer {
+namespace {
+struct Pair {
+  int k;
+  hipEvent_t a, b;
+};
+std::atomic<bool> g_on{false};
+std::mutex g_mu;
+std::vector<Pair *> g_done[kCount];  // recorded pairs per kernel
+std::vector<hipEvent_t> g_free;      // recycled timing events
+hipEvent_t take_event() {
+  hipEvent_t e = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_free.empty()) { e = g_free.back(); g_free.pop_back(); }
+  }
+  if (!e && hipEventCreate(&e) != hipSuccess) e = nullptr;
+  return e;
+}
+}  // namespace
+
+void set(bool on) { g_on.store(on); }
+bool on() { return g_on.load(std::memory_order_relaxed); }
+
+void *begin(Kernel k, hipStream_t s) {
+  if (!on()) return nullptr;
+  Pair *p = new Pair{k, take_event(), take_event()};
+  if (!p->a || !p->b || hipEventRecord(p->a, s) != hipSuccess) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (p->a) g_free.push_back(p->a);
+    if (p->b) g_free.push_back(p->b);
+    delete p;
+    return nullptr;
+  }
+  return p;
+}
+
+void end(void *token, hipStream_t s) {
+  if (!token) return;
+  Pair *p = static_cast<Pair *>(token);
+  (void)hipEventRecord(p->b, s);
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_done[p->k].push_back(p);
+}
+
+int read(Kernel k, double *ms, uint64_t *launches) {
+  std::vector<Pair *> v;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    v.swap(g_done[k]);
+  }
+  int rc = 0;
+  for (Pair *p : v) {
+    float t = 0.f;
+    hipError_t e = hipEventSynchronize(p->b);
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, p->a, p->b);
+    if (e == hipSuccess) {
+      *ms += t;
+      *launches += 1;
+    } else if (!rc) {
+      rc = (int)e;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_free.push_back(p->a);
+    g_free.push_back(p->b);
+    delete p;
+  }
+  return rc;
+}
+
+}  // namespace ktimer
 
 namespace {
 
@@ -459,15 +536,18 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
   const bool live = raw < live_groups;
   const uint32_t g = live ? raw : live_groups - 1;  // whole quads stay active for DPP
   const int c = (int)(threadIdx.x & 3);
-  const ge_p3 *S = mw.wsum + (size_t)g * p.W;
-  fe acc = reinterpret_cast<const fe *>(&S[p.W - 1])[c];
+  // one running-sum lane per window (P = 1): its T is the window sum, read
+  // in place (k_msm_wsum does not run)
+  const uint32_t st = p.P == 1 ? 2 : 1;
+  const ge_p3 *S = p.P == 1 ? mw.wpart + 2ull * g * p.W : mw.wsum + (size_t)g * p.W;
+  fe acc = reinterpret_cast<const fe *>(&S[st * (p.W - 1)])[c];
   fe r, q, qc;
   for (int wI = (int)p.W - 2; wI >= 0; wI--) {
     for (uint32_t d = 0; d < p.c; d++) {
       quad::dbl(r, acc);
       quad::p1p1_to_p3(acc, r);
     }
-    q = reinterpret_cast<const fe *>(&S[wI])[c];
+    q = reinterpret_cast<const fe *>(&S[st * wI])[c];
     quad::to_cached(qc, q);
     quad::add(r, acc, qc);
     quad::p1p1_to_p3(acc, r);
@@ -786,6 +866,7 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
                                  hipStream_t stream) {
   const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
   const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
+  void *tk = ktimer::begin(ktimer::kAccum, stream);
   if (p.L == 8)
     hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   else if (p.L == 16)
@@ -794,9 +875,13 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
     hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   hipError_t e;
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  ktimer::end(tk, stream);
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
+  tk = ktimer::begin(ktimer::kWpart, stream);
   hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  ktimer::end(tk, stream);
+  if (p.P == 1) return hipSuccess;  // the parts are the window sums
   const uint64_t rows = (uint64_t)p.groups * p.W;
   hipLaunchKernelGGL(k_msm_wsum, dim3((uint32_t)((rows + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
   return hipGetLastError();

@@ -31,6 +31,7 @@
 #include "host/pool.h"
 #include "host/shard_plan.h"
 #include "host/wait.h"
+#include "ktimer.h"
 #include "verify_kernels.h"
 #include "votes.h"
 #include "valset.h"
@@ -237,6 +238,7 @@ int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
 // the batch check does 2-3x less work.  Flags override per call.
 uint32_t g_msm_min = 16384;
 uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk length (A/B measurement)
+uint32_t g_msm_parts = 0;  // TMV_MSM_PARTS: running-sum lanes per window (power of two <= H; A/B measurement)
 // Key-cached batches up to this size run as one fused latency kernel
 // (TMV_CACHED_FUSED_MAX; commit-sized calls such as VerifyCommit).
 uint32_t g_cached_fused_max = 4096;
@@ -261,7 +263,10 @@ int64_t g_timeout_ms = 60000;
 // per device (TMV_STREAM_CHUNK).
 int g_stream = 1;
 bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
-uint32_t g_stream_first = 16384, g_stream_part = 65536, g_stream_chunk = 1u << 21;
+// 320k C2 entries end to end (tools/gpu_stream_check.sh): 6.0-6.4 ms with
+// parts of 16k / 64k, 5.9-6.0 ms with 32k / 128k, 6.7 with 64k / 256k,
+// 6.9 ms unstreamed (two lanes of 80k chunks)
+uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 21;
 
 void read_env() {
   static std::once_flag once;
@@ -281,6 +286,8 @@ void read_env() {
     if (hc) g_host_chunk = (uint32_t)strtoul(hc, nullptr, 10);
     const char *hl = getenv("TMV_HOST_LANES");
     if (hl) g_host_lanes = std::min<uint32_t>(kLanes, std::max<uint32_t>(1, (uint32_t)strtoul(hl, nullptr, 10)));
+    const char *mp = getenv("TMV_MSM_PARTS");
+    if (mp) g_msm_parts = (uint32_t)strtoul(mp, nullptr, 10);
     const char *mc = getenv("TMV_MSM_CHUNK");
     if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
     const char *to = getenv("TMV_DEVICE_TIMEOUT_MS");
@@ -363,6 +370,7 @@ tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged =
   c = std::max<uint32_t>(4, std::min<uint32_t>(9, c));
   tmv::MsmParams p = tmv::MsmParams::make(n, m_log2, c, merged);
   if (g_msm_chunk == 8 || g_msm_chunk == 16 || g_msm_chunk == 32) p.L = g_msm_chunk;
+  if (g_msm_parts && g_msm_parts <= p.H && !(g_msm_parts & (g_msm_parts - 1))) p.P = g_msm_parts;
   return p;
 }
 
@@ -910,6 +918,26 @@ static int launch_ed25519(Device &d, const LaunchOpts &o, const uint8_t *pk, con
 }
 
 extern "C" {
+
+int tmv_kernel_timing(tmv_ctx *ctx, int enable) {
+  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
+  tmv::ktimer::set(enable != 0);
+  return 0;
+}
+
+int tmv_kernel_timing_read(tmv_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches) {
+  if (!ctx || !kernel || !total_ms || !launches) { set_error("null argument"); return TMV_ERR_ARG; }
+  tmv::ktimer::Kernel k;
+  if (!strcmp(kernel, "k_msm_accum")) k = tmv::ktimer::kAccum;
+  else if (!strcmp(kernel, "k_msm_wpart")) k = tmv::ktimer::kWpart;
+  else if (!strcmp(kernel, "k_prep_fused")) k = tmv::ktimer::kPrep;
+  else { set_error("unknown timed kernel"); return TMV_ERR_ARG; }
+  *total_ms = 0;
+  *launches = 0;
+  const int e = tmv::ktimer::read(k, total_ms, launches);
+  if (e) { set_error("hipEventElapsedTime", (hipError_t)e); return TMV_ERR_LAUNCH; }
+  return 0;
+}
 
 const char *tmv_last_error(void) { return g_last_error.c_str(); }
 const char *tmv_version(void) { return "tmverify-mi355x 0.1 (gfx950)"; }

@@ -15,6 +15,7 @@
 #include "verify_kernels.h"
 #include "kernel_util.h"
 #include "comb.h"
+#include "ktimer.h"
 
 namespace tmv {
 
@@ -839,9 +840,12 @@ hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg
   const uint32_t dblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
   const uint32_t hblocks = (n + kVerifyBlock - 1) / kVerifyBlock;
   if (prep_fused()) {
+    void *tk = ktimer::begin(ktimer::kPrep, stream);
     hipLaunchKernelGGL(k_prep_fused<SR>, dim3(dblocks + hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off,
                        idx, count_ptr, n, w, prefix, aligned, dblocks);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    ktimer::end(tk, stream);
+    return e;
   }
   hipLaunchKernelGGL(k_prep_decode<SR>, dim3(dblocks), dim3(kVerifyBlock), 0, stream, pk, sig, idx, count_ptr, n, w,
                      aligned);
