@@ -78,7 +78,7 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-PMC_DIRS = ("r02", "r01_close")  # newest first
+PMC_DIRS = ("r02_close", "r02", "r01_close")  # newest first
 
 
 def _load_pmc(method: str, batches_per_step: int = 32):
@@ -155,7 +155,7 @@ def _rocprof_avg_ms(kernel_prefix: str):
     """Average duration of a kernel in the committed rocprofv3 --stats summary
     of the bench (newest round first)."""
     import csv
-    for d in ("r03", "r02"):
+    for d in ("r02_close",):
         path = os.path.join(REPO, "profiles", d, "bench_kernel_stats.csv")
         if not os.path.exists(path):
             continue

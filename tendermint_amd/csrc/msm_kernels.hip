@@ -862,11 +862,13 @@ k_msm_subcheck(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx
 }
 
 // Bucket sums, window parts and window sums (shared by both forms).
+// timed: bracket the first two kernels with the live kernel timer (the
+// located fallback's second pass over the failing groups is not timed).
 static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork mw, const MsmParams &p,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, bool timed = true) {
   const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
   const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
-  void *tk = ktimer::begin(ktimer::kAccum, stream);
+  void *tk = timed ? ktimer::begin(ktimer::kAccum, stream) : nullptr;
   if (p.L == 8)
     hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   else if (p.L == 16)
@@ -877,7 +879,7 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
-  tk = ktimer::begin(ktimer::kWpart, stream);
+  tk = timed ? ktimer::begin(ktimer::kWpart, stream) : nullptr;
   hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
@@ -1043,7 +1045,7 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t n_slots = p.groups << p.m_log2;
-    if ((e = launch_buckets(mw.loc_count, n_slots, mw, p, stream)) != hipSuccess) return e;
+    if ((e = launch_buckets(mw.loc_count, n_slots, mw, p, stream, false)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
                        mw.loc_count, n_slots, mw, p, nullptr, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;

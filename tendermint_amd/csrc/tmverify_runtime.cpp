@@ -189,6 +189,10 @@ struct HostLane {
   // first use)
   hipStream_t copy = nullptr;
   std::vector<hipEvent_t> part_ready;
+  // odd parts run their kernels on `helper`, so two parts' kernels overlap;
+  // `join` orders the launch's tail after them
+  hipStream_t helper = nullptr;
+  hipEvent_t join = nullptr;
 };
 constexpr int kLanes = 4;  // streams per device; TMV_HOST_LANES of them carry chunks
 
@@ -263,10 +267,12 @@ int64_t g_timeout_ms = 60000;
 // per device (TMV_STREAM_CHUNK).
 int g_stream = 1;
 bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
-// 320k C2 entries end to end (tools/gpu_stream_check.sh): 6.0-6.4 ms with
-// parts of 16k / 64k, 5.9-6.0 ms with 32k / 128k, 6.7 with 64k / 256k,
-// 6.9 ms unstreamed (two lanes of 80k chunks)
-uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 21;
+int g_stream_two = 1;              // TMV_STREAM_TWO=0: every part on the lane's stream
+// 320k C2 entries end to end (tools/gpu_stream_check.sh, parts on two
+// streams): 5.7 ms with parts of 32k / 64k, 5.8 with 16k / 64k, 5.85-6.0
+// with 32k / 128k, 6.1 with 16k / 32k; one stream 6.05-6.3; unstreamed
+// (two lanes of 80k chunks) 6.9 ms
+uint32_t g_stream_first = 32768, g_stream_part = 65536, g_stream_chunk = 1u << 21;
 
 void read_env() {
   static std::once_flag once;
@@ -294,6 +300,8 @@ void read_env() {
     if (to) g_timeout_ms = strtoll(to, nullptr, 10);
     const char *st = getenv("TMV_STREAM");
     if (st) g_stream = atoi(st);
+    const char *s2 = getenv("TMV_STREAM_TWO");
+    if (s2) g_stream_two = atoi(s2);
     const char *smd = getenv("TMV_STREAM_MODE");
     if (smd) g_stream_prep_only = !strcmp(smd, "prep");
     const char *sf = getenv("TMV_STREAM_FIRST");
@@ -762,9 +770,9 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
   return &w;
 }
 
-// Stages the inputs of entries [e0, e1) of a streamed launch and makes the
-// launch stream wait for their copy (stage_and_launch); 0 or < 0.
-using PartFeeder = std::function<int(uint32_t e0, uint32_t e1)>;
+// Stages the inputs of entries [e0, e1) of a streamed launch and enqueues
+// their copy; *ready = an event recorded after it (stage_and_launch); 0 or < 0.
+using PartFeeder = std::function<int(uint32_t e0, uint32_t e1, hipEvent_t *ready)>;
 
 // Part boundaries of a streamed launch of n entries: whole groups, the first
 // part g_stream_first entries, then g_stream_part each.
@@ -779,9 +787,11 @@ static std::vector<uint32_t> stream_parts(uint32_t n, uint32_t m) {
   return b;
 }
 
+// feed: streamed launch, parts alternating between s and s2 (if given,
+// joined back into s by `join` before the tail).
 static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *pk, const uint8_t *sig,
                        const uint8_t *msg, const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s,
-                       const PartFeeder *feed = nullptr) {
+                       const PartFeeder *feed = nullptr, hipStream_t s2 = nullptr, hipEvent_t join = nullptr) {
   int rc;
   Workspace *ws = reserve_work(d, n, false, s, &rc, &o.p);
   if (!ws) return rc;
@@ -790,11 +800,19 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   hipError_t e;
   if (feed) {  // parts as their inputs land, then one tail
     const std::vector<uint32_t> b = stream_parts(n, o.p.m());
+    const bool two = s2 && join && b.size() > 2;
     for (size_t j = 0; j + 1 < b.size(); j++) {
-      if ((rc = (*feed)(b[j], b[j + 1])) != 0) return rc;
+      hipEvent_t ready = nullptr;
+      if ((rc = (*feed)(b[j], b[j + 1], &ready)) != 0) return rc;
+      const hipStream_t t = two && (j & 1) ? s2 : s;
+      if ((e = hipStreamWaitEvent(t, ready, 0)) != hipSuccess) { set_error("part wait", e); return TMV_ERR_LAUNCH; }
       e = tmv::launch_batch_check_part(sr, pk, sig, msg, off, n, b[j], b[j + 1], d.d_btab_q, d.d_prefix, w, mw, o.p,
-                                       o.seed[sr ? 1 : 0], out, s, g_stream_prep_only);
+                                       o.seed[sr ? 1 : 0], out, t, g_stream_prep_only);
       if (e != hipSuccess) { set_error("batch check part launch", e); return TMV_ERR_LAUNCH; }
+    }
+    if (two && ((e = hipEventRecord(join, s2)) != hipSuccess || (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess)) {
+      set_error("part join", e);
+      return TMV_ERR_LAUNCH;
     }
     e = tmv::launch_batch_check_tail(sr, pk, sig, n, d.d_btab_q, w, mw, o.p, o.seed[sr ? 1 : 0], out, s,
                                      g_stream_prep_only);
@@ -977,6 +995,11 @@ void tmv_close(tmv_ctx *ctx) {
       l.part_ready.clear();
       if (l.copy) (void)hipStreamDestroy(l.copy);
       l.copy = nullptr;
+      if (l.helper) (void)hipStreamSynchronize(l.helper);
+      if (l.helper) (void)hipStreamDestroy(l.helper);
+      if (l.join) (void)hipEventDestroy(l.join);
+      l.helper = nullptr;
+      l.join = nullptr;
       l.d_in.release();
       l.d_out.release();
       l.h_in.release();
@@ -1091,7 +1114,11 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
     const uint32_t base = msg_off[lo];
     size_t part = 0;
-    const PartFeeder feed = [&](uint32_t a, uint32_t b) -> int {
+    if (g_stream_two && !ln.helper) {
+      if (hipStreamCreateWithFlags(&ln.helper, hipStreamNonBlocking) != hipSuccess) ln.helper = nullptr;
+      else if (hipEventCreateWithFlags(&ln.join, hipEventDisableTiming) != hipSuccess) ln.join = nullptr;
+    }
+    const PartFeeder feed = [&](uint32_t a, uint32_t b, hipEvent_t *ready) -> int {
       for (uint32_t i = a; i <= b; i++) off[i] = msg_off[lo + i] - base;
       const size_t m0 = off[a], m1 = off[b];
       const CopySpan sp[3] = {{h + L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a)},
@@ -1113,16 +1140,19 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
           set_error("hipMemcpyAsync(H2D)", ce);
           return TMV_ERR_LAUNCH;
         }
-      if ((ce = hipEventRecord(ev, ln.copy)) != hipSuccess || (ce = hipStreamWaitEvent(ln.stream, ev, 0)) != hipSuccess) {
+      if ((ce = hipEventRecord(ev, ln.copy)) != hipSuccess) {
         set_error("part event", ce);
         return TMV_ERR_LAUNCH;
       }
+      *ready = ev;
       return 0;
     };
     tm.mark("stage", n);
     const int rc = batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off),
-                               n, static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed);
+                               n, static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed,
+                               g_stream_two ? ln.helper : nullptr, g_stream_two ? ln.join : nullptr);
     if (rc != 0) return rc;
+    tm.mark("parts staged + launched", n);
     if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
       set_error("hipMemcpyAsync(D2H)", e);
       return TMV_ERR_LAUNCH;

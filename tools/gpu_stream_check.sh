@@ -10,7 +10,7 @@ TMV_STREAM_MODE=prep timeout -k 10 600 python -u -m pytest -x -q --timeout 300 -
   || { tail -40 $out/tests_prep.log; exit 1; }
 tail -1 $out/tests_prep.log
 tail -1 $out/tests.log
-for cfg in "TMV_STREAM=0" "TMV_STREAM=1" "TMV_STREAM_FIRST=32768 TMV_STREAM_PART=131072" "TMV_STREAM_MODE=prep" "TMV_STREAM_MODE=prep TMV_STREAM_FIRST=8192 TMV_STREAM_PART=32768" "TMV_STREAM_MODE=prep TMV_STREAM_FIRST=32768 TMV_STREAM_PART=131072" "TMV_STREAM_FIRST=65536 TMV_STREAM_PART=262144"; do
+for cfg in "TMV_STREAM=0" "TMV_STREAM_TWO=0" "TMV_STREAM_TWO=1" "TMV_STREAM_FIRST=16384 TMV_STREAM_PART=65536" "TMV_STREAM_FIRST=16384 TMV_STREAM_PART=32768" "TMV_STREAM_FIRST=32768 TMV_STREAM_PART=65536" "TMV_STREAM_TWO=0" "TMV_STREAM_TWO=1"; do
   echo -n "$cfg: "
   env $cfg timeout -k 10 120 python -u tools/e2e_probe.py 2>&1 | tail -1 || exit 1
 done | tee $out/sweep.txt
