@@ -15,6 +15,6 @@ for rep in 1 2 3; do
 done
 for v in old new; do
   cp $B/ab_$v.so $B/libtmgpu.so
-  echo -n "$v s1536: "; run --steps 1536
+  echo -n "$v s48: "; run --steps 48
 done
 cp $B/ab_new.so $B/libtmgpu.so
