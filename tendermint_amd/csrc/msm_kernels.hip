@@ -1242,16 +1242,32 @@ hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, cons
                                     Ed25519Work w_ed, Ed25519Work w_sr, MsmWork m_ed, MsmWork m_sr,
                                     const MsmParams &p, const MsmSeed &seed_ed, const MsmSeed &seed_sr,
                                     uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, int8_t *status,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, const KindStreams *ks) {
   if (n == 0) return hipSuccess;
   uint8_t *out = reinterpret_cast<uint8_t *>(status);
   hipError_t e = launch_partition(kind, n, counts, idx_ed, idx_sr, out, stream);
   if (e != hipSuccess) return e;
+  // the sr25519 pipeline on the helper stream, forked after the partition
+  // and joined at the end: the two kinds' pipelines (own work arrays, own
+  // entries of `out`) overlap, so one kind's latency tail runs beside the
+  // other's throughput stages
+  hipStream_t s_sr = stream;
+  if (ks && ks->helper && ks->fork && ks->join) {
+    if ((e = hipEventRecord(ks->fork, stream)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(ks->helper, ks->fork, 0)) != hipSuccess) return e;
+    s_sr = ks->helper;
+  }
+  e = launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p, seed_sr, out,
+                         s_sr);
+  if (e != hipSuccess) return e;
   e = launch_check<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, m_ed, p, seed_ed, out,
                           stream);
   if (e != hipSuccess) return e;
-  return launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p, seed_sr,
-                            out, stream);
+  if (s_sr != stream) {
+    if ((e = hipEventRecord(ks->join, s_sr)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(stream, ks->join, 0)) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace tmv

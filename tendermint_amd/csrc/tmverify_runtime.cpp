@@ -169,6 +169,9 @@ struct KeyIndex {
 struct Workspace {
   DeviceBuf work, work2, idx, msm, msm2, gather;
   hipEvent_t done = nullptr;
+  // mixed batch-equation launches: the sr25519 pipeline's stream and its
+  // fork / join events (created on first use; TMV_MIXED_TWO=0: one stream)
+  tmv::KindStreams kinds{nullptr, nullptr, nullptr};
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
   const uint8_t *sub_ok[2] = {nullptr, nullptr};  // sub-group verdicts (k_msm_subcheck), if it ran
@@ -268,6 +271,7 @@ int64_t g_timeout_ms = 60000;
 int g_stream = 1;
 bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
 int g_stream_two = 1;              // TMV_STREAM_TWO=0: every part on the lane's stream
+int g_mixed_two = 1;               // TMV_MIXED_TWO=0: a mixed launch's two kind pipelines on one stream
 // 320k C2 entries end to end (tools/gpu_stream_check.sh, parts on two
 // streams): 5.7 ms with parts of 32k / 64k, 5.8 with 16k / 64k, 5.85-6.0
 // with 32k / 128k, 6.1 with 16k / 32k; one stream 6.05-6.3; unstreamed
@@ -300,6 +304,8 @@ void read_env() {
     if (to) g_timeout_ms = strtoll(to, nullptr, 10);
     const char *st = getenv("TMV_STREAM");
     if (st) g_stream = atoi(st);
+    const char *m2 = getenv("TMV_MIXED_TWO");
+    if (m2) g_mixed_two = atoi(m2);
     const char *s2 = getenv("TMV_STREAM_TWO");
     if (s2) g_stream_two = atoi(s2);
     const char *smd = getenv("TMV_STREAM_MODE");
@@ -858,8 +864,16 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
   if (o.batch_eq) {
     tmv::MsmWork m1 = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
     tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p);
+    read_env();
+    tmv::KindStreams &ks = ws->kinds;
+    if (g_mixed_two && !ks.helper) {
+      if (hipStreamCreateWithFlags(&ks.helper, hipStreamNonBlocking) != hipSuccess) ks.helper = nullptr;
+      if (hipEventCreateWithFlags(&ks.fork, hipEventDisableTiming) != hipSuccess) ks.fork = nullptr;
+      if (hipEventCreateWithFlags(&ks.join, hipEventDisableTiming) != hipSuccess) ks.join = nullptr;
+    }
     e = tmv::launch_mixed_batch_check(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, m1, m2, o.p,
-                                      o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s);
+                                      o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s,
+                                      g_mixed_two ? &ks : nullptr);
     ws->group_ok[0] = m1.group_ok;
     ws->group_ok[1] = m2.group_ok;
     ws->sub_ok[0] = tmv::subcheck_enabled(o.p.m_log2) ? m1.sub_ok : nullptr;
@@ -1014,6 +1028,11 @@ void tmv_close(tmv_ctx *ctx) {
       kv.second->msm2.release();
       kv.second->gather.release();
       if (kv.second->done) (void)hipEventDestroy(kv.second->done);
+      tmv::KindStreams &ks = kv.second->kinds;
+      if (ks.helper) (void)hipStreamSynchronize(ks.helper);
+      if (ks.fork) (void)hipEventDestroy(ks.fork);
+      if (ks.join) (void)hipEventDestroy(ks.join);
+      if (ks.helper) (void)hipStreamDestroy(ks.helper);
     }
     d->ws.clear();
     d->d_kbuild.release();
