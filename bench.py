@@ -313,6 +313,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = local_rank  # this rank's HIP device (one process per GPU)
+    if not args.cpu_stub and torch.cuda.device_count() <= local_rank:
+        gpu = 0  # the launcher exposed one device per process
     F = max(1, args.inflight)
     R = max(1, min(64, args.resident))
     K = max(1, min(64, args.per_step))
@@ -330,11 +333,16 @@ def main():
         Stream, Event, stream_ctx = (lambda d: _HostStream()), _HostEvent, (lambda st: contextlib.nullcontext())
     else:
         if world > 1:
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        dev = torch.device("cuda", local_rank)
+            torch.cuda.set_device(gpu)
+            # RCCL; TMV_BENCH_BACKEND=gloo rehearses N ranks on a one-GPU box
+            backend = os.environ.get("TMV_BENCH_BACKEND", "nccl")
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            else:
+                dist.init_process_group(backend)
+        dev = torch.device("cuda", gpu)
         torch.cuda.set_device(dev)
-        ctx = N.Context(1 << local_rank)
+        ctx = N.Context(1 << gpu)
         ctx.set_batch_options(group_log2=args.group_log2, window_bits=args.window)
         sync = torch.cuda.synchronize
         Stream, Event, stream_ctx = torch.cuda.Stream, torch.cuda.Event, torch.cuda.stream
@@ -363,7 +371,7 @@ def main():
                        for b in batches]
     gathered = {}
 
-    def launch(i, first, kk, ev_pair=None):
+    def launch(i, first, kk, ev_pair=None, gather=True):
         f = i % F
         st = streams[f]
         if ev_pair is not None:
@@ -372,10 +380,10 @@ def main():
             for j in range(kk):
                 d_valid[f][j * n:(j + 1) * n] = stub_status[(first + j) % R]
         else:
-            ctx.verify_batches_device(local_rank, N.TMV_KIND_ED25519, flags, refs(f, first, kk), st.cuda_stream)
+            ctx.verify_batches_device(gpu, N.TMV_KIND_ED25519, flags, refs(f, first, kk), st.cuda_stream)
         if ev_pair is not None:
             ev_pair[1].record(st)
-        if world > 1:
+        if world > 1 and gather:
             # one collective per launch (its kk vectors are contiguous), in
             # issue order on one stream, after this launch
             comm.wait_stream(st)
@@ -442,7 +450,7 @@ def main():
         ctx.kernel_timing(True)
         for _ in range(5):
             e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            launch(0, 0, K, e)
+            launch(0, 0, K, e, gather=False)  # rank 0 alone: no collective
             torch.cuda.synchronize(dev)
             alone.append(e[0].elapsed_time(e[1]))
         ctx.kernel_timing(False)
@@ -452,7 +460,7 @@ def main():
         lat = []
         for _ in range(12):
             e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            launch(0, 0, 1, e)
+            launch(0, 0, 1, e, gather=False)
             torch.cuda.synchronize(dev)
             lat.append(e[0].elapsed_time(e[1]))
         batch_ms = statistics.median(lat[2:])
