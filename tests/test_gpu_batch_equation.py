@@ -281,3 +281,27 @@ def test_located_fallback_placements(bctx, kind):
         pre = C.sr25519_prechecks(b.pk, sig)
     assert groups == (n + 63) // 64
     assert failed == C.failing_groups(pre, ref == 1, 64) and failed >= 3
+
+
+def test_kernel_timing_records_each_launch(bctx):
+    """tmv_kernel_timing (bench.py's dominant-kernel roofline): every
+    batch-equation launch while it is on adds one k_msm_accum / k_msm_wpart /
+    k_prep_fused record of positive duration; none while it is off; a read
+    forgets what it returned; an unknown name is an argument error."""
+    b = make_c2_batch(20_000, seed=91)
+    for k in ("k_msm_accum", "k_msm_wpart", "k_prep_fused"):
+        bctx.kernel_timing_read(k)
+    bctx.kernel_timing(True)
+    try:
+        for _ in range(3):
+            bctx.verify_batch_ex(ED, BEQ, b.pk, b.sig, b.msg, b.off)
+    finally:
+        bctx.kernel_timing(False)
+    for k in ("k_msm_accum", "k_msm_wpart", "k_prep_fused"):
+        ms, cnt = bctx.kernel_timing_read(k)
+        assert cnt == 3 and ms > 0, (k, ms, cnt)
+        assert bctx.kernel_timing_read(k) == (0.0, 0)
+    bctx.verify_batch_ex(ED, BEQ, b.pk, b.sig, b.msg, b.off)
+    assert bctx.kernel_timing_read("k_msm_accum") == (0.0, 0)
+    with pytest.raises(N.NativeError):
+        bctx.kernel_timing_read("k_nonexistent")
