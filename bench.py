@@ -151,20 +151,24 @@ def accum_entries_per_sig(m: int = 64, c: int = 5, samples: int = 4000, seed: in
     return tot / samples + nonzero(rng.randrange(l_order), w) / m
 
 
-def _rocprof_avg_ms(kernel_prefix: str):
-    """Average duration of a kernel in the committed rocprofv3 --stats summary
-    of the bench (newest round first)."""
-    import csv
-    for d in ("r02_close",):
-        path = os.path.join(REPO, "profiles", d, "bench_kernel_stats.csv")
-        if not os.path.exists(path):
-            continue
+def _rocprof_avg_ms(steps: int):
+    """rocprofv3 --kernel-trace average of the primary k_msm_accum dispatches
+    in the timed region of a traced run of this bench command (committed:
+    profiles/r02_close/accum_trace_avg.json, tools/trace_kernel_avg.py), next
+    to the live value that run printed."""
+    path = os.path.join(REPO, "profiles", "r02_close", "accum_trace_avg.json")
+    try:
         with open(path) as f:
-            for row in csv.DictReader(f):
-                if row["Name"].replace("void ", "").replace("tmv::", "").startswith(kernel_prefix):
-                    return {"avg_ms": round(float(row["AverageNs"]) / 1e6, 4), "calls": int(row["Calls"]),
-                            "source": f"profiles/{d}/bench_kernel_stats.csv"}
-    return None
+            d = json.load(f)
+    except Exception:
+        return None
+    key = "bench --steps 20 --warmup 5" if steps <= 20 else "bench --steps 48 --warmup 8 --no-extras"
+    if key not in d:
+        return None
+    e = d[key]
+    return {"command": key, "avg_ms": e["rocprof_kernel_trace"]["primary_avg_ms"],
+            "dispatches": e["rocprof_kernel_trace"]["primary_dispatches"],
+            "live_avg_ms_same_run": e["live_avg_launch_ms"], "source": "profiles/r02_close/accum_trace_avg.json"}
 
 
 def host_cpu_info():
@@ -584,7 +588,7 @@ def main():
                   "frac_alone": round(per_launch / (alone[0] / alone[1] * 1e-3) / peak, 4) if alone[1] else None,
                   "other_kernels_avg_ms": {k: round(v[0] / v[1], 4) for k, v in ktimes.items()
                                            if v[1] and k != "k_msm_accum"},
-                  "rocprof": _rocprof_avg_ms("k_msm_accum")}
+                  "rocprof": _rocprof_avg_ms(steps)}
             if kp.get("SQ_INSTS_VALU_INT64"):
                 scale = K / pmc.get("batches_per_launch", 32)
                 dk["executed_int64_lane_ops_per_launch"] = int(kp["SQ_INSTS_VALU_INT64"] * 64 * scale)

@@ -3,7 +3,10 @@
 // light-client verification).  Not part of the public C-ABI.
 #pragma once
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <string>
 
@@ -12,6 +15,28 @@
 #include "tm_types.h"
 
 namespace tmh_internal {
+
+// Phase timing of a host-layer call, printed to stderr when the environment
+// variable TMV_HOST_TIMING is set (profiling aid).
+struct PhaseTimer {
+  const char *tag;
+  bool on = std::getenv("TMV_HOST_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit PhaseTimer(const char *tag_) : tag(tag_) {}
+  void mark(const char *what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[%s] %-8s %9.3f ms\n", tag, what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+// Marks `what` when it goes out of scope: declared right after the timer,
+// before a call's containers, it times their destruction.
+struct PhaseEnd {
+  PhaseTimer &tm;
+  const char *what;
+  ~PhaseEnd() { tm.mark(what); }
+};
 
 void put_err(char *err, size_t cap, const std::string &s);
 tmh::KeyType to_kind(uint8_t k);

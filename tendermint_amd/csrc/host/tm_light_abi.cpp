@@ -160,6 +160,8 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
   if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
   for (uint32_t j = 0; j < n_jobs; j++)
     if (jobs[j].mode < TMV_LIGHT_VERIFY || jobs[j].mode > TMV_LIGHT_NON_ADJACENT) return TMV_ERR_ARG;
+  PhaseTimer tm("tmv_light_verify_many");
+  const PhaseEnd tm_end{tm, "release"};
   // distinct headers, commits and validator sets, converted once
   Interner<tmv_header> H;
   Interner<tmv_commit> C;
@@ -188,6 +190,7 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
     else vsets[i - nh - nc] = vals_of(V.src[i - nh - nc]->vals, V.src[i - nh - nc]->n_vals,
                                       V.src[i - nh - nc]->proposer_index);
   });
+  tm.mark("convert");
   // hashes the checks may need: Header.Hash of untrusted headers,
   // ValidatorSet.Hash of untrusted validator sets
   std::vector<uint8_t> need_h(nh, 0), need_v(vsets.size(), 0);
@@ -203,7 +206,9 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
     if (need_v[i]) vq[i] = vsets[i].get();
   std::vector<tmh::Bytes> hh, vh;
   int rc = header_hashes(ctx, hq, hh);
+  tm.mark("hdr hash");
   if (rc >= 0) rc = valset_hashes(ctx, vq, V.src, vh);
+  tm.mark("vs hash");
   if (rc < 0) {
     if (errs && err_stride) put_err(errs, err_stride, tmv_last_error());
     return rc;
@@ -229,6 +234,7 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
     lj.trust_den = jb.trust_den;
     plans[j] = tmh::PlanLight(lj, r.uh == UINT32_MAX ? kNone : hh[r.uh], r.uv == UINT32_MAX ? kNone : vh[r.uv]);
   });
+  tm.mark("plan");
   // the commit checks of every job, one signature batch
   std::vector<tmv_commit_job> cj;
   std::vector<uint32_t> cfirst(n_jobs + 1, 0);
@@ -255,6 +261,7 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
       return rc;
     }
   }
+  tm.mark("commits");
   int bad = 0;
   for (uint32_t j = 0; j < n_jobs; j++) {
     const size_t k = plans[j].checks.size();
@@ -270,6 +277,15 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
     if (errs && err_stride) put_err(errs + (size_t)j * err_stride, err_stride, lr.text);
     bad += lr.kind != tmh::kLightOk;
   }
+  tm.mark("finish");
+  // many small heap objects (validators, signatures, plans): freed in parallel
+  const size_t nrel = std::max({headers.size(), commits.size(), vsets.size(), (size_t)n_jobs});
+  parallel_for(nrel, 16, [&](size_t i) {
+    if (i < headers.size()) headers[i].reset();
+    if (i < commits.size()) commits[i].reset();
+    if (i < vsets.size()) vsets[i].reset();
+    if (i < n_jobs) plans[i] = tmh::LightPlan();
+  });
   return bad;
 }
 
