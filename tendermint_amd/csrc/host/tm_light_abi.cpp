@@ -101,18 +101,21 @@ int valset_hashes(tmv_ctx *ctx, const std::vector<const tmh::ValidatorSet *> &vs
   }
   parallel_for(host.size(), 4, [&](size_t k) { out[host[k]] = tmh::ValidatorSetHashHost(*vs[host[k]]); });
   if (dev.empty()) return 0;
-  std::vector<uint8_t> pk, kind;
-  std::vector<int64_t> power;
-  std::vector<uint32_t> off{0};
-  for (uint32_t i : dev) {
-    const tmv_validator_set &s = *src[i];
-    for (uint32_t k = 0; k < s.n_vals; k++) {
-      pk.insert(pk.end(), s.vals[k].pub_key, s.vals[k].pub_key + 32);
-      kind.push_back(s.vals[k].key_kind);
-      power.push_back(s.vals[k].voting_power);
+  // pack the sets' keys, kinds and powers (offsets first, then the sets in
+  // parallel: a light window holds ~10^5 validators)
+  std::vector<uint32_t> off(dev.size() + 1, 0);
+  for (size_t k = 0; k < dev.size(); k++) off[k + 1] = off[k] + src[dev[k]]->n_vals;
+  const size_t total = off.back();
+  std::vector<uint8_t> pk(32 * total), kind(total);
+  std::vector<int64_t> power(total);
+  parallel_for(dev.size(), 16, [&](size_t k) {
+    const tmv_validator_set &s = *src[dev[k]];
+    for (uint32_t v = 0; v < s.n_vals; v++) {
+      std::memcpy(pk.data() + 32ull * (off[k] + v), s.vals[v].pub_key, 32);
+      kind[off[k] + v] = s.vals[v].key_kind;
+      power[off[k] + v] = s.vals[v].voting_power;
     }
-    off.push_back((uint32_t)kind.size());
-  }
+  });
   std::vector<uint8_t> roots(32 * dev.size());
   const int rc = tmv_validator_set_hashes(ctx, pk.empty() ? nullptr : pk.data(), kind.empty() ? nullptr : kind.data(),
                                           power.empty() ? nullptr : power.data(), off.data(), (uint32_t)dev.size(),

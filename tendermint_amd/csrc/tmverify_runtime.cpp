@@ -1170,7 +1170,12 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     const int rc = batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off),
                                n, static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed,
                                g_stream_two ? ln.helper : nullptr, g_stream_two ? ln.join : nullptr);
-    if (rc != 0) return rc;
+    if (rc != 0) {  // parts already enqueued still use the lane's buffers: drain before returning
+      (void)wait_stream(d, ln.copy);
+      if (ln.helper) (void)wait_stream(d, ln.helper);
+      (void)wait_stream(d, ln.stream);
+      return rc;
+    }
     tm.mark("parts staged + launched", n);
     if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
       set_error("hipMemcpyAsync(D2H)", e);
