@@ -4,7 +4,8 @@
   python bench.py --gpus N --steps K --warmup W
 
 A *step* = one device launch (tmv_verify_batches_device) that verifies
-`--batches-per-step` (default 32) synthetic C2 batches (BASELINE.json
+`--batches-per-step` (default 64, the most one launch takes) synthetic C2
+batches (BASELINE.json
 configs[1]: 10,000 ed25519 signatures over commit-vote sign-bytes, 1%
 corrupted / ZIP-215 edge cases each) already resident in HBM, producing every
 batch's exact validity vector: the batches are gathered on the device, run
@@ -297,10 +298,10 @@ def main():
                                                            "C2 batches)")
     ap.add_argument("--warmup", type=int, default=8, help="untimed steps before timing (at least --inflight)")
     ap.add_argument("--batch", type=int, default=10_000)
-    ap.add_argument("--batches-per-step", "--per-launch", dest="per_step", type=int, default=32,
+    ap.add_argument("--batches-per-step", "--per-launch", dest="per_step", type=int, default=64,
                     help="C2 batches per step (one tmv_verify_batches_device launch, <= 64)")
     ap.add_argument("--inflight", type=int, default=4, help="launches in flight (streams)")
-    ap.add_argument("--resident", type=int, default=32, help="distinct C2 batches held in HBM per rank")
+    ap.add_argument("--resident", type=int, default=64, help="distinct C2 batches held in HBM per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / end-to-end / C1 measurements")
     ap.add_argument("--method", choices=["batch", "per-entry"], default="batch",
