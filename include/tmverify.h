@@ -206,9 +206,10 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
  * written to its own d_status (as tmv_verify_batch_device_ex).  Verdicts are
  * per entry, so this equals n_batches separate calls; it only widens the
  * launches (a node draining a queue of batches, blocksync look-ahead).
- * msg_bytes = msg_off[n] - msg_off[0].  Up to 64 batches; key_kind
- * TMV_KIND_ED25519 or TMV_KIND_SR25519.  Asynchronous like the other
- * device-resident entry points. */
+ * msg_bytes = msg_off[n] - msg_off[0].  Up to TMV_MAX_BATCHES batches (and
+ * 2^26 entries in all); key_kind TMV_KIND_ED25519 or TMV_KIND_SR25519.
+ * Asynchronous like the other device-resident entry points. */
+#define TMV_MAX_BATCHES 256
 typedef struct tmv_batch_ref {
   const uint8_t *pk;
   const uint8_t *sig;

@@ -9,6 +9,9 @@
 
 namespace tmv {
 
+// Batches [0, nb) of one BatchRefs cover gathered entries [start[0],
+// start[nb]) and message bytes [msg_base[0], msg_base[nb]) (a launch of more
+// than kMaxBatches batches passes several BatchRefs).
 __device__ __forceinline__ uint32_t batch_of(const BatchRefs &r, uint32_t e) {
   uint32_t b = 0;
   for (uint32_t k = 1; k < r.nb; k++) b = (e >= r.start[k]) ? k : b;
@@ -32,8 +35,8 @@ k_gather(BatchRefs r, uint8_t *__restrict__ pk, uint8_t *__restrict__ sig, uint3
          uint8_t *__restrict__ msg) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t N = r.start[r.nb], M = r.msg_base[r.nb];
-  if (t < N) {
-    const uint32_t e = t;
+  if (r.start[0] + t < N) {
+    const uint32_t e = r.start[0] + t;
     const uint32_t b = batch_of(r, e), i = e - r.start[b];
     const uint8_t *spk = r.pk[b] + 32ull * i, *ssig = r.sig[b] + 64ull * i;
     if (((((uintptr_t)spk) | ((uintptr_t)ssig)) & 15) == 0) {
@@ -51,7 +54,7 @@ k_gather(BatchRefs r, uint8_t *__restrict__ pk, uint8_t *__restrict__ sig, uint3
     off[e] = r.msg_base[b] + (so[i] - so[0]);
     if (e + 1 == N) off[N] = r.msg_base[b] + (so[i + 1] - so[0]);
   }
-  const uint32_t x0 = 16 * t;
+  const uint32_t x0 = r.msg_base[0] + 16 * t;
   if (x0 >= M) return;
   uint32_t b = batch_of_byte(r, x0);
   const uint32_t x1 = min(M, x0 + 16);
@@ -63,7 +66,7 @@ k_gather(BatchRefs r, uint8_t *__restrict__ pk, uint8_t *__restrict__ sig, uint3
 
 __global__ void __launch_bounds__(256)
 k_scatter(BatchRefs r, const int8_t *__restrict__ status) {
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t e = r.start[0] + blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= r.start[r.nb]) return;
   const uint32_t b = batch_of(r, e);
   r.out[b][e - r.start[b]] = status[e];
@@ -71,15 +74,15 @@ k_scatter(BatchRefs r, const int8_t *__restrict__ status) {
 
 hipError_t launch_gather(const BatchRefs &r, uint8_t *pk, uint8_t *sig, uint32_t *off, uint8_t *msg,
                          hipStream_t stream) {
-  const uint32_t N = r.start[r.nb];
+  const uint32_t N = r.start[r.nb] - r.start[0];
   if (N == 0) return hipSuccess;
-  const uint32_t lanes = max(N, (r.msg_base[r.nb] + 15) / 16);
+  const uint32_t lanes = max(N, (r.msg_base[r.nb] - r.msg_base[0] + 15) / 16);
   hipLaunchKernelGGL(k_gather, dim3((lanes + 255) / 256), dim3(256), 0, stream, r, pk, sig, off, msg);
   return hipGetLastError();
 }
 
 hipError_t launch_scatter(const BatchRefs &r, const int8_t *status, hipStream_t stream) {
-  const uint32_t N = r.start[r.nb];
+  const uint32_t N = r.start[r.nb] - r.start[0];
   if (N == 0) return hipSuccess;
   hipLaunchKernelGGL(k_scatter, dim3((N + 255) / 256), dim3(256), 0, stream, r, status);
   return hipGetLastError();

@@ -1615,12 +1615,14 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
     set_error("tmv_verify_batches_device: key_kind must be ed25519 or sr25519");
     return TMV_ERR_ARG;
   }
-  if (n_batches == 0 || n_batches > tmv::kMaxBatches || !batches) {
-    set_error("tmv_verify_batches_device: 1..64 batches");
+  if (n_batches == 0 || n_batches > TMV_MAX_BATCHES || !batches) {
+    set_error("tmv_verify_batches_device: 1..256 batches");
     return TMV_ERR_ARG;
   }
-  tmv::BatchRefs r{};
-  r.nb = n_batches;
+  // one BatchRefs (kernel argument) per kMaxBatches batches; entry and
+  // message offsets are global over the launch
+  const uint32_t n_refs = (n_batches + tmv::kMaxBatches - 1) / tmv::kMaxBatches;
+  std::vector<tmv::BatchRefs> refs(n_refs);
   uint64_t N = 0, M = 0;
   for (uint32_t b = 0; b < n_batches; b++) {
     const tmv_batch_ref &x = batches[b];
@@ -1632,15 +1634,18 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
       set_error("tmv_verify_batches_device: message bytes in an empty batch");
       return TMV_ERR_ARG;
     }
-    r.pk[b] = x.pk; r.sig[b] = x.sig; r.msg[b] = x.msg; r.off[b] = x.msg_off; r.out[b] = x.status;
-    r.start[b] = (uint32_t)N;
-    r.msg_base[b] = (uint32_t)M;
+    tmv::BatchRefs &r = refs[b / tmv::kMaxBatches];
+    const uint32_t k = b % tmv::kMaxBatches;
+    r.pk[k] = x.pk; r.sig[k] = x.sig; r.msg[k] = x.msg; r.off[k] = x.msg_off; r.out[k] = x.status;
+    r.start[k] = (uint32_t)N;
+    r.msg_base[k] = (uint32_t)M;
+    r.nb = k + 1;
     N += x.n;
     M += x.msg_bytes;
+    if (N > 0xffffffffull / 64 || M > 0xffffffffull) { set_error("tmv_verify_batches_device: too large"); return TMV_ERR_ARG; }
+    r.start[k + 1] = (uint32_t)N;
+    r.msg_base[k + 1] = (uint32_t)M;
   }
-  if (N > 0xffffffffull / 64 || M > 0xffffffffull) { set_error("tmv_verify_batches_device: too large"); return TMV_ERR_ARG; }
-  r.start[n_batches] = (uint32_t)N;
-  r.msg_base[n_batches] = (uint32_t)M;
   if (N == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
@@ -1660,16 +1665,18 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   uint8_t *g = static_cast<uint8_t *>(ws->gather.ptr);
   uint32_t *goff = reinterpret_cast<uint32_t *>(g + L.off);
   int8_t *gst = reinterpret_cast<int8_t *>(g + L.total);
-  if ((e = tmv::launch_gather(r, g + L.pk, g + L.sig, goff, g + L.msg, s)) != hipSuccess) {
-    set_error("gather launch", e);
-    return TMV_ERR_LAUNCH;
-  }
+  for (const tmv::BatchRefs &r : refs)
+    if ((e = tmv::launch_gather(r, g + L.pk, g + L.sig, goff, g + L.msg, s)) != hipSuccess) {
+      set_error("gather launch", e);
+      return TMV_ERR_LAUNCH;
+    }
   if (key_kind == TMV_KIND_ED25519)
     rc = launch_ed25519(*dev, o, g + L.pk, g + L.sig, g + L.msg, goff, n, reinterpret_cast<uint8_t *>(gst), s);
   else
     rc = launch_sr25519(*dev, o, g + L.pk, g + L.sig, g + L.msg, goff, n, gst, s);
   if (rc != 0) return rc;
-  if ((e = tmv::launch_scatter(r, gst, s)) != hipSuccess) { set_error("scatter launch", e); return TMV_ERR_LAUNCH; }
+  for (const tmv::BatchRefs &r : refs)
+    if ((e = tmv::launch_scatter(r, gst, s)) != hipSuccess) { set_error("scatter launch", e); return TMV_ERR_LAUNCH; }
   (void)hipEventRecord(ws->done, s);
   return TMV_NOT_ALL;
 }

@@ -305,3 +305,37 @@ def test_kernel_timing_records_each_launch(bctx):
     assert bctx.kernel_timing_read("k_msm_accum") == (0.0, 0)
     with pytest.raises(N.NativeError):
         bctx.kernel_timing_read("k_nonexistent")
+
+
+def test_multi_batch_launch_over_64(bctx):
+    """More batches than one kernel argument holds (kMaxBatches = 64): 150
+    batches of ragged sizes -- empty ones at the 64 / 128 edges -- gathered
+    by three gather launches into one pipeline; each vector equals the
+    oracle's, and 257 batches are refused."""
+    import torch
+    dev = torch.device("cuda:0")
+    pool = make_c2_batch(3000, seed=47, edge_scale=6.0)
+    _, ref_all = C.ed25519_verify_packed(pool.pk, pool.sig, pool.msg, pool.off, threads=8)
+    t = {k: torch.from_numpy(getattr(pool, k)).to(dev) for k in ("pk", "sig", "msg")}
+    doff = torch.from_numpy(pool.off.view(np.int32)).to(dev)
+    refs, want, lo = [], [], 0
+    for b in range(150):
+        n = 0 if b in (63, 64, 127, 128) else 1 + (b * 7) % 37
+        if n == 0:
+            refs.append(N.BatchRef(0, 0, 0, 0, 0, 0, 0))
+            continue
+        n = min(n, pool.n - lo)
+        out = torch.full((n,), -7, dtype=torch.int8, device=dev)
+        refs.append(N.BatchRef(t["pk"].data_ptr() + 32 * lo, t["sig"].data_ptr() + 64 * lo, t["msg"].data_ptr(),
+                               doff.data_ptr() + 4 * lo, n, int(pool.off[lo + n] - pool.off[lo]), out.data_ptr()))
+        want.append((out, ref_all[lo:lo + n]))
+        lo += n
+    assert lo > 2000
+    for flags in (BEQ, N.TMV_FLAG_PER_ENTRY):
+        torch.cuda.synchronize()
+        bctx.verify_batches_device(0, ED, flags, refs, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        for out, ref in want:
+            assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref), flags
+    with pytest.raises(N.NativeError):
+        bctx.verify_batches_device(0, ED, BEQ, [N.BatchRef(0, 0, 0, 0, 0, 0, 0)] * 257)
