@@ -944,6 +944,8 @@ static uint32_t locate_min() {
   return v;
 }
 
+uint32_t locate_min_entries() { return locate_min(); }
+
 bool subcheck_enabled(uint32_t m_log2) {
   const int mode = subcheck_mode();
   return mode < 0 ? m_log2 >= 8 : mode == 1;

@@ -369,8 +369,16 @@ int faulted_rc(Device &d) {
 // The key-merged form (merged = true; keyed batches are commit traffic,
 // nearly always valid) defaults to groups of 256: its MSM has only the R
 // points and its fallback is the cheaper key-cached comb.
-tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false) {
-  if (m_log2 == 0) m_log2 = merged ? 8 : 6;
+tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false, bool ed_only = false) {
+  // uncached ed25519 launches large enough for the located fallback
+  // (tmv::locate_min_entries): groups of 128 (c = 6 by the cost model) --
+  // a failing group costs one located entry, not 128 verifications; C2
+  // bench 98.1-98.3 -> 100.7-100.8 M/s, groups of 256: 91.7-92.0
+  // (profiles/r02_close/ab_group.txt).  sr25519 / mixed batches keep 64
+  // (the factory's sr25519 corruption rate puts two bad entries in too many
+  // groups of 128).
+  const uint32_t lmin = tmv::locate_min_entries();
+  if (m_log2 == 0) m_log2 = merged ? 8 : (ed_only && lmin && n >= lmin ? 7 : 6);
   m_log2 = std::max<uint32_t>(5, std::min<uint32_t>(10, m_log2));
   if (c == 0) {
     const double m = double(1u << m_log2);
@@ -437,7 +445,7 @@ struct tmv_ctx {
 
 // Options of one launch of n entries: per-entry or batch equation (flags,
 // else TMV_MSM_MIN), parameters and fresh randomness.
-static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merged = false) {
+static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merged = false, bool ed_only = false) {
   read_env();
   LaunchOpts o;
   if (flags & TMV_FLAG_PER_ENTRY) o.batch_eq = false;
@@ -448,7 +456,7 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
   bool fixed;
   {
     std::lock_guard<std::mutex> lk(ctx->opt_mu);  // tmv_set_batch_options writes these
-    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged);
+    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged, ed_only);
     fixed = ctx->fixed_seed;
     if (fixed) std::memcpy(key, ctx->seed, 32);
   }
@@ -1093,7 +1101,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     }
   }
   tm.mark("keys", n);
-  LaunchOpts o = make_opts(ctx, flags, n, cached);
+  LaunchOpts o = make_opts(ctx, flags, n, cached, sch == Scheme::Ed25519 || sch == Scheme::Ed25519Cached);
   // key-merged form: worth it while a group holds few keys (runs <= n / 2)
   bool merged = cached && o.batch_eq;
   uint32_t distinct = 0;
@@ -1596,7 +1604,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
-  const LaunchOpts o = make_opts(ctx, flags, n);
+  const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
   std::lock_guard<std::mutex> lk(dev->mu);
   uint8_t *out = reinterpret_cast<uint8_t *>(d_status);
   int rc;
@@ -1651,7 +1659,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
   const uint32_t n = (uint32_t)N;
-  const LaunchOpts o = make_opts(ctx, flags, n);
+  const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc;
   Workspace *ws = reserve_work(*dev, n, false, s, &rc, o.batch_eq ? &o.p : nullptr);
@@ -1818,7 +1826,7 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
-  const LaunchOpts o = make_opts(ctx, 0, n);
+  const LaunchOpts o = make_opts(ctx, 0, n, false, true);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc = launch_ed25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, d_valid, s);
   return rc != 0 ? rc : TMV_NOT_ALL;

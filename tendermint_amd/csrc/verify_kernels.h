@@ -117,6 +117,9 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
 // k_msm_subcheck runs before the per-entry fallback for groups of 2^m_log2
 // (default m >= 256; TMV_SUBCHECK=0 never, =1 always).
 bool subcheck_enabled(uint32_t m_log2);
+// Launches of at least this many entries use the located fallback
+// (TMV_LOCATE_MIN, 0 = never).
+uint32_t locate_min_entries();
 hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
                             uint8_t *out, hipStream_t stream);
 

@@ -254,8 +254,8 @@ def test_multi_batch_launch(bctx, flags):
         assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref)
 
 
-@pytest.mark.parametrize("kind", [ED, SR])
-def test_located_fallback_placements(bctx, kind):
+@pytest.mark.parametrize("kind,m_log2", [(ED, 0), (ED, 6), (SR, 0)], ids=["ed-default", "ed-64", "sr-default"])
+def test_located_fallback_placements(bctx, kind, m_log2):
     """Launches of >= 150k entries (TMV_LOCATE_MIN) re-check a failing group
     with index weights (j + 1) z_j and verify only the entry that locates;
     groups with two or more bad entries fall back to every entry.  One bad
@@ -270,7 +270,9 @@ def test_located_fallback_placements(bctx, kind):
     for i in bad:
         sig[64 * i + 5] ^= 0x10  # R byte: R mostly still decodes, the equation fails
     bb = _B(b.pk, sig, b.msg, b.off)
-    ok, st, groups, failed = _run(bctx, kind, bb)
+    # default group size at this launch size: 128 for ed25519, 64 for sr25519
+    m = 1 << m_log2 if m_log2 else (128 if kind == ED else 64)
+    ok, st, groups, failed = _run(bctx, kind, bb, group_log2=m_log2)
     if kind == ED:
         ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
         assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
@@ -279,8 +281,8 @@ def test_located_fallback_placements(bctx, kind):
         ref = C.sr25519_status_packed(b.pk, sig, b.msg, b.off, threads=16)
         assert np.array_equal(st, ref)
         pre = C.sr25519_prechecks(b.pk, sig)
-    assert groups == (n + 63) // 64
-    assert failed == C.failing_groups(pre, ref == 1, 64) and failed >= 3
+    assert groups == (n + m - 1) // m
+    assert failed == C.failing_groups(pre, ref == 1, m) and failed >= 3
 
 
 def test_kernel_timing_records_each_launch(bctx):
