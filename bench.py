@@ -151,6 +151,24 @@ def accum_entries_per_sig(m: int = 64, c: int = 5, samples: int = 4000, seed: in
     return tot / samples + nonzero(rng.randrange(l_order), w) / m
 
 
+def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: int = 150_000):
+    """The runtime's batch-equation shape for an uncached ed25519 launch of
+    n_launch entries (tmverify_runtime.cpp msm_params): groups of 128 from
+    the located-fallback size up, else 64; the window from the same cost
+    model.  Returns (m, c)."""
+    m_log2 = group_log2 or (7 if n_launch >= locate_min else 6)
+    m = 1 << m_log2
+    if window:
+        return m, window
+    best, c = None, 5
+    for cc in range(4, 10):
+        w, wr, h = -(-254 // cc), -(-129 // cc), 1 << (cc - 1)
+        cost = m * (w + wr) + 2.2 * w * h
+        if best is None or cost < best:
+            best, c = cost, cc
+    return m, c
+
+
 def _rocprof_avg_ms(steps: int):
     """rocprofv3 --kernel-trace average of the primary k_msm_accum dispatches
     in the timed region of a traced run of this bench command (committed:
@@ -578,7 +596,8 @@ def main():
         if ktimes.get("k_msm_accum", (0, 0))[1] and args.method == "batch":
             ms, cnt = ktimes["k_msm_accum"]
             avg = ms / cnt
-            per_launch = K * n * accum_entries_per_sig(c=args.window or 5) * ACCUM_PRODUCTS_PER_ENTRY
+            m_grp, c_win = msm_shape(K * n, args.group_log2, args.window)
+            per_launch = K * n * accum_entries_per_sig(m=m_grp, c=c_win) * ACCUM_PRODUCTS_PER_ENTRY
             acc = per_launch / (avg * 1e-3)
             kp = pmc.get("kernels", {}).get("tmv::k_msm_accum<16>", {})
             alone = ktimes_alone.get("k_msm_accum", (0, 0))
@@ -589,9 +608,10 @@ def main():
                             "duration under the bench's overlap",
                   "avg_launch_ms_alone": round(alone[0] / alone[1], 4) if alone[1] else None,
                   "algorithmic_products_per_launch": round(per_launch),
+                  "msm_shape": {"group": m_grp, "window_bits": c_win},
                   "algorithmic_note": f"{K} x {n} signatures x expected bucket entries per signature (nonzero signed "
-                                      "5-bit digits of z and z k mod l, + the group's B scalar; simulated recoding) x "
-                                      "7 field multiplications x 100 int32 products",
+                                      f"{c_win}-bit digits of z and z k mod l, + the group's B scalar over {m_grp}; "
+                                      "simulated recoding) x 7 field multiplications x 100 int32 products",
                   "achieved": round(acc / 1e12, 4), "peak": round(peak / 1e12, 4), "unit": "Tmul/s",
                   "frac": round(acc / peak, 4),
                   "frac_alone": round(per_launch / (alone[0] / alone[1] * 1e-3) / peak, 4) if alone[1] else None,
