@@ -103,7 +103,8 @@ if "5" in only:
     st = torch.cuda.Stream()
     ref = None
     c5_methods = [("per-entry", N.TMV_FLAG_PER_ENTRY, 0), ("batch m=32", N.TMV_FLAG_BATCH_EQUATION, 5),
-                  ("batch m=64", N.TMV_FLAG_BATCH_EQUATION, 6), ("batch m=256", N.TMV_FLAG_BATCH_EQUATION, 8)]
+                  ("batch m=64", N.TMV_FLAG_BATCH_EQUATION, 6), ("batch m=128", N.TMV_FLAG_BATCH_EQUATION, 7),
+                  ("batch m=256", N.TMV_FLAG_BATCH_EQUATION, 8)]
     if a.c5_methods:
         c5_methods = [m for m in c5_methods if m[0] in a.c5_methods.split(",")]
     for label, flags, mlog in c5_methods:
