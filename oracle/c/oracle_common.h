@@ -236,35 +236,64 @@ static int sc_is_canonical(const uint8_t s[32]) {
     return 0; /* equal to l */
 }
 
-/* reduce a 64-byte little-endian integer mod l (schoolbook long division on bits) */
+/* reduce a 64-byte little-endian integer mod l: Barrett reduction (HAC
+ * 14.42) in base 2^64, k = 4 words, mu = floor(2^512 / l) (5 words) */
 static void sc_reduce64(uint8_t out[32], const uint8_t in[64]) {
-    /* represent as 9 u64 words; shift-subtract l·2^k */
-    uint64_t x[9] = {0}, l[9] = {0};
+    static const uint64_t MU[5] = {0xed9ce5a30a2c131bULL, 0x2106215d086329a7ULL, 0xffffffffffffffebULL,
+                                   0xffffffffffffffffULL, 0x000000000000000fULL};
+    static const uint64_t LW[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0x0000000000000000ULL,
+                                   0x1000000000000000ULL};
+    uint64_t x[8] = {0};
     for (int i = 0; i < 64; i++) x[i / 8] |= (uint64_t)in[i] << (8 * (i % 8));
-    for (int i = 0; i < 32; i++) l[i / 8] |= (uint64_t)L_BYTES[i] << (8 * (i % 8));
-    for (int k = 512 - 253; k >= 0; k--) {
-        /* t = l << k */
-        uint64_t t[9] = {0};
-        int ws = k / 64, bs = k % 64;
-        for (int i = 0; i < 4; i++) {
-            if (i + ws < 9) t[i + ws] |= l[i] << bs;
-            if (bs && i + ws + 1 < 9) t[i + ws + 1] |= l[i] >> (64 - bs);
+    /* q1 = x >> 192 (5 words); q2 = q1 * mu (10 words); q3 = q2 >> 320 */
+    uint64_t q2[10] = {0};
+    for (int i = 0; i < 5; i++) {
+        u128 c = 0;
+        for (int j = 0; j < 5; j++) {
+            c += (u128)x[3 + i] * MU[j] + q2[i + j];
+            q2[i + j] = (uint64_t)c;
+            c >>= 64;
         }
-        int ge_ = 1;
-        for (int i = 8; i >= 0; i--) {
-            if (x[i] > t[i]) { ge_ = 1; break; }
-            if (x[i] < t[i]) { ge_ = 0; break; }
+        q2[i + 5] = (uint64_t)c;
+    }
+    const uint64_t *q3 = q2 + 5;
+    /* r2 = (q3 * l) mod 2^320 */
+    uint64_t r2[5] = {0};
+    for (int i = 0; i < 5; i++) {
+        u128 c = 0;
+        for (int j = 0; j < 4 && i + j < 5; j++) {
+            c += (u128)q3[i] * LW[j] + r2[i + j];
+            r2[i + j] = (uint64_t)c;
+            c >>= 64;
         }
-        if (ge_) {
-            uint64_t br = 0;
-            for (int i = 0; i < 9; i++) {
-                u128 d = (u128)x[i] - t[i] - br;
-                x[i] = (uint64_t)d;
-                br = (uint64_t)(d >> 64) ? 1 : 0;
+        if (i == 0) r2[4] = (uint64_t)c;  /* row 0's carry; later rows' carries fall past 2^320 */
+    }
+    /* r = (x mod 2^320) - r2 (mod 2^320), then subtract l while r >= l */
+    uint64_t r[5];
+    u128 br = 0;
+    for (int i = 0; i < 5; i++) {
+        u128 d = (u128)x[i] - r2[i] - br;
+        r[i] = (uint64_t)d;
+        br = (d >> 64) ? 1 : 0;
+    }
+    for (int it = 0; it < 3; it++) {
+        int ge_ = r[4] != 0;
+        if (!ge_) {
+            ge_ = 1;
+            for (int i = 3; i >= 0; i--) {
+                if (r[i] > LW[i]) { ge_ = 1; break; }
+                if (r[i] < LW[i]) { ge_ = 0; break; }
             }
         }
+        if (!ge_) break;
+        br = 0;
+        for (int i = 0; i < 5; i++) {
+            u128 d = (u128)r[i] - (i < 4 ? LW[i] : 0) - br;
+            r[i] = (uint64_t)d;
+            br = (d >> 64) ? 1 : 0;
+        }
     }
-    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(x[i / 8] >> (8 * (i % 8)));
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(r[i / 8] >> (8 * (i % 8)));
 }
 
 /* r = [a]P + [b]Q, 4-bit fixed windows (Straus), variable time */

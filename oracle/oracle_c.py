@@ -71,6 +71,27 @@ def ed25519_verify_packed(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, off:
     return bool(ok), out[:n]
 
 
+def ed25519_batch_verify_voi(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, off: np.ndarray,
+                             threads: int = 1, batch: int = 1024, seed: int = 1):
+    """voi-style batch verification (c/ed25519_batch_cpu.c): one random
+    linear combination per `batch` entries, entry-by-entry on failure.
+    Returns (ok, uint8 vector, batches whose equation failed)."""
+    L = lib()
+    if not getattr(L, "_batch_voi", False):
+        L.oracle_ed25519_batch_verify_voi.argtypes = [ctypes.c_void_p] * 4 + [
+            ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64,
+            ctypes.POINTER(ctypes.c_size_t)]
+        L._batch_voi = True
+    n = len(off) - 1
+    out = np.zeros(max(n, 1), np.uint8)
+    msg = msg if len(msg) else np.zeros(1, np.uint8)
+    failed = ctypes.c_size_t(0)
+    ok = L.oracle_ed25519_batch_verify_voi(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data,
+                                           np.ascontiguousarray(off, np.uint32).ctypes.data, n, out.ctypes.data,
+                                           threads, batch, seed, ctypes.byref(failed))
+    return bool(ok), out[:n], failed.value
+
+
 def sr25519_status_packed(pk, sig, msg, off, threads: int = 1) -> np.ndarray:
     n = len(off) - 1
     out = np.zeros(max(n, 1), np.int8)

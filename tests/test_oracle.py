@@ -124,3 +124,20 @@ def test_empty_batch_is_false():
     ok, vec = C.ed25519_verify_packed(np.zeros(0, np.uint8), np.zeros(0, np.uint8), np.zeros(0, np.uint8),
                                       np.zeros(1, np.uint32))
     assert ok is False and len(vec) == 0
+
+
+def test_cpu_batch_verifier_matches_per_entry():
+    """oracle/c/ed25519_batch_cpu.c (bench.py's cpu_baseline: voi's batch
+    algorithm restated in C) gives the per-entry vector: honest batches pass
+    their equation (no fallback), batches with edge cases fall back and still
+    match, small-order ZIP-215 entries included."""
+    import oracle_c as C
+    from tendermint_amd.testing.factory import make_c2_batch, make_commit_batch
+    h = make_commit_batch(300)
+    ok, v, failed = C.ed25519_batch_verify_voi(h.pk, h.sig, h.msg, h.off, threads=2, batch=64)
+    assert ok and v.all() and failed == 0
+    c = make_c2_batch(1200, seed=77, edge_scale=3.0)
+    _, ref = C.ed25519_verify_packed(c.pk, c.sig, c.msg, c.off, threads=4)
+    for batch in (1, 50, 1200):
+        ok, v, failed = C.ed25519_batch_verify_voi(c.pk, c.sig, c.msg, c.off, threads=3, batch=batch)
+        assert np.array_equal(v, ref) and not ok and failed >= 1
