@@ -747,15 +747,19 @@ template hipError_t launch_comb_fallback<true>(const uint8_t *, const uint32_t *
                                                Ed25519Work, KeyTable, const fe *, uint8_t *, int, const uint8_t *,
                                                uint32_t, hipStream_t);
 
-// k_verify_quad's -A tables: LDS (default) or global scratch
-// (TMV_QUAD_TABLE=global).  Measured on the C2 bench in one GPU call
-// (profiles/r01_msm/ab_quad_table.log): LDS 72.8 / 73.5 M/s, global 70.8 /
-// 71.2 M/s (5 instead of 2 waves per SIMD, but every window's entry then
-// comes from L2); per entry 45.6-45.7 M/s either way.
-static bool quad_table_global() {
-  static const bool g = [] {
+// k_verify_quad's -A tables: LDS or global scratch.  Measured on the C2 bench
+// in one GPU call (profiles/r01_msm/ab_quad_table.log, when the quad kernel
+// still ran every entry): LDS 72.8 / 73.5 M/s, global 70.8 / 71.2 M/s (5
+// instead of 2 waves per SIMD, but every window's entry then comes from L2);
+// per entry 45.6-45.7 M/s either way.  As the batch-equation fallback almost
+// every block exits at once, and the 22.5 KB of LDS a block holds only caps
+// how fast the grid drains: global there (C2 bench, profiles/r02_close/
+// ab_quad_fallback.txt: 101.5 / 101.8 -> 102.8 / 102.5 M/s), LDS for the
+// per-entry pipeline.  TMV_QUAD_TABLE=global|lds forces one.
+static int quad_table_env() {
+  static const int g = [] {
     const char *e = getenv("TMV_QUAD_TABLE");
-    return e && !strcmp(e, "global");
+    return !e ? 0 : !strcmp(e, "global") ? 1 : !strcmp(e, "lds") ? 2 : 0;
   }();
   return g;
 }
@@ -766,8 +770,9 @@ static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig
                         int aligned, const uint8_t *group_ok, uint32_t group_log2,
                         const uint8_t *sub_ok = nullptr, const uint32_t *fail_list = nullptr,
                         const uint32_t *fail_count = nullptr, const uint32_t *fb_list = nullptr,
-                        const uint32_t *fb_count = nullptr) {
-  if (quad_table_global())
+                        const uint32_t *fb_count = nullptr, bool fallback = false) {
+  const int forced = quad_table_env();
+  if (forced == 1 || (forced == 0 && fallback))
     hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
                        w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count, fb_list,
                        fb_count);
@@ -809,7 +814,7 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
                            : fail_list ? ((((n + (1u << group_log2) - 1) >> group_log2)) << (group_log2 - 4))
                                        : (n + kQuadSigs - 1) / kQuadSigs;
   launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok,
-                  fail_list, fail_count, fb_list, fb_count);
+                  fail_list, fail_count, fb_list, fb_count, true);
   return hipGetLastError();
 }
 template hipError_t launch_quad_fallback<false>(const uint8_t *, const uint32_t *, const uint32_t *, uint32_t,

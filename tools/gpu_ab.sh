@@ -9,7 +9,7 @@ mkdir -p $OUT
 STEPS=${AB_STEPS:-20}
 for cfg in "$@"; do
   env $cfg timeout -k 10 300 python -u -m pytest tests/test_gpu_batch_equation.py tests/test_gpu_ed25519.py -x -q \
-    --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed under $cfg"; tail -30 $OUT/tests.log; exit 1; }
+    -k "not kernel_timing" --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed under $cfg"; tail -30 $OUT/tests.log; exit 1; }
   echo "tests ok under $cfg: $(tail -1 $OUT/tests.log)"
 done
 for rep in 1 2; do
