@@ -25,11 +25,26 @@ __device__ __forceinline__ uint32_t batch_of_byte(const BatchRefs &r, uint32_t x
   return b;
 }
 
+// 16 bytes from any byte address: aligned dword loads (each holds at least
+// one wanted byte, so none reaches past the source's last page) shifted
+// together.
+__device__ __forceinline__ uint4 load16_any(const uint8_t *src) {
+  const uintptr_t a = (uintptr_t)src;
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(a - sh);
+  const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3];
+  if (sh == 0) return make_uint4(w0, w1, w2, w3);
+  const uint32_t w4 = p[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
 // Lane t: entry t's key and signature (16-byte vector copies when the source
-// is aligned) and rebased message offset, and gathered message bytes
-// [16 t, 16 t + 16).  A batch's messages are one contiguous run in its
-// source and in the gathered buffer, so consecutive lanes copy consecutive
-// bytes (coalesced) instead of each lane walking its own message.
+// is aligned) and rebased message offset, and the t-th 16-byte-aligned span
+// of the gathered message bytes.  A batch's messages are one contiguous run
+// in its source and in the gathered buffer, so a span inside one batch is one
+// 16-byte store; spans at the run's ends or across a batch boundary go byte
+// by byte.
 __global__ void __launch_bounds__(256)
 k_gather(BatchRefs r, uint8_t *__restrict__ pk, uint8_t *__restrict__ sig, uint32_t *__restrict__ off,
          uint8_t *__restrict__ msg) {
@@ -54,12 +69,20 @@ k_gather(BatchRefs r, uint8_t *__restrict__ pk, uint8_t *__restrict__ sig, uint3
     off[e] = r.msg_base[b] + (so[i] - so[0]);
     if (e + 1 == N) off[N] = r.msg_base[b] + (so[i + 1] - so[0]);
   }
-  const uint32_t x0 = r.msg_base[0] + 16 * t;
-  if (x0 >= M) return;
-  uint32_t b = batch_of_byte(r, x0);
-  const uint32_t x1 = min(M, x0 + 16);
-  for (uint32_t x = x0; x < x1; x++) {
-    while (b + 1 < r.nb && x >= r.msg_base[b + 1]) b++;  // a 16-byte span may cross into the next batch
+  // spans start where msg + x is 16-byte aligned
+  const int64_t mis = (int64_t)((uintptr_t)msg & 15);
+  const int64_t x0 = ((((int64_t)r.msg_base[0] + mis) & ~(int64_t)15) - mis) + 16 * (int64_t)t;
+  if (x0 >= (int64_t)M) return;
+  const uint32_t lo = (uint32_t)max(x0, (int64_t)r.msg_base[0]);
+  const uint32_t hi = (uint32_t)min((int64_t)M, x0 + 16);
+  uint32_t b = batch_of_byte(r, lo);
+  if ((int64_t)lo == x0 && hi == lo + 16 && (b + 1 == r.nb || hi <= r.msg_base[b + 1])) {
+    const uint8_t *src = r.msg[b] + r.off[b][0] + (lo - r.msg_base[b]);
+    *reinterpret_cast<uint4 *>(msg + lo) = load16_any(src);
+    return;
+  }
+  for (uint32_t x = lo; x < hi; x++) {
+    while (b + 1 < r.nb && x >= r.msg_base[b + 1]) b++;  // a span may cross into the next batch
     msg[x] = r.msg[b][r.off[b][0] + (x - r.msg_base[b])];
   }
 }
@@ -76,7 +99,8 @@ hipError_t launch_gather(const BatchRefs &r, uint8_t *pk, uint8_t *sig, uint32_t
                          hipStream_t stream) {
   const uint32_t N = r.start[r.nb] - r.start[0];
   if (N == 0) return hipSuccess;
-  const uint32_t lanes = max(N, (r.msg_base[r.nb] - r.msg_base[0] + 15) / 16);
+  // one more span than the bytes need: spans are aligned to msg's address
+  const uint32_t lanes = max(N, (r.msg_base[r.nb] - r.msg_base[0]) / 16 + 2);
   hipLaunchKernelGGL(k_gather, dim3((lanes + 255) / 256), dim3(256), 0, stream, r, pk, sig, off, msg);
   return hipGetLastError();
 }

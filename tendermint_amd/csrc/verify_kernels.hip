@@ -181,15 +181,19 @@ constexpr int kQuadSigs = kQuadBlock / 4;
 // while the wave runs) instead of LDS, so LDS (22.5 KB per wave otherwise)
 // no longer caps residency; each window's entry is loaded before its four
 // doublings, like the B entry.
+// One 16-entry block (blk) of k_verify_quad; every return before the
+// __syncthreads is block-uniform except the passing-group branch, which
+// k_verify_quad_list never takes.
 template <bool SR, bool GT>
-__global__ void __launch_bounds__(kQuadBlock)
-k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
-              uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
-              const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok,
-              const uint32_t *__restrict__ fail_list, const uint32_t *__restrict__ fail_count,
-              const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count) {
-  __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
-  __shared__ int8_t dig[kQuadSigs][2][64];
+__device__ __forceinline__ void quad_block(uint32_t blk, fe *tabA_lds, int8_t (*dig)[2][64],
+                                           const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
+                                           const uint32_t *count_ptr, uint32_t n, const Ed25519Work &w,
+                                           const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
+                                           const uint8_t *__restrict__ group_ok, uint32_t group_log2,
+                                           const uint8_t *__restrict__ sub_ok,
+                                           const uint32_t *__restrict__ fail_list,
+                                           const uint32_t *__restrict__ fail_count,
+                                           const uint32_t *__restrict__ fb_list, uint32_t nl) {
   const uint32_t m = entry_count(count_ptr, n);
   const int c = threadIdx.x & 3;
   const int q = threadIdx.x >> 2;
@@ -201,18 +205,17 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
   uint32_t b0 = 0, e;
   bool live;
   if (fb_list) {
-    const uint32_t nl = *fb_count;
-    if (blockIdx.x * kQuadSigs >= nl) return;  // block-uniform
-    const uint32_t t = blockIdx.x * kQuadSigs + q;
+    if (blk * kQuadSigs >= nl) return;  // block-uniform
+    const uint32_t t = blk * kQuadSigs + q;
     live = t < nl;
     e = fb_list[live ? t : nl - 1];
   } else {
     if (fail_list) {
       const uint32_t per_log2 = group_log2 - 4;  // 16-entry blocks per group
-      if (blockIdx.x >= (*fail_count << per_log2)) return;  // block-uniform
-      b0 = (fail_list[blockIdx.x >> per_log2] << group_log2) + ((blockIdx.x & ((1u << per_log2) - 1)) << 4);
+      if (blk >= (*fail_count << per_log2)) return;  // block-uniform
+      b0 = (fail_list[blk >> per_log2] << group_log2) + ((blk & ((1u << per_log2) - 1)) << 4);
     } else {
-      b0 = blockIdx.x * kQuadSigs;
+      b0 = blk * kQuadSigs;
     }
     if (b0 >= m) return;  // block-uniform
     const uint32_t raw = b0 + q;
@@ -343,6 +346,39 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
     status = ok ? 1 : 0;
   }
   if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
+}
+
+
+template <bool SR, bool GT>
+__global__ void __launch_bounds__(kQuadBlock)
+k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+              uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
+              const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok,
+              const uint32_t *__restrict__ fail_list, const uint32_t *__restrict__ fail_count,
+              const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count) {
+  __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
+  __shared__ int8_t dig[kQuadSigs][2][64];
+  quad_block<SR, GT>(blockIdx.x, tabA_lds, dig, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok,
+                     group_log2, sub_ok, fail_list, fail_count, fb_list, fb_list ? *fb_count : 0u);
+}
+
+// The located fallback's entry list (k_loc_search) is usually a few entries
+// but may hold every entry, so a grid sized for the worst case is mostly
+// blocks that exit at once, and dispatching them is what the launch costs.
+// Here a bounded grid strides over the list's 16-entry blocks instead.
+template <bool SR>
+__global__ void __launch_bounds__(kQuadBlock)
+k_verify_quad_list(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
+                   uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out,
+                   int aligned, const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count) {
+  __shared__ fe tabA_lds[4];
+  __shared__ int8_t dig[kQuadSigs][2][64];
+  const uint32_t nl = *fb_count;
+  for (uint32_t blk = blockIdx.x; blk * kQuadSigs < nl; blk += gridDim.x) {
+    quad_block<SR, true>(blk, tabA_lds, dig, sig, idx, count_ptr, n, w, btab_q, out, aligned, nullptr, 0u, nullptr,
+                         nullptr, nullptr, fb_list, nl);
+    __syncthreads();  // dig is rewritten by the next block
+  }
 }
 
 // Mixed batches: split indices by key kind (TMV_KIND_ED25519 = 0,
@@ -813,6 +849,13 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
   const uint32_t qblocks = fb_list ? (n + kQuadSigs - 1) / kQuadSigs
                            : fail_list ? ((((n + (1u << group_log2) - 1) >> group_log2)) << (group_log2 - 4))
                                        : (n + kQuadSigs - 1) / kQuadSigs;
+  if (fb_list && quad_table_env() != 2) {
+    // at most 16 waves per CU (the kernel fits 5 per SIMD); blocks stride over the list
+    const uint32_t grid = qblocks < 256u * 16u ? qblocks : 256u * 16u;
+    hipLaunchKernelGGL(k_verify_quad_list<SR>, dim3(grid), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
+                       btab_q, out, aligned, fb_list, fb_count);
+    return hipGetLastError();
+  }
   launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok,
                   fail_list, fail_count, fb_list, fb_count, true);
   return hipGetLastError();

@@ -33,7 +33,8 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"TMV_KERNEL": "single"}, {"TMV_QUAD_TABLE": "global"}, {"TMV_MSM_CHUNK": "8"},
+@pytest.mark.parametrize("env", [{"TMV_KERNEL": "single"}, {"TMV_QUAD_TABLE": "global"}, {"TMV_QUAD_TABLE": "lds"},
+                                 {"TMV_MSM_CHUNK": "8"},
                                  {"TMV_MSM_CHUNK": "32"}, {"TMV_KERNEL": "quad", "TMV_MSM_MIN": "0"}])
 def test_variant_matches_oracle(env):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
