@@ -78,7 +78,7 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-PMC_DIRS = ("r02_close", "r02", "r01_close")  # newest first
+PMC_DIRS = ("r02_final", "r02_close", "r02", "r01_close")  # newest first
 
 
 def _load_pmc(method: str, batches_per_step: int = 32):
@@ -172,9 +172,9 @@ def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: i
 def _rocprof_avg_ms(steps: int):
     """rocprofv3 --kernel-trace average of the primary k_msm_accum dispatches
     in the timed region of a traced run of this bench command (committed:
-    profiles/r02_close/accum_trace_avg.json, tools/trace_kernel_avg.py), next
+    profiles/r02_final/accum_trace_avg.json, tools/trace_kernel_avg.py), next
     to the live value that run printed."""
-    path = os.path.join(REPO, "profiles", "r02_close", "accum_trace_avg.json")
+    path = os.path.join(REPO, "profiles", "r02_final", "accum_trace_avg.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -186,7 +186,7 @@ def _rocprof_avg_ms(steps: int):
     e = d[key]
     return {"command": key, "avg_ms": e["rocprof_kernel_trace"]["primary_avg_ms"],
             "dispatches": e["rocprof_kernel_trace"]["primary_dispatches"],
-            "live_avg_ms_same_run": e["live_avg_launch_ms"], "source": "profiles/r02_close/accum_trace_avg.json"}
+            "live_avg_ms_same_run": e["live_avg_launch_ms"], "source": "profiles/r02_final/accum_trace_avg.json"}
 
 
 def host_cpu_info():
