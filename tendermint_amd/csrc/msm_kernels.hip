@@ -148,10 +148,8 @@ __device__ __forceinline__ void p3_dbl(ge_p3 &a) {
 // Bucket b's sum; false if the bucket is empty.  A bucket that fits in one
 // chunk was stored whole by k_msm_accum; a longer one is the run that left
 // its first chunk, the middle chunks and the run that ended in its last.
-__device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &out) {
-  const uint32_t cnt = mw.bk_cnt[b];
+__device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &out, uint32_t cnt, uint32_t bs) {
   if (cnt == 0) return false;
-  const uint32_t bs = mw.bk_start[b];
   const uint32_t t0 = bs / L, t1 = (bs + cnt - 1) / L;
   if (t0 == t1) {
     out = mw.bk_sum[b];
@@ -480,9 +478,18 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t s = p.H / p.P;
   ge_p3 U, T;
   bool u_set = false, t_set = false;
+  // the next bucket's count and start are loaded one iteration ahead, so
+  // only its point load is exposed
+  const uint32_t b0 = g * p.W * p.H + wdx * p.H + part * s;
+  uint32_t cnt = mw.bk_cnt[b0 + s - 1], bst = mw.bk_start[b0 + s - 1];
   for (int i = (int)s - 1; i >= 0; i--) {
     ge_p3 B;
-    if (bucket_value(mw, p.L, g * p.W * p.H + wdx * p.H + part * s + (uint32_t)i, B)) {
+    const uint32_t c_i = cnt, s_i = bst;
+    if (i > 0) {
+      cnt = mw.bk_cnt[b0 + (uint32_t)i - 1];
+      bst = mw.bk_start[b0 + (uint32_t)i - 1];
+    }
+    if (bucket_value(mw, p.L, b0 + (uint32_t)i, B, c_i, s_i)) {
       if (u_set) p3_add(U, B);
       else { U = B; u_set = true; }
     }
@@ -494,7 +501,7 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   if (!u_set) ge_p3_identity(U);
   if (!t_set) ge_p3_identity(T);
   mw.wpart[2ull * t] = T;
-  mw.wpart[2ull * t + 1] = U;
+  if (p.P > 1) mw.wpart[2ull * t + 1] = U;  // P = 1: k_msm_horner reads T only
 }
 
 // Window sums: S_w = sum_q T_q + s * sum_q q U_q (s = H / P).
