@@ -84,7 +84,11 @@ struct MsmParams {
     p.W = merged ? p.WR : (254 + c - 1) / c;
     p.H = 1u << (c - 1);
     const uint32_t m = 1u << m_log2;
-    const uint32_t slots = merged ? m * p.WR : (2 * m + 1) * p.W;
+    // entries per group <= nonzero digits: R weights z < 2^128 (WR windows;
+    // the located pass's z (j + 1) < 2^136), A weights and the B scalar < l
+    // (W windows)
+    const uint32_t rw = p.WR > (136 + c - 1) / c ? p.WR : (136 + c - 1) / c;
+    const uint32_t slots = merged ? m * p.WR : m * rw + (m + 1) * p.W;
     p.cap = (slots + kMsmChunkMax - 1) / kMsmChunkMax * kMsmChunkMax;
     // chunk length at least the mean bucket size of the low windows (2m / H
     // entries) so buckets rarely span chunks (few partials to merge);

@@ -373,11 +373,13 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     const uint32_t e = e0 + tid + r * BS;
     for_each_digit<ZW>(z[r], WRz, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      if (pos >= p.cap) return;  // cannot happen (MsmParams::make bounds the digits); never write past the group
       ent_pt[pos] = ((KM ? e : 2 * e) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
     if (!KM) for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      if (pos >= p.cap) return;  // cannot happen (MsmParams::make bounds the digits); never write past the group
       ent_pt[pos] = ((2 * e + 1) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
@@ -385,6 +387,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   if (!KM && tid == 0) {
     for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool neg) {
       const uint32_t pos = atomicAdd(&hist[bk], 1u);
+      if (pos >= p.cap) return;  // cannot happen (MsmParams::make bounds the digits); never write past the group
       ent_pt[pos] = (mw.n_pts << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
