@@ -354,13 +354,18 @@ def header_hash(h) -> bytes:
     return _merkle(leaves)
 
 
-def _signed_header(H, chain_id, height, round_, t, vals, nvals, signers_sorted, last_block_id, rng, sign=True):
-    """A header over (vals, nvals) and the commit of all signers for it."""
+def _header_and_block_id(H, chain_id, height, t, vals, nvals, last_block_id, rng):
+    """A header over (vals, nvals) and the BlockID of its hash."""
     hdr = H.Header(chain_id=chain_id, height=height, time=t, last_block_id=last_block_id,
                    last_commit_hash=_rand32(rng), data_hash=_rand32(rng), validators_hash=_valset_hash(vals),
                    next_validators_hash=_valset_hash(nvals), consensus_hash=_rand32(rng), app_hash=_rand32(rng)[:20],
                    proposer_address=vals.validators[0].address)
-    hbid = H.BlockID(header_hash(hdr), 1, _rand32(rng))
+    return hdr, H.BlockID(header_hash(hdr), 1, _rand32(rng))
+
+
+def _signed_header(H, chain_id, height, round_, t, vals, nvals, signers_sorted, last_block_id, rng, sign=True):
+    """A header over (vals, nvals) and the commit of all signers for it."""
+    hdr, hbid = _header_and_block_id(H, chain_id, height, t, vals, nvals, last_block_id, rng)
     bid = BlockID(hbid.hash, PartSetHeader(hbid.psh_total, hbid.psh_hash))
     sigs = []
     for i, s in enumerate(signers_sorted):
@@ -370,70 +375,137 @@ def _signed_header(H, chain_id, height, round_, t, vals, nvals, signers_sorted, 
     return H.SignedHeader(hdr, H.Commit(height, round_, hbid, sigs))
 
 
+@dataclass
+class PackedVotes:
+    """Every commit vote of a generated chain as one packed batch (the
+    input of a test's checker): commit c's votes are entries [commit_off[c],
+    commit_off[c + 1]) in signature order; key_idx / seeds name the signer."""
+    batch: "Batch"
+    commit_off: np.ndarray
+
+
+class _VoteSink:
+    """Collects commit votes (messages built and signed in bulk, bulk.py)."""
+
+    def __init__(self, seeds: List[bytes]):
+        self.seeds = seeds
+        self.msgs, self.offs, self.keys, self.counts = [], [], [], []
+
+    def add_commit(self, chain_id, height, round_, hbid, key_ids, secs, nanos):
+        from . import bulk
+        bid = BlockID(hbid.hash, PartSetHeader(hbid.psh_total, hbid.psh_hash))
+        m, o = bulk.vote_messages(bulk.commit_vote_head(height, round_, bid), chain_id, secs, nanos)
+        self.msgs.append(m)
+        self.offs.append(o)
+        self.keys.append(np.asarray(key_ids, np.uint32))
+        self.counts.append(len(key_ids))
+
+    def sign(self, pks: List[bytes]) -> PackedVotes:
+        from . import bulk
+        msg = np.concatenate(self.msgs) if self.msgs else np.zeros(0, np.uint8)
+        lens = np.concatenate([o[1:] - o[:-1] for o in self.offs]) if self.offs else np.zeros(0, np.uint32)
+        off = np.zeros(len(lens) + 1, np.uint32)
+        off[1:] = np.cumsum(lens)
+        keys = np.concatenate(self.keys) if self.keys else np.zeros(0, np.uint32)
+        sig = bulk.sign_many(self.seeds, keys, msg, off)
+        pk_tab = np.frombuffer(b"".join(pks), np.uint8).reshape(-1, 32)
+        pk = pk_tab[keys].reshape(-1) if len(keys) else np.zeros(0, np.uint8)
+        co = np.zeros(len(self.counts) + 1, np.int64)
+        co[1:] = np.cumsum(self.counts)
+        return PackedVotes(Batch(pk, sig, msg, off), co)
+
+
+def _commit_sigs(H, packed: PackedVotes, c: int, addrs, secs, nanos):
+    lo = int(packed.commit_off[c])
+    raw = packed.batch.sig[64 * lo:64 * int(packed.commit_off[c + 1])].tobytes()
+    return [H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, a, (int(s), int(ns)), raw[64 * i:64 * i + 64])
+            for i, (a, s, ns) in enumerate(zip(addrs, secs, nanos))]
+
+
 def _rand32(rng) -> bytes:
     return bytes(rng.randrange(256) for _ in range(32))
 
 
-def make_light_chain(n_headers: int, n_vals: int = 100, chain_id: str = "test", rotate: int = 1, seed: int = 7):
+def make_light_chain(n_headers: int, n_vals: int = 100, chain_id: str = "test", rotate: int = 1, seed: int = 7,
+                     packed: bool = False):
     """Config 3 shape (light/helpers_test.go:165-216 genLightBlocksWithKeys):
     n_vals validators of power 2, `rotate` keys replaced per height, round 1,
     every validator signs, one header per second.  Returns (trusted
     LightBlock at height 1, [LightBlock] for heights 2..n_headers+1); every
     LightBlock carries its validator set and the next one, every header's
-    Hash() is the BlockID its commit signs."""
+    Hash() is the BlockID its commit signs.  packed=True also returns every
+    commit's votes as one PackedVotes (trusted block first).  The set at
+    step s (height s + 1) is keys [s rotate, s rotate + n_vals) (ChangeKeys:
+    the oldest `rotate` keys leave, new ones join); messages and signatures
+    are made in bulk (bulk.py)."""
     from .. import host as H
+    from . import bulk
     rng = random.Random(seed)
-    next_key = [n_vals]
-    signers = [Ed25519Signer(key_seed(i, "lkey")) for i in range(n_vals)]
+    n_keys = (n_headers + 1) * rotate + n_vals
+    seeds = [key_seed(k, "lkey") for k in range(n_keys)]
+    pks = bulk.public_keys(seeds)
+    addr = [hashlib.sha256(pk).digest()[:20] for pk in pks]
+    sets = {}
 
-    def valset(sgs):
-        vs = sorted(sgs, key=lambda s: hashlib.sha256(s.public_key).digest()[:20])
-        return vs, H.ValidatorSet([H.Validator(hashlib.sha256(s.public_key).digest()[:20], s.public_key, 2)
-                                   for s in vs], proposer_index=0)
-
-    def rotated(cur):
-        nxt = list(cur)
-        for _ in range(rotate):
-            nxt = nxt[1:] + [Ed25519Signer(key_seed(next_key[0], "lkey"))]
-            next_key[0] += 1
-        return nxt
+    def valset(step):
+        if step not in sets:
+            ks = sorted(range(step * rotate, step * rotate + n_vals), key=lambda k: addr[k])
+            sets[step] = (ks, H.ValidatorSet([H.Validator(addr[k], pks[k], 2) for k in ks], proposer_index=0))
+            sets.pop(step - 2, None)
+        return sets[step]
 
     t0 = 1577836800
-    cur = signers
-    nxt = rotated(cur)
-    out = []
+    sink = _VoteSink(seeds)
+    heads = []
     last_bid = H.BlockID()
     for h in range(1, n_headers + 2):
-        vs, vals = valset(cur)
-        _, nvals = valset(nxt)
-        sh = _signed_header(H, chain_id, h, 1, (t0 + h, 0), vals, nvals, vs, last_bid, rng)
-        out.append(H.LightBlock(sh, vals, nvals))
-        last_bid = sh.commit.block_id
-        cur, nxt = nxt, rotated(nxt)
+        ks, vals = valset(h - 1)
+        _, nvals = valset(h)
+        hdr, hbid = _header_and_block_id(H, chain_id, h, (t0 + h, 0), vals, nvals, last_bid, rng)
+        sink.add_commit(chain_id, h, 1, hbid, ks, [t0 + h] * n_vals, list(range(n_vals)))
+        heads.append((hdr, hbid, vals, nvals))
+        last_bid = hbid
+    pv = sink.sign(pks)
+    out = []
+    for c, (hdr, hbid, vals, nvals) in enumerate(heads):
+        sigs = _commit_sigs(H, pv, c, [v.address for v in vals.validators], [hdr.time[0]] * n_vals, range(n_vals))
+        out.append(H.LightBlock(H.SignedHeader(hdr, H.Commit(hdr.height, 1, hbid, sigs)), vals, nvals))
+    if packed:
+        return out[0], out[1:], pv
     return out[0], out[1:]
 
 
-def make_block_chain(n_blocks: int, n_vals: int = 175, chain_id: str = "test_chain_id", seed: int = 11):
+def make_block_chain(n_blocks: int, n_vals: int = 175, chain_id: str = "test_chain_id", seed: int = 11,
+                     packed: bool = False):
     """Config 4 shape: a chain of n_blocks (heights 1..n_blocks, initial height
     1) with a static n_vals-validator set; block h carries LastCommit = the
-    commit for h-1 (none at height 1).  Returns (ValidatorSet, [Block])."""
+    commit for h-1 (none at height 1).  Returns (ValidatorSet, [Block]);
+    packed=True also returns the votes of the commits for heights
+    1..n_blocks as one PackedVotes (commit c = height c + 1)."""
     from .. import host as H
     from ..chains import Block
+    from . import bulk
     rng = random.Random(seed)
-    signers = sorted((Ed25519Signer(key_seed(i, "bkey")) for i in range(n_vals)),
-                     key=lambda s: hashlib.sha256(s.public_key).digest()[:20])
-    vals = H.ValidatorSet([H.Validator(hashlib.sha256(s.public_key).digest()[:20], s.public_key, 10)
-                           for s in signers], proposer_index=0)
-    blocks = []
-    prev_commit = None
+    seeds = [key_seed(i, "bkey") for i in range(n_vals)]
+    pks = bulk.public_keys(seeds)
+    addr = [hashlib.sha256(pk).digest()[:20] for pk in pks]
+    ks = sorted(range(n_vals), key=lambda k: addr[k])
+    vals = H.ValidatorSet([H.Validator(addr[k], pks[k], 10) for k in ks], proposer_index=0)
+    sink = _VoteSink(seeds)
+    bids = []
+    nanos = [i * 1000 for i in range(n_vals)]
     for h in range(1, n_blocks + 1):
         bid = random_block_id(rng)
         hbid = H.BlockID(bid.hash, bid.part_set_header.total, bid.part_set_header.hash)
+        bids.append(hbid)
+        sink.add_commit(chain_id, h, 0, hbid, ks, [1577836800 + h] * n_vals, nanos)
+    pv = sink.sign(pks)
+    addrs = [v.address for v in vals.validators]
+    blocks = []
+    prev_commit = None
+    for h, hbid in enumerate(bids, start=1):
         blocks.append(Block(h, hbid, prev_commit))
-        sigs = []
-        for i, s in enumerate(signers):
-            ts = (1577836800 + h, i * 1000)
-            msg = commit_vote_message(chain_id, h, 0, bid, ts[0], ts[1])
-            sigs.append(H.CommitSig(H.BLOCK_ID_FLAG_COMMIT, vals.validators[i].address, ts, s.sign(msg)))
-        prev_commit = H.Commit(h, 0, hbid, sigs)
+        prev_commit = H.Commit(h, 0, hbid, _commit_sigs(H, pv, h - 1, addrs, [1577836800 + h] * n_vals, nanos))
+    if packed:
+        return vals, blocks, pv
     return vals, blocks

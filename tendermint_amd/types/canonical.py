@@ -94,9 +94,9 @@ def _timestamp(ts: Timestamp) -> bytes:
     return out
 
 
-def canonical_vote(chain_id: str, vtype: int, height: int, round_: int, block_id: Optional[BlockID],
-                   timestamp: Timestamp) -> bytes:
-    """Proto encoding of CanonicalVote (no length prefix)."""
+def canonical_vote_head(vtype: int, height: int, round_: int, block_id: Optional[BlockID]) -> bytes:
+    """The CanonicalVote fields before the timestamp (type, height, round,
+    block ID): the part every vote of one commit shares."""
     out = b""
     if vtype != 0:
         out += b"\x08" + uvarint(vtype)
@@ -107,6 +107,13 @@ def canonical_vote(chain_id: str, vtype: int, height: int, round_: int, block_id
     if block_id is not None and not block_id.is_nil():
         cb = _canonical_block_id(block_id)
         out += b"\x22" + uvarint(len(cb)) + cb
+    return out
+
+
+def canonical_vote(chain_id: str, vtype: int, height: int, round_: int, block_id: Optional[BlockID],
+                   timestamp: Timestamp) -> bytes:
+    """Proto encoding of CanonicalVote (no length prefix)."""
+    out = canonical_vote_head(vtype, height, round_, block_id)
     ts = _timestamp(timestamp)
     out += b"\x2a" + uvarint(len(ts)) + ts
     cid = chain_id.encode()

@@ -18,8 +18,8 @@ from tendermint_amd import _native as N, host as H, chains
 from tendermint_amd.testing import factory as Fa
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--headers", type=int, default=2000)
-ap.add_argument("--blocks", type=int, default=1000)
+ap.add_argument("--headers", type=int, default=10_000)
+ap.add_argument("--blocks", type=int, default=10_000)
 ap.add_argument("--c5", type=int, default=1_000_000)
 ap.add_argument("--only", default="1,3,4,5")
 ap.add_argument("--c5-methods", default="", help="comma list of C5 method labels (default: all)")
