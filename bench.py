@@ -284,7 +284,37 @@ def cpu_baseline(batches, seconds_target: float = 4.0):
     out["per_entry_port"] = {"value": round(reps * batch.n / wall, 1), "unit": "verifies/s", "cores": threads,
                              "sample": f"C2 batch x {reps} passes, oracle/c/ed25519_oracle.c per-entry verification"}
     out["openssl_proxy"] = _openssl_proxy(threads)
+    out["verify_commit_150"] = _c1_cpu(oracle_c)
     return out
+
+
+def _c1_cpu(oracle_c, calls: int = 300):
+    """BASELINE configs[0] on the CPU: types.VerifyCommit's signature work on
+    the 150-validator C1 commit, one thread (the Go benchmark runs one
+    goroutine, types/validator_set_test.go:1530-1556): every vote's
+    sign-bytes, then one voi-style batch of 150 (oracle/c/ed25519_batch_cpu.c
+    oracle_verify_commit_cpu).  p50 / p99 over `calls` calls."""
+    from tendermint_amd.testing.bulk import commit_vote_head
+    from tendermint_amd.types.canonical import BlockID, PartSetHeader
+    vals, bid, commit = make_c1_commit(150)
+    head = commit_vote_head(3, 0, BlockID(bid.hash, PartSetHeader(bid.psh_total, bid.psh_hash)))
+    pk = np.frombuffer(b"".join(v.pub_key for v in vals.validators), np.uint8)
+    sig = np.frombuffer(b"".join(cs.signature for cs in commit.signatures), np.uint8)
+    call = oracle_c.CommitCPU(head, "test_chain_id", [cs.timestamp[0] for cs in commit.signatures],
+                              [cs.timestamp[1] for cs in commit.signatures], pk, sig)
+    assert call()
+    lat = []
+    for _ in range(calls):
+        t1 = time.perf_counter()
+        ok = call()
+        lat.append((time.perf_counter() - t1) * 1e3)
+        assert ok
+    lat.sort()
+    return {"p50_ms": round(lat[len(lat) // 2], 4), "p99_ms": round(lat[int(len(lat) * 0.99) - 1], 4),
+            "calls": calls, "cores": 1, "kind": "port",
+            "sample": "C1 commit (150 validators): 150 vote sign-bytes + one 150-entry voi-style batch verify, one "
+                      "thread, oracle/c/ed25519_batch_cpu.c (plain-C restatement; NOT the reference: Go/voi are not "
+                      "buildable here; voi's expanded-key cache not restated)"}
 
 
 def _openssl_proxy(threads: int, seconds_target: float = 5.0):
@@ -689,6 +719,12 @@ def main():
             result["data"] = "CPU STUB (--cpu-stub): control-flow check only, no verification, not a measurement"
         if world == 1 and not args.no_cpu_baseline and not stub:
             result["cpu_baseline"] = cpu_baseline(batches)
+            c1 = result["cpu_baseline"].get("verify_commit_150") or {}
+            if "verify_commit_150_p50_ms" in result and c1:
+                # beside the GPU's C1 latency: the CPU restatement, labelled
+                result["verify_commit_150_cpu_p50_ms"] = c1["p50_ms"]
+                result["verify_commit_150_cpu_p99_ms"] = c1["p99_ms"]
+                result["verify_commit_150_cpu_note"] = "CPU port, one thread, not the reference (cpu_baseline.verify_commit_150)"
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)

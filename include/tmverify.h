@@ -126,8 +126,14 @@ int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const ui
  * size, or 4..9; seed32: NULL = a fresh getrandom() key per call (production),
  * else a fixed ChaCha20 key (tests: reproducible weights).
  * opt_flags: TMV_BATCHOPT_STATS = count group verdicts (host-buffer calls;
- * costs one small device read per call). */
+ * costs one small device read per call); TMV_BATCHOPT_SUBCHECK_ON / _OFF =
+ * re-check failing groups by sub-groups of 8 before the per-entry fallback
+ * (default: for groups of >= 256, $TMV_SUBCHECK overrides); with it off,
+ * launches of >= $TMV_LOCATE_MIN (150000) entries locate a failing group's
+ * one bad entry by a second, index-weighted equation. */
 #define TMV_BATCHOPT_STATS 1u
+#define TMV_BATCHOPT_SUBCHECK_ON 2u
+#define TMV_BATCHOPT_SUBCHECK_OFF 4u
 int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bits, const uint8_t *seed32,
                           uint32_t opt_flags);
 /* Groups checked / failed since the context was opened (TMV_BATCHOPT_STATS). */
@@ -179,6 +185,31 @@ int tmv_kernel_timing_read(tmv_ctx *ctx, const char *kernel, double *total_ms, u
 
 /* Cumulative key-cache counters over the context's devices. */
 int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t *used, uint32_t *capacity);
+
+/* Library metrics (verifies/s, batch size, fallback count, H2D
+ * bytes -- the reference exports its own per package through Prometheus,
+ * e.g. internal/consensus/metrics.gen.go; a Go shim would publish these).
+ * Cumulative since tmv_open or the last tmv_metrics_reset.  The group fields
+ * count host-buffer calls made with TMV_BATCHOPT_STATS
+ * (tmv_set_batch_options); the rest are always kept. */
+typedef struct tmv_metrics {
+  uint64_t calls;               /* verification calls (host-buffer and device-resident entry points) */
+  uint64_t signatures;          /* entries submitted to them */
+  uint64_t max_batch;           /* largest call, in entries */
+  uint64_t batch_eq_signatures; /* entries verified through the batch equation */
+  uint64_t host_signatures;     /* entries of host-buffer calls */
+  double host_seconds;          /* wall time inside host-buffer calls (end-to-end rate = host_signatures / it) */
+  uint64_t h2d_bytes;           /* host-to-device bytes of host-buffer calls (zero-copy reads not counted) */
+  uint64_t d2h_bytes;           /* device-to-host bytes of host-buffer calls */
+  uint64_t groups;              /* batch-equation groups checked (TMV_BATCHOPT_STATS) */
+  uint64_t groups_failed;       /* of which failed */
+  uint64_t located_groups;      /* failing groups whose one bad entry the located pass named */
+  uint64_t fallback_signatures; /* entries verified one by one after failing groups */
+  uint64_t key_cache_hits;      /* expanded-key cache (TMV_FLAG_KEY_CACHE) */
+  uint64_t key_cache_misses;
+} tmv_metrics;
+int tmv_metrics_read(tmv_ctx *ctx, tmv_metrics *out);
+int tmv_metrics_reset(tmv_ctx *ctx);
 
 /* Device-resident variants: every pointer is device memory on HIP device
  * `device` (inputs already in HBM), `stream` is a hipStream_t (NULL = the

@@ -224,3 +224,59 @@ int oracle_ed25519_batch_verify_voi(const uint8_t *pk, const uint8_t *sig, const
     for (size_t i = 0; i < n; i++) ok &= out[i];
     return ok;
 }
+
+static size_t put_uvarint(uint8_t *p, uint64_t u) {
+    size_t n = 0;
+    while (u >= 0x80) { p[n++] = (uint8_t)(u | 0x80); u >>= 7; }
+    p[n++] = (uint8_t)u;
+    return n;
+}
+
+/* One commit vote's sign-bytes (types/vote.go:149-157 VoteSignBytes =
+ * MarshalDelimited(CanonicalVote)): uvarint(L) || head ||
+ * 2a len {08 secs, 10 nanos} || 32 len chain_id, head = the fields before the
+ * timestamp (type, height, round, block ID). */
+static size_t vote_sign_bytes(uint8_t *out, const uint8_t *head, uint32_t head_len, const uint8_t *chain,
+                              uint32_t chain_len, int64_t secs, int32_t nanos) {
+    uint8_t ts[24], tsl[10], chl[10];
+    size_t tl = 0;
+    if (secs) { ts[tl++] = 0x08; tl += put_uvarint(ts + tl, (uint64_t)secs); }
+    if (nanos) { ts[tl++] = 0x10; tl += put_uvarint(ts + tl, (uint64_t)(int64_t)nanos); }
+    const size_t tsl_n = put_uvarint(tsl, tl), chl_n = chain_len ? put_uvarint(chl, chain_len) : 0;
+    const size_t body = head_len + 1 + tsl_n + tl + (chain_len ? 1 + chl_n + chain_len : 0);
+    uint8_t *p = out;
+    p += put_uvarint(p, body);
+    memcpy(p, head, head_len); p += head_len;
+    *p++ = 0x2a; memcpy(p, tsl, tsl_n); p += tsl_n; memcpy(p, ts, tl); p += tl;
+    if (chain_len) { *p++ = 0x32; memcpy(p, chl, chl_n); p += chl_n; memcpy(p, chain, chain_len); p += chain_len; }
+    return (size_t)(p - out);
+}
+
+/* bench.py's C1 CPU baseline: the signature work of types.VerifyCommit on one
+ * commit of n votes (types/validation.go:154-258 verifyCommitBatch), on the
+ * calling thread -- every vote's sign-bytes (Commit.VoteSignBytes,
+ * types/block.go:836-862), then one voi-style batch of the n entries
+ * (BatchVerifier.Verify, crypto/ed25519/ed25519.go:231-233: one random linear
+ * combination, entry by entry if it fails).  A is decoded per entry (voi's
+ * expanded-key cache is not restated).  Returns 1 iff every entry is valid;
+ * out gets the vector. */
+int oracle_verify_commit_cpu(const uint8_t *head, uint32_t head_len, const uint8_t *chain, uint32_t chain_len,
+                             const int64_t *secs, const int32_t *nanos, const uint8_t *pk, const uint8_t *sig,
+                             uint32_t n, uint8_t *out, uint64_t seed) {
+    init_consts();
+    if (n == 0) return 0;
+    const size_t cap = (size_t)n * (head_len + chain_len + 48);
+    uint8_t *msg = (uint8_t *)malloc(cap);
+    uint32_t *off = (uint32_t *)malloc(4 * ((size_t)n + 1));
+    size_t o = 0;
+    off[0] = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        o += vote_sign_bytes(msg + o, head, head_len, chain, chain_len, secs[i], nanos[i]);
+        off[i + 1] = (uint32_t)o;
+    }
+    size_t failed = 0;
+    const int ok = oracle_ed25519_batch_verify_voi(pk, sig, msg, off, n, out, 1, n, seed, &failed);
+    free(msg);
+    free(off);
+    return ok;
+}

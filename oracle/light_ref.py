@@ -768,7 +768,10 @@ def verify_skipping(trusted: LightBlock, target: LightBlock, provider: Callable[
         elif e.kind == CANT_TRUST:
             if depth == len(cache) - 1:
                 pivot = schedule(verified.signed_header.header.height, cache[depth].signed_header.header.height)
-                cache.append(provider(pivot))
+                try:
+                    cache.append(provider(pivot))
+                except Exception as pe:  # light/client.go:706-709: the provider's error, wrapped
+                    return None, (verified.signed_header.header.height, pivot, LightError(OTHER, str(pe)))
             depth += 1
         else:
             return None, (verified.signed_header.header.height, cand.signed_header.header.height, e)

@@ -92,6 +92,38 @@ def ed25519_batch_verify_voi(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray, o
     return bool(ok), out[:n], failed.value
 
 
+class CommitCPU:
+    """types.VerifyCommit's signature work for one commit on the CPU, one
+    thread (c/ed25519_batch_cpu.c oracle_verify_commit_cpu: every vote's
+    sign-bytes, then one voi-style batch): bench.py's C1 CPU baseline.
+    Arrays are prepared once; __call__() verifies the commit again."""
+
+    def __init__(self, head: bytes, chain_id: str, secs, nanos, pk: np.ndarray, sig: np.ndarray):
+        L = lib()
+        if not getattr(L, "_commit_cpu", False):
+            L.oracle_verify_commit_cpu.restype = ctypes.c_int
+            L.oracle_verify_commit_cpu.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                   ctypes.c_uint64]
+            L._commit_cpu = True
+        self.L = L
+        self.head, self.chain = head, chain_id.encode()
+        self.secs = np.ascontiguousarray(secs, np.int64)
+        self.nanos = np.ascontiguousarray(nanos, np.int32)
+        self.pk, self.sig = np.ascontiguousarray(pk, np.uint8), np.ascontiguousarray(sig, np.uint8)
+        self.n = len(self.secs)
+        self.out = np.zeros(max(self.n, 1), np.uint8)
+        self.seed = 1
+
+    def __call__(self) -> bool:
+        self.seed += 1
+        return bool(self.L.oracle_verify_commit_cpu(self.head, len(self.head), self.chain, len(self.chain),
+                                                    self.secs.ctypes.data, self.nanos.ctypes.data,
+                                                    self.pk.ctypes.data, self.sig.ctypes.data, self.n,
+                                                    self.out.ctypes.data, self.seed))
+
+
 def sr25519_status_packed(pk, sig, msg, off, threads: int = 1) -> np.ndarray:
     n = len(off) - 1
     out = np.zeros(max(n, 1), np.int8)

@@ -31,6 +31,8 @@ TMV_FLAG_KEY_CACHE = 1
 TMV_FLAG_BATCH_EQUATION = 2
 TMV_FLAG_PER_ENTRY = 4
 TMV_BATCHOPT_STATS = 1
+TMV_BATCHOPT_SUBCHECK_ON = 2
+TMV_BATCHOPT_SUBCHECK_OFF = 4
 TMV_KIND_MIXED = 2
 TMV_VOTE_WITH_BLOCK = 0x80000000
 
@@ -46,7 +48,7 @@ EXPORTS = [
     "tmv_subgroup_stats", "tmv_validator_set_hashes",
     "tmv_verify_mixed_batch_ex", "tmv_verify_batch_device_ex", "tmv_verify_batches_device",
     "tmv_verify_votes", "tmv_vote_sign_bytes_device", "tmv_merkle_roots",
-    "tmv_kernel_timing", "tmv_kernel_timing_read",
+    "tmv_kernel_timing", "tmv_kernel_timing_read", "tmv_metrics_read", "tmv_metrics_reset",
     # include/tmhost.h
     "tmv_batch_new", "tmv_batch_add", "tmv_batch_len", "tmv_batch_verify", "tmv_batch_free",
     "tmv_vote_sign_bytes", "tmv_vote_template_encode", "tmv_verify_commit", "tmv_verify_commits",
@@ -59,6 +61,16 @@ class BatchRef(ctypes.Structure):
     _fields_ = [("pk", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("msg", ctypes.c_void_p),
                 ("msg_off", ctypes.c_void_p), ("n", ctypes.c_uint32), ("msg_bytes", ctypes.c_uint32),
                 ("status", ctypes.c_void_p)]
+
+
+class Metrics(ctypes.Structure):
+    """tmv_metrics (include/tmverify.h)."""
+    _fields_ = [("calls", ctypes.c_uint64), ("signatures", ctypes.c_uint64), ("max_batch", ctypes.c_uint64),
+                ("batch_eq_signatures", ctypes.c_uint64), ("host_signatures", ctypes.c_uint64),
+                ("host_seconds", ctypes.c_double), ("h2d_bytes", ctypes.c_uint64), ("d2h_bytes", ctypes.c_uint64),
+                ("groups", ctypes.c_uint64), ("groups_failed", ctypes.c_uint64),
+                ("located_groups", ctypes.c_uint64), ("fallback_signatures", ctypes.c_uint64),
+                ("key_cache_hits", ctypes.c_uint64), ("key_cache_misses", ctypes.c_uint64)]
 
 
 class VoteTemplate(ctypes.Structure):
@@ -143,6 +155,8 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.c_uint32, u8p, ctypes.c_size_t, u32p]
         L.tmv_ed25519_verify_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
         L.tmv_verify_mixed_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp, vp]
+        L.tmv_metrics_read.argtypes = [vp, ctypes.POINTER(Metrics)]
+        L.tmv_metrics_reset.argtypes = [vp]
         _lib = L
         return L
 
@@ -297,18 +311,20 @@ class Context:
         return ms.value, cnt.value
 
     def set_batch_options(self, group_log2: int = 0, window_bits: int = 0, seed: bytes | None = None,
-                          stats: bool = False) -> None:
+                          stats: bool = False, subcheck: bool | None = None) -> None:
         """Batch-equation options (tmv_set_batch_options): group size 2^group_log2,
         window bits, a fixed ChaCha20 key (tests only; None = fresh randomness
-        per call) and group-verdict counting."""
+        per call), group-verdict counting and sub-group bisection (None =
+        the default policy)."""
         sp = None
         if seed is not None:
             if len(seed) != 32:
                 raise ValueError("seed must be 32 bytes")
             self._seed_buf = np.frombuffer(seed, np.uint8).copy()
             sp = _p(self._seed_buf)
-        self._check(self._lib.tmv_set_batch_options(self._h, group_log2, window_bits, sp,
-                                                    TMV_BATCHOPT_STATS if stats else 0),
+        opt = (TMV_BATCHOPT_STATS if stats else 0) | \
+            ({True: TMV_BATCHOPT_SUBCHECK_ON, False: TMV_BATCHOPT_SUBCHECK_OFF}.get(subcheck, 0))
+        self._check(self._lib.tmv_set_batch_options(self._h, group_log2, window_bits, sp, opt),
                     "tmv_set_batch_options")
 
     def validator_set_hashes(self, pk: np.ndarray, kind: np.ndarray, power: np.ndarray,
@@ -350,6 +366,18 @@ class Context:
         self._check(self._lib.tmv_key_cache_stats(self._h, ctypes.byref(h), ctypes.byref(m), ctypes.byref(u),
                                                   ctypes.byref(c)), "tmv_key_cache_stats")
         return {"hits": h.value, "misses": m.value, "used": u.value, "capacity": c.value}
+
+    def metrics(self) -> dict:
+        """tmv_metrics: cumulative counters (plus verifies_per_s_host, the
+        end-to-end rate of the host-buffer calls)."""
+        m = Metrics()
+        self._check(self._lib.tmv_metrics_read(self._h, ctypes.byref(m)), "tmv_metrics_read")
+        d = {k: getattr(m, k) for k, _ in Metrics._fields_}
+        d["verifies_per_s_host"] = d["host_signatures"] / d["host_seconds"] if d["host_seconds"] else 0.0
+        return d
+
+    def metrics_reset(self) -> None:
+        self._check(self._lib.tmv_metrics_reset(self._h), "tmv_metrics_reset")
 
     def ed25519_verify_batch_device(self, device: int, d_pk: int, d_sig: int, d_msg: int, d_off: int, n: int,
                                     d_valid: int, stream: int = 0) -> None:

@@ -107,11 +107,15 @@ def verify_skipping(ctx, trusted: LightBlock, target: LightBlock, provider: Call
     current candidate, the rest of the cache and up to `speculate` further
     pivots (the heights schedule() would request next) in ONE engine call, and
     the results are consumed in the reference's order, so the trace and the
-    error equal the reference's.  Returns (trace heights, None) or
+    error equal the reference's.  A provider error on a speculative pivot
+    only stops the speculation; on a pivot the reference requests it is
+    returned as ErrVerificationFailed{verified, pivot, err}
+    (light/client.go:706-709).  Returns (trace heights, None) or
     (None, ErrVerificationFailed)."""
     run = verify_many or (lambda jobs: H.light_verify_many(ctx, jobs))
     cache = [target]
     fetched: Dict[int, LightBlock] = {}
+    refused: Dict[int, Exception] = {}  # speculative fetches that failed (asked again only when needed)
     depth = 0
     verified = trusted
     trace = [trusted.height]
@@ -121,6 +125,17 @@ def verify_skipping(ctx, trusted: LightBlock, target: LightBlock, provider: Call
         if h not in fetched:
             fetched[h] = provider(h)
         return fetched[h]
+
+    def speculative(h: int) -> Optional[LightBlock]:
+        """A pivot the reference may never request: a provider error only
+        ends the speculation (the reference would not have seen it)."""
+        if h in refused:
+            return None
+        try:
+            return block_at(h)
+        except Exception as e:  # noqa: BLE001 -- any provider failure
+            refused[h] = e
+            return None
 
     while True:
         cand = cache[depth]
@@ -132,7 +147,10 @@ def verify_skipping(ctx, trusted: LightBlock, target: LightBlock, provider: Call
                 p = schedule(verified.height, last)
                 if p <= verified.height or p >= last:
                     break
-                batch.append(block_at(p))
+                b = speculative(p)
+                if b is None:
+                    break
+                batch.append(b)
                 last = p
             # the client passes the verified block's own validator set
             # (light/client.go:680-681)
@@ -151,7 +169,12 @@ def verify_skipping(ctx, trusted: LightBlock, target: LightBlock, provider: Call
             trace.append(verified.height)
         elif kind == H.LIGHT_ERR_CANT_TRUST:
             if depth == len(cache) - 1:
-                cache.append(block_at(schedule(verified.height, cache[depth].height)))
+                pivot = schedule(verified.height, cache[depth].height)
+                refused.pop(pivot, None)  # the reference requests this one: ask again
+                try:
+                    cache.append(block_at(pivot))
+                except Exception as e:  # noqa: BLE001 -- light/client.go:706-709
+                    return None, VerificationFailed(verified.height, pivot, H.LIGHT_ERR_OTHER, str(e))
             depth += 1
         else:
             return None, VerificationFailed(verified.height, cand.height, kind, text)

@@ -74,33 +74,68 @@ TMV_HD void fe_cmov(fe &h, const fe &g, bool b) {
   for (int i = 0; i < 10; i++) h.v[i] = b ? g.v[i] : h.v[i];
 }
 
+// Rounding bias of column i: it is carried with a shift of 26 (even i) or
+// 25 (odd i) bits, rounded to nearest: k = (c + 2^(shift-1)) >> shift.
+TMV_HD int64_t carry_bias(int i) { return (int64_t)1 << ((i & 1) ? 24 : 25); }
+// Column accumulation c + a * b as one v_mad_i64_i32, written out on the
+// device: left to itself the compiler splits each column into partial sums
+// joined by extra 64-bit adds and moves a constant addend (the carry bias
+// below) to a separate add at the end -- 10 + 10 extra adds per multiply.
+// Ten independent columns give the scheduler enough parallelism.
+TMV_HD int64_t mad_acc(int32_t a, int32_t b, int64_t c) {
+  int64_t r = c + (int64_t)a * b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(r));  // no instruction: keeps the column one chain
+#endif
+  return r;
+}
+// carry_bias(i) + a * b (the column's first product; the bias from an SGPR pair)
+TMV_HD int64_t mad_bias(int32_t a, int32_t b, int i) {
+  int64_t bias = carry_bias(i);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(bias));  // an opaque addend, so the multiply-add takes it
+#endif
+  return mad_acc(a, b, bias);
+}
+
 // Carry a column-sum vector back to level 1.  Two interleaved chains
-// (0->1->2->3->4 and 4->5->...->9->0->1) for ILP.
-TMV_HD void fe_carry_wide(fe &h, int64_t c[10]) {
-  const int64_t R25 = (int64_t)1 << 25, R24 = (int64_t)1 << 24;
+// (0->1->2->3->4 and 4->5->...->9->0->1) for ILP.  The columns arrive
+// already holding their rounding bias (c[i] = carry_bias(i) + sum: the
+// multiplies start each column's accumulation at its bias instead of 0), so
+// a step is k = c >> shift (no rounding add), the remainder keeps the bias
+// through later carries into it, and each limb drops it once at the end --
+// the same limbs as rounding every step, 12 fewer 64-bit adds per multiply.
+TMV_HD void fe_carry_biased(fe &h, int64_t c[10]) {
   int64_t k;
-  k = (c[0] + R25) >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
-  k = (c[4] + R25) >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
-  k = (c[1] + R24) >> 25; c[2] += k; c[1] -= k * ((int64_t)1 << 25);
-  k = (c[5] + R24) >> 25; c[6] += k; c[5] -= k * ((int64_t)1 << 25);
-  k = (c[2] + R25) >> 26; c[3] += k; c[2] -= k * ((int64_t)1 << 26);
-  k = (c[6] + R25) >> 26; c[7] += k; c[6] -= k * ((int64_t)1 << 26);
-  k = (c[3] + R24) >> 25; c[4] += k; c[3] -= k * ((int64_t)1 << 25);
-  k = (c[7] + R24) >> 25; c[8] += k; c[7] -= k * ((int64_t)1 << 25);
-  k = (c[4] + R25) >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
-  k = (c[8] + R25) >> 26; c[9] += k; c[8] -= k * ((int64_t)1 << 26);
-  k = (c[9] + R24) >> 25; c[0] += k * 19; c[9] -= k * ((int64_t)1 << 25);
-  k = (c[0] + R25) >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
+  k = c[0] >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
+  k = c[4] >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
+  k = c[1] >> 25; c[2] += k; c[1] -= k * ((int64_t)1 << 25);
+  k = c[5] >> 25; c[6] += k; c[5] -= k * ((int64_t)1 << 25);
+  k = c[2] >> 26; c[3] += k; c[2] -= k * ((int64_t)1 << 26);
+  k = c[6] >> 26; c[7] += k; c[6] -= k * ((int64_t)1 << 26);
+  k = c[3] >> 25; c[4] += k; c[3] -= k * ((int64_t)1 << 25);
+  k = c[7] >> 25; c[8] += k; c[7] -= k * ((int64_t)1 << 25);
+  k = c[4] >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
+  k = c[8] >> 26; c[9] += k; c[8] -= k * ((int64_t)1 << 26);
+  k = c[9] >> 25; c[0] += k * 19; c[9] -= k * ((int64_t)1 << 25);
+  k = c[0] >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
 #pragma unroll
-  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)c[i];
+  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)(c[i] - carry_bias(i));
+}
+
+// The same for columns without the bias.
+TMV_HD void fe_carry_wide(fe &h, int64_t c[10]) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) c[i] += carry_bias(i);
+  fe_carry_biased(h, c);
 }
 
 // Re-carry any level <= 3 value to level 1.
 TMV_HD void fe_carry(fe &h, const fe &f) {
   int64_t c[10];
 #pragma unroll
-  for (int i = 0; i < 10; i++) c[i] = f.v[i];
-  fe_carry_wide(h, c);
+  for (int i = 0; i < 10; i++) c[i] = (int64_t)f.v[i] + carry_bias(i);
+  fe_carry_biased(h, c);
 }
 
 // 19 x as two full-rate shift-adds (v_mul_lo_u32 is quarter rate on CDNA4)
@@ -130,17 +165,16 @@ TMV_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   }
   int64_t c[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) c[k] = 0;
-#pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
     for (int j = 0; j < 10; j++) {
       const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      if (i + j < 10) c[i + j] += (int64_t)a * g.v[j];
-      else            c[i + j - 10] += (int64_t)a * g19[j];
+      if (i == 0) c[j] = mad_bias(a, g.v[j], j);  // column j starts at its bias
+      else if (i + j < 10) c[i + j] = mad_acc(a, g.v[j], c[i + j]);
+      else                 c[i + j - 10] = mad_acc(a, g19[j], c[i + j - 10]);
     }
   }
-  fe_carry_wide(h, c);
+  fe_carry_biased(h, c);
 }
 
 // h = f^2 (55 products via symmetry)
@@ -149,9 +183,10 @@ TMV_HD void fe_sq(fe &h, const fe &f) {
   int32_t f2[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = mul19(f.v[i]); }
+  // column k starts at its bias with its first product: (0, k) for k <= 9,
+  // then (k - 9, 9) for the wrapped columns 0..8 (i + j = k + 10)
   int64_t c[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) c[k] = 0;
+  bool started[10] = {false, false, false, false, false, false, false, false, false, false};
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -160,11 +195,13 @@ TMV_HD void fe_sq(fe &h, const fe &f) {
       const int oddodd = (i & 1) && (j & 1);
       int32_t a = (i == j) ? f.v[i] : f2[i];
       if (oddodd) a = 2 * a;
-      if (i + j < 10) c[i + j] += (int64_t)a * f.v[j];
-      else            c[i + j - 10] += (int64_t)a * f19[j];
+      const int k = i + j < 10 ? i + j : i + j - 10;
+      const int32_t b = i + j < 10 ? f.v[j] : f19[j];
+      if (!started[k]) { c[k] = mad_bias(a, b, k); started[k] = true; }
+      else c[k] = mad_acc(a, b, c[k]);
     }
   }
-  fe_carry_wide(h, c);
+  fe_carry_biased(h, c);
 }
 
 // h = 2 f^2

@@ -70,8 +70,12 @@ struct MsmParams {
   uint32_t P;        // lanes per window in k_msm_wpart (power of two <= H)
   uint32_t L;        // sorted entries per k_msm_accum lane (8, 16 or 32)
   uint32_t merged;   // key-merged form: R points only, W = WR
+  uint32_t sub;      // 1: sub-group bisection (k_msm_subcheck) of failing groups; set by the runtime
 
   TMV_HD uint32_t m() const { return 1u << m_log2; }
+  // windows of the located pass's R weights z (j + 1) < 2^(128 + m_log2)
+  // (signed digits need one bit more, as WR for z < 2^128)
+  TMV_HD uint32_t WL() const { return (129 + m_log2 + c - 1) / c; }
   TMV_HD uint32_t buckets_per_group() const { return W * H; }
   TMV_HD uint32_t chunks_per_group() const { return cap / L; }
 
@@ -80,14 +84,15 @@ struct MsmParams {
     p.m_log2 = m_log2;
     p.c = c;
     p.merged = merged ? 1 : 0;
+    p.sub = 0;
     p.WR = (129 + c - 1) / c;
     p.W = merged ? p.WR : (254 + c - 1) / c;
     p.H = 1u << (c - 1);
     const uint32_t m = 1u << m_log2;
     // entries per group <= nonzero digits: R weights z < 2^128 (WR windows;
-    // the located pass's z (j + 1) < 2^136), A weights and the B scalar < l
-    // (W windows)
-    const uint32_t rw = p.WR > (136 + c - 1) / c ? p.WR : (136 + c - 1) / c;
+    // the located pass's z (j + 1) < 2^(128 + m_log2), WL windows), A
+    // weights and the B scalar < l (W windows)
+    const uint32_t rw = p.WR > p.WL() ? p.WR : p.WL();
     const uint32_t slots = merged ? m * p.WR : m * rw + (m + 1) * p.W;
     p.cap = (slots + kMsmChunkMax - 1) / kMsmChunkMax * kMsmChunkMax;
     // chunk length at least the mean bucket size of the low windows (2m / H
@@ -128,6 +133,11 @@ struct MsmWork {
   ge_p3 *wpart;        // groups x W x P x 2: (T, U) of each window part
   ge_p3 *wsum;         // groups x W: window sums
   uint8_t *group_ok;   // groups
+  // 1 when a group's bucket entries would not fit its cap slots (cannot
+  // happen: MsmParams::make bounds the digits; k_msm_sort then leaves the
+  // group empty and the flag fails it).  [g]: group g (k_msm_horner),
+  // [groups + f]: the located pass's slot f (k_loc_search)
+  uint8_t *sort_ovf;   // 2 x groups
   uint32_t n_pts;      // index of B (= 2n)
   // sub-group bisection of failing groups (k_msm_subcheck; null in the
   // key-merged form, whose fallback is the key-cached comb)
@@ -140,6 +150,7 @@ struct MsmWork {
   fe *fail_T;            // groups x 8 fe: [8f .. 8f+3] T (P3Q lanes), [8f+4 .. 8f+7] T'
   uint32_t *loc_count;   // failing groups x m: entry count of the locate MSM (device)
   uint32_t *fb_count;    // entries in fb_list
+  uint32_t *loc_found;   // failing groups whose one bad entry the search named (tmv_metrics)
   uint32_t *fb_list;     // n: work indices verified one by one
   // key-merged form only (null otherwise)
   uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
@@ -153,7 +164,7 @@ struct MsmWork {
     const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
     const size_t chunks = ent / p.L;
     size_t b = (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
-               2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 16 * 16;
+               2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 2 * G + 16 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
     else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
               G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16;
@@ -177,6 +188,7 @@ struct MsmWork {
     w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.P * sizeof(ge_p3));
     w.wsum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * sizeof(ge_p3));
     w.group_ok = b + o; o = up(o + G);
+    w.sort_ovf = b + o; o = up(o + 2 * G);
     w.n_pts = 2 * n;
     w.wscal = w.bscal = nullptr;
     w.item_pt = nullptr;
@@ -184,7 +196,7 @@ struct MsmWork {
     w.sub_ok = nullptr;
     w.tabR = nullptr;
     w.fail_T = nullptr;
-    w.loc_count = w.fb_count = w.fb_list = nullptr;
+    w.loc_count = w.fb_count = w.fb_list = w.loc_found = nullptr;
     if (!p.merged) {
       w.fail_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
       w.fail_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
@@ -192,7 +204,8 @@ struct MsmWork {
       w.tabR = reinterpret_cast<fe *>(b + o); o = up(o + (size_t)n * 32 * sizeof(fe));
       w.fail_T = reinterpret_cast<fe *>(b + o); o = up(o + G * 8 * sizeof(fe));
       w.loc_count = reinterpret_cast<uint32_t *>(b + o);
-      w.fb_count = w.loc_count + 1; o = up(o + 16);
+      w.fb_count = w.loc_count + 1;
+      w.loc_found = w.loc_count + 2; o = up(o + 16);
       w.fb_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4ull * n);
     }
     if (p.merged) {

@@ -171,7 +171,8 @@ __device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &o
 // the key cache.  LOC (located fallback): block f sorts the f-th FAILING
 // group into slot f with every weight multiplied by (j + 1), j the entry's
 // index in its group, so the same bucket stages compute
-// T'_f = sum (j+1) z_j Delta_j (z_j (j+1) < 2^136: ceil(136/c) R windows).
+// T'_f = sum (j+1) z_j Delta_j (z_j (j+1) < 2^(128 + m_log2): p.WL() R
+// windows).
 template <bool SR, bool KM, int BS = kMsmSortBlock, bool LOC = false>
 __global__ void __launch_bounds__(BS)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
@@ -187,6 +188,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     if (g == 0 && tid == 0) {
       *mw.loc_count = nf << p.m_log2;  // the bucket stages' entry count: nf slots
       *mw.fb_count = 0;                // k_loc_search appends the entries left to verify
+      *mw.loc_found = 0;
     }
     if (g >= nf) return;  // block-uniform
   }
@@ -210,8 +212,8 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   uint32_t *scan = red + BS * 9;    // BS + 1
 
   constexpr int R = 4;  // entries per thread: m <= 4 * BS
-  constexpr int ZW = LOC ? 5 : 4;  // words of the R weight (LOC: z (j + 1) < 2^136)
-  const uint32_t WRz = LOC ? (136 + p.c - 1) / p.c : p.WR;
+  constexpr int ZW = LOC ? 5 : 4;  // words of the R weight (LOC: z (j + 1) < 2^(128 + m_log2), m_log2 <= 31)
+  const uint32_t WRz = LOC ? p.WL() : p.WR;
   uint32_t z[R][ZW], wv[R][8];
   bool live[R];
   uint32_t acc[9];
@@ -352,6 +354,19 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   __syncthreads();
   const uint32_t gbase = slot * p.cap;
   const uint32_t bbase = slot * WH;
+  // more entries than slots cannot happen (MsmParams::make sizes cap by the
+  // digits that can occur); if it did, leave the group empty and flag it so
+  // k_msm_horner / k_loc_search fail it -- never a wrong sum
+  const bool ovf = scan[BS] > p.cap;  // block-uniform
+  if (tid == 0) mw.sort_ovf[(LOC ? p.groups : 0) + slot] = ovf ? 1 : 0;
+  if (ovf) {
+    for (uint32_t t = tid; t < WH; t += BS) {
+      mw.bk_start[bbase + t] = gbase;
+      mw.bk_cnt[bbase + t] = 0;
+    }
+    for (uint32_t t = tid; t < p.cap; t += BS) mw.ent_bk[gbase + t] = kMsmEmpty;
+    return;
+  }
   {
     uint32_t off = scan[tid];
     for (uint32_t t = lo; t < hi; t++) {
@@ -372,22 +387,19 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     if (!live[r]) continue;
     const uint32_t e = e0 + tid + r * BS;
     for_each_digit<ZW>(z[r], WRz, p, [&](uint32_t bk, bool neg) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      if (pos >= p.cap) return;  // cannot happen (MsmParams::make bounds the digits); never write past the group
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);  // < cap: checked above
       ent_pt[pos] = ((KM ? e : 2 * e) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
     if (!KM) for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool neg) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      if (pos >= p.cap) return;  // cannot happen (MsmParams::make bounds the digits); never write past the group
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);  // < cap: checked above
       ent_pt[pos] = ((2 * e + 1) << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
   }
   if (!KM && tid == 0) {
     for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool neg) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);
-      if (pos >= p.cap) return;  // cannot happen (MsmParams::make bounds the digits); never write past the group
+      const uint32_t pos = atomicAdd(&hist[bk], 1u);  // < cap: checked above
       ent_pt[pos] = (mw.n_pts << 1) | (neg ? 1u : 0u);
       ent_bk[pos] = bbase + bk;
     });
@@ -583,6 +595,7 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
   } else {
     ok = quad::is_identity_times8(acc);
   }
+  ok = ok && !mw.sort_ovf[g];
   int f = -1;
   if (live && c == 0) {
     mw.group_ok[g] = ok ? 1 : 0;
@@ -655,8 +668,11 @@ k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   __syncthreads();
   const uint32_t e0 = mw.fail_list[f] << p.m_log2;
   const uint32_t mlive = min(m, entry_count(count_ptr, n) - e0);
-  if (s_cnt == 1 && (uint32_t)s_j < mlive) {  // block-uniform
-    if (threadIdx.x == 0) mw.fb_list[atomicAdd(mw.fb_count, 1u)] = e0 + (uint32_t)s_j;
+  if (s_cnt == 1 && (uint32_t)s_j < mlive && !mw.sort_ovf[p.groups + f]) {  // block-uniform
+    if (threadIdx.x == 0) {
+      mw.fb_list[atomicAdd(mw.fb_count, 1u)] = e0 + (uint32_t)s_j;
+      atomicAdd(mw.loc_found, 1u);
+    }
     return;
   }
   if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
@@ -956,6 +972,11 @@ static uint32_t locate_min() {
 
 uint32_t locate_min_entries() { return locate_min(); }
 
+bool locate_enabled(uint32_t n, const MsmParams &p) {
+  const uint32_t lmin = locate_min();
+  return fallback_compact() && lmin && n >= lmin && !p.sub && p.WL() <= p.W;
+}
+
 bool subcheck_enabled(uint32_t m_log2) {
   const int mode = subcheck_mode();
   return mode < 0 ? m_log2 >= 8 : mode == 1;
@@ -987,6 +1008,7 @@ static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0)
   mw.wpart += g0 * p.W * 2ull * p.P;
   mw.wsum += g0 * p.W;
   mw.group_ok += g0;
+  mw.sort_ovf += g0;  // [g] of the part's groups (the located half is the tail's, full structs)
   if (mw.sub_ok) mw.sub_ok += (g0 << p.m_log2) / kSubGroup;
   if (mw.tabR) mw.tabR += 32 * e0;
   return mw;
@@ -1041,8 +1063,7 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
   hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
                      nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const uint32_t lmin = locate_min();
-  if (compact && lmin && n >= lmin && !subcheck_enabled(p.m_log2) && (136 + p.c - 1) / p.c <= p.W) {
+  if (compact && locate_enabled(n, p)) {
     // second MSM over the failing groups (slot f = f-th failing group), then
     // the search, then one-by-one verification of the listed entries only
     if (p.m_log2 <= 8 && sort_block() == 64) {
@@ -1067,7 +1088,7 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
                                     nullptr, nullptr, nullptr, mw.fb_list, mw.fb_count);
   }
   const uint8_t *sub_ok = nullptr;
-  if (subcheck_enabled(p.m_log2)) {
+  if (p.sub) {
     // grid for every group failing; blocks past the failing count exit at once
     const uint64_t subs = (uint64_t)p.groups << (p.m_log2 - kSubGroupLog2);
     hipLaunchKernelGGL(k_msm_subcheck<SR>, dim3((uint32_t)((subs + 15) / 16)), dim3(64), 0, stream, sig, idx,

@@ -30,6 +30,7 @@
 #include "merlin_dev.h"
 #include "host/pool.h"
 #include "host/shard_plan.h"
+#include "host/shard_run.h"
 #include "host/wait.h"
 #include "ktimer.h"
 #include "verify_kernels.h"
@@ -175,8 +176,9 @@ struct Workspace {
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
   const uint8_t *sub_ok[2] = {nullptr, nullptr};  // sub-group verdicts (k_msm_subcheck), if it ran
-  uint32_t groups = 0, m_log2 = 0;
+  uint32_t groups = 0, m_log2 = 0, n = 0;
   const uint32_t *counts = nullptr;  // mixed launches: per-kind entry counts on the device
+  const uint32_t *loc[2] = {nullptr, nullptr};  // located pass ran: its (slots, fb_count, found) words
 };
 
 // One lane of the host-buffer pipeline: a stream with its own pinned and
@@ -369,7 +371,8 @@ int faulted_rc(Device &d) {
 // The key-merged form (merged = true; keyed batches are commit traffic,
 // nearly always valid) defaults to groups of 256: its MSM has only the R
 // points and its fallback is the cheaper key-cached comb.
-tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false, bool ed_only = false) {
+tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false, bool ed_only = false,
+                          int sub = -1) {
   // uncached ed25519 launches large enough for the located fallback
   // (tmv::locate_min_entries): groups of 128 (c = 6 by the cost model) --
   // a failing group costs one located entry, not 128 verifications; C2
@@ -393,6 +396,9 @@ tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged =
   tmv::MsmParams p = tmv::MsmParams::make(n, m_log2, c, merged);
   if (g_msm_chunk == 8 || g_msm_chunk == 16 || g_msm_chunk == 32) p.L = g_msm_chunk;
   if (g_msm_parts && g_msm_parts <= p.H && !(g_msm_parts & (g_msm_parts - 1))) p.P = g_msm_parts;
+  // sub-group bisection: the context's choice, else the default policy
+  // (the key-merged form's fallback is the key-cached comb: never)
+  p.sub = merged ? 0 : (sub < 0 ? (tmv::subcheck_enabled(m_log2) ? 1 : 0) : (uint32_t)sub);
   return p;
 }
 
@@ -436,11 +442,24 @@ struct tmv_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   // batch-equation options (tmv_set_batch_options)
   uint32_t msm_m_log2 = 0, msm_c = 0;
+  int msm_sub = -1;  // TMV_BATCHOPT_SUBCHECK_ON / _OFF, -1 = default
   bool fixed_seed = false, stats = false;
   uint8_t seed[32] = {0};
   std::atomic<uint64_t> launches{0};
   std::atomic<uint64_t> groups{0}, groups_failed{0}, subgroups{0}, subgroups_failed{0};
+  // tmv_metrics
+  std::atomic<uint64_t> m_calls{0}, m_sigs{0}, m_max{0}, m_beq{0}, m_host_sigs{0}, m_host_ns{0}, m_h2d{0}, m_d2h{0},
+      m_located{0}, m_fallback{0};
+  uint64_t khits_base = 0, kmiss_base = 0;
   std::mutex opt_mu;
+
+  void count_call(uint64_t n) {
+    m_calls++;
+    m_sigs += n;
+    uint64_t cur = m_max.load();
+    while (n > cur && !m_max.compare_exchange_weak(cur, n)) {
+    }
+  }
 };
 
 // Options of one launch of n entries: per-entry or batch equation (flags,
@@ -452,11 +471,12 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
   else if (flags & TMV_FLAG_BATCH_EQUATION) o.batch_eq = true;
   else o.batch_eq = g_msm_min > 0 && n >= g_msm_min;
   if (!o.batch_eq) return o;
+  ctx->m_beq += n;
   uint8_t key[32];
   bool fixed;
   {
     std::lock_guard<std::mutex> lk(ctx->opt_mu);  // tmv_set_batch_options writes these
-    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged, ed_only);
+    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged, ed_only, ctx->msm_sub);
     fixed = ctx->fixed_seed;
     if (fixed) std::memcpy(key, ctx->seed, 32);
   }
@@ -483,11 +503,14 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
   auto it = d.ws.find(s);
   if (it == d.ws.end() || !it->second->group_ok[0]) return;
   Workspace &w = *it->second;
-  uint32_t live[2] = {0, 0};
+  uint32_t live[2] = {0, 0}, live_n[2] = {0, 0};
   if (w.counts) {
     uint32_t c[2];
     if (hipMemcpy(c, w.counts, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) return;
-    for (int k = 0; k < 2; k++) live[k] = (c[k] + (1u << w.m_log2) - 1) >> w.m_log2;
+    for (int k = 0; k < 2; k++) {
+      live[k] = (c[k] + (1u << w.m_log2) - 1) >> w.m_log2;
+      live_n[k] = c[k];
+    }
   } else {
     live[0] = w.groups;
   }
@@ -499,6 +522,16 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
     for (uint8_t v : ok) failed += v ? 0 : 1;
     ctx->groups += live[k];
     ctx->groups_failed += failed;
+    if (failed && w.loc[k]) {  // located pass: its search counted the entries it left to verify
+      uint32_t lc[4];
+      if (hipMemcpy(lc, w.loc[k], sizeof(lc), hipMemcpyDeviceToHost) != hipSuccess) return;
+      ctx->m_fallback += lc[1];
+      ctx->m_located += lc[2];
+    } else if (failed && !w.sub_ok[k]) {  // every entry of a failing group
+      const uint32_t m = 1u << w.m_log2, nk = w.counts ? live_n[k] : w.n;
+      for (uint32_t g = 0; g < live[k]; g++)
+        if (!ok[g]) ctx->m_fallback += std::min<uint32_t>(m, nk - g * m);
+    }
     if (!w.sub_ok[k] || !failed) continue;
     // sub-groups of the failing groups (the only ones k_msm_subcheck writes)
     const uint32_t per = 1u << (w.m_log2 - tmv::kSubGroupLog2);
@@ -510,9 +543,17 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
         for (uint32_t j = 0; j < per; j++) sfail += sub[(size_t)g * per + j] ? 0 : 1;
     ctx->subgroups += failed * per;
     ctx->subgroups_failed += sfail;
+    // per-entry fallback by 16-entry blocks holding a failing sub-group
+    for (uint32_t g = 0; g < live[k]; g++)
+      if (!ok[g])
+        for (uint32_t j = 0; j + 1 < per + 1; j += 2) {
+          const bool bad = !sub[(size_t)g * per + j] || (j + 1 < per && !sub[(size_t)g * per + j + 1]);
+          if (bad) ctx->m_fallback += 2 * tmv::kSubGroup;
+        }
   }
   w.group_ok[0] = w.group_ok[1] = nullptr;
   w.sub_ok[0] = w.sub_ok[1] = nullptr;
+  w.loc[0] = w.loc[1] = nullptr;
 }
 
 static int init_device(Device &d) {
@@ -837,11 +878,14 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   if (e != hipSuccess) { set_error("batch check launch", e); return TMV_ERR_LAUNCH; }
   ws->group_ok[0] = mw.group_ok;
   ws->group_ok[1] = nullptr;
-  ws->sub_ok[0] = tmv::subcheck_enabled(o.p.m_log2) ? mw.sub_ok : nullptr;
+  ws->sub_ok[0] = o.p.sub ? mw.sub_ok : nullptr;
   ws->sub_ok[1] = nullptr;
   ws->groups = (n + o.p.m() - 1) >> o.p.m_log2;
   ws->m_log2 = o.p.m_log2;
+  ws->n = n;
   ws->counts = nullptr;
+  ws->loc[0] = tmv::locate_enabled(n, o.p) ? mw.loc_count : nullptr;
+  ws->loc[1] = nullptr;
   (void)hipEventRecord(ws->done, s);
   return 0;
 }
@@ -884,11 +928,14 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
                                       g_mixed_two ? &ks : nullptr);
     ws->group_ok[0] = m1.group_ok;
     ws->group_ok[1] = m2.group_ok;
-    ws->sub_ok[0] = tmv::subcheck_enabled(o.p.m_log2) ? m1.sub_ok : nullptr;
-    ws->sub_ok[1] = tmv::subcheck_enabled(o.p.m_log2) ? m2.sub_ok : nullptr;
+    ws->sub_ok[0] = o.p.sub ? m1.sub_ok : nullptr;
+    ws->sub_ok[1] = o.p.sub ? m2.sub_ok : nullptr;
     ws->groups = o.p.groups;
     ws->m_log2 = o.p.m_log2;
+    ws->n = n;
     ws->counts = counts;
+    ws->loc[0] = tmv::locate_enabled(n, o.p) ? m1.loc_count : nullptr;
+    ws->loc[1] = tmv::locate_enabled(n, o.p) ? m2.loc_count : nullptr;
   } else {
     e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed, idx_sr,
                                  status, s);
@@ -929,7 +976,9 @@ static int launch_key_merged(Device &d, const LaunchOpts &o, bool sr, const uint
   ws->sub_ok[0] = ws->sub_ok[1] = nullptr;
   ws->groups = o.p.groups;
   ws->m_log2 = o.p.m_log2;
+  ws->n = n;
   ws->counts = nullptr;
+  ws->loc[0] = ws->loc[1] = nullptr;  // the key-cached comb fallback checks every entry of a failing group
   (void)hipEventRecord(ws->done, s);
   return 0;
 }
@@ -1162,11 +1211,13 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       hipError_t ce;
       const size_t offs[4][2] = {{L.pk + 32ull * a, 32ull * (b - a)}, {L.sig + 64ull * a, 64ull * (b - a)},
                                  {L.off + 4ull * a, 4ull * (b - a + 1)}, {L.msg + m0, m1 - m0}};
-      for (const auto &c : offs)
+      for (const auto &c : offs) {
         if (c[1] && (ce = hipMemcpyAsync(dd + c[0], h + c[0], c[1], hipMemcpyHostToDevice, ln.copy)) != hipSuccess) {
           set_error("hipMemcpyAsync(H2D)", ce);
           return TMV_ERR_LAUNCH;
         }
+        ctx->m_h2d += c[1];
+      }
       if ((ce = hipEventRecord(ev, ln.copy)) != hipSuccess) {
         set_error("part event", ce);
         return TMV_ERR_LAUNCH;
@@ -1189,6 +1240,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       set_error("hipMemcpyAsync(D2H)", e);
       return TMV_ERR_LAUNCH;
     }
+    ctx->m_d2h += n;
     return 0;
   }
   const uint32_t G = merged ? o.p.groups : 0;
@@ -1277,6 +1329,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       set_error("hipMemcpyAsync(H2D)", e);
       return TMV_ERR_LAUNCH;
     }
+    ctx->m_h2d += L.msg + (total - L.total);
     const tmv::VoteTab *tab = reinterpret_cast<const tmv::VoteTab *>(dd + tab_at);
     if ((e = tmv::launch_vote_signbytes(reinterpret_cast<const tmv_vote *>(dd + votes_at), tab,
                                         dd + tab_at + vs->blob_at, doff, n, dd + L.msg, ln.stream)) != hipSuccess) {
@@ -1286,6 +1339,8 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
   } else if ((e = hipMemcpyAsync(ln.d_in.ptr, h, total, hipMemcpyHostToDevice, ln.stream)) != hipSuccess) {
     set_error("hipMemcpyAsync(H2D)", e);
     return TMV_ERR_LAUNCH;
+  } else {
+    ctx->m_h2d += total;
   }
   uint8_t *out = static_cast<uint8_t *>(zero_copy ? ln.h_out.dev : ln.d_out.ptr);
   const uint32_t *dslots = reinterpret_cast<const uint32_t *>(dd + kind_at);
@@ -1318,6 +1373,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     set_error("hipMemcpyAsync(D2H)", e);
     return TMV_ERR_LAUNCH;
   }
+  ctx->m_d2h += n;
   return 0;
 }
 
@@ -1334,6 +1390,18 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     return TMV_ERR_ARG;
   }
   read_env();
+  ctx->count_call(n);
+  const auto t_call = std::chrono::steady_clock::now();
+  struct HostTime {  // wall time of the call into tmv_metrics, on every return
+    tmv_ctx *c;
+    uint32_t n;
+    std::chrono::steady_clock::time_point t;
+    ~HostTime() {
+      c->m_host_sigs += n;
+      c->m_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now() - t).count();
+    }
+  } host_time{ctx, n, t_call};
   // streamed batch-equation chunks are large (one pipeline, one tail each);
   // other paths alternate smaller chunks over the lanes
   const uint32_t per_dev = n / (uint32_t)ctx->devs.size();
@@ -1347,42 +1415,42 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
   for (uint32_t s = 0; s < shards; s++)
     if (ctx->devs[s]->faulted) return faulted_rc(*ctx->devs[s]);
-  int rc = 0;
   EngineTimer tm;
-  auto harvest = [&](Device &d, HostLane &ln) {
-    if (ln.n == 0) return;
-    hipError_t e = wait_stream(d, ln.stream);
-    if (e != hipSuccess && rc == 0) {
-      if (e != hipErrorNotReady) set_error("hipStreamSynchronize", e);
-      rc = wait_rc(e);
-    }
-    if (rc == 0) std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
-    if (rc == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
-    ln.n = 0;
-  };
   // chunk k of every shard, then chunk k + 1: the devices work side by side
-  for (uint32_t k = 0; k < plan.max_chunks && rc == 0; k++) {
-    for (uint32_t s = 0; s < shards && rc == 0; s++) {
-      if (k >= plan.nchunks[s]) continue;
-      Device &d = *ctx->devs[s];
-      const uint32_t c0 = plan.chunk_lo(s, k), c1 = plan.chunk_lo(s, k + 1);
-      HostLane &ln = d.lane[k % g_host_lanes];
-      (void)hipSetDevice(d.id);
-      harvest(d, ln);  // the lane's previous chunk
-      if (rc != 0) break;
-      rc = stage_and_launch(ctx, flags, d, ln, sch, kind, pk, sig, msg, msg_off, c0, c1, vs);
-      if (rc == 0) { ln.lo = c0; ln.n = c1 - c0; }
-    }
-  }
-  tm.mark("launched", n);
-  for (uint32_t s = 0; s < shards; s++) {
-    Device &d = *ctx->devs[s];
-    (void)hipSetDevice(d.id);
-    for (HostLane &ln : d.lane) {
-      if (rc != 0) { if (ln.n && !d.faulted) (void)wait_stream(d, ln.stream); ln.n = 0; continue; }
-      harvest(d, ln);
-    }
-  }
+  // (host/shard_run.h; the CPU test double runs the same order)
+  int rc = tmh::run_shard_plan(
+      plan, g_host_lanes,
+      [&](uint32_t s, uint32_t lane, bool ok) -> int {
+        Device &d = *ctx->devs[s];
+        HostLane &ln = d.lane[lane];
+        if (ln.n == 0) return 0;
+        (void)hipSetDevice(d.id);
+        int r = 0;
+        if (ok || !d.faulted) {
+          const hipError_t e = wait_stream(d, ln.stream);
+          if (e != hipSuccess) {
+            if (e != hipErrorNotReady) set_error("hipStreamSynchronize", e);
+            r = wait_rc(e);
+          }
+        }
+        if (ok && r == 0) {
+          std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
+          if (ctx->stats) collect_stats(ctx, d, ln.stream);
+        }
+        ln.n = 0;
+        return r;
+      },
+      [&](uint32_t s, uint32_t lane, uint32_t c0, uint32_t c1) -> int {
+        Device &d = *ctx->devs[s];
+        HostLane &ln = d.lane[lane];
+        (void)hipSetDevice(d.id);
+        const int r = stage_and_launch(ctx, flags, d, ln, sch, kind, pk, sig, msg, msg_off, c0, c1, vs);
+        if (r == 0) {
+          ln.lo = c0;
+          ln.n = c1 - c0;
+        }
+        return r;
+      });
   tm.mark("synced", n);
   if (rc != 0) return rc;
   for (uint32_t i = 0; i < n; i++)
@@ -1544,6 +1612,7 @@ int tmv_set_batch_options(tmv_ctx *ctx, uint32_t group_log2, uint32_t window_bit
   ctx->fixed_seed = seed32 != nullptr;
   if (seed32) std::memcpy(ctx->seed, seed32, 32);
   ctx->stats = (opt_flags & TMV_BATCHOPT_STATS) != 0;
+  ctx->msm_sub = (opt_flags & TMV_BATCHOPT_SUBCHECK_ON) ? 1 : (opt_flags & TMV_BATCHOPT_SUBCHECK_OFF) ? 0 : -1;
   return 0;
 }
 
@@ -1576,6 +1645,49 @@ int tmv_key_cache_stats(tmv_ctx *ctx, uint64_t *hits, uint64_t *misses, uint32_t
   return 0;
 }
 
+int tmv_metrics_read(tmv_ctx *ctx, tmv_metrics *out) {
+  if (!ctx || !out) { set_error("null argument"); return TMV_ERR_ARG; }
+  std::memset(out, 0, sizeof(*out));
+  out->calls = ctx->m_calls;
+  out->signatures = ctx->m_sigs;
+  out->max_batch = ctx->m_max;
+  out->batch_eq_signatures = ctx->m_beq;
+  out->host_signatures = ctx->m_host_sigs;
+  out->host_seconds = (double)ctx->m_host_ns.load() * 1e-9;
+  out->h2d_bytes = ctx->m_h2d;
+  out->d2h_bytes = ctx->m_d2h;
+  out->groups = ctx->groups;
+  out->groups_failed = ctx->groups_failed;
+  out->located_groups = ctx->m_located;
+  out->fallback_signatures = ctx->m_fallback;
+  uint64_t h = 0, m = 0;
+  for (auto &d : ctx->devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    h += d->khits;
+    m += d->kmisses;
+  }
+  out->key_cache_hits = h - ctx->khits_base;
+  out->key_cache_misses = m - ctx->kmiss_base;
+  return 0;
+}
+
+int tmv_metrics_reset(tmv_ctx *ctx) {
+  if (!ctx) { set_error("null context"); return TMV_ERR_ARG; }
+  for (auto *a : {&ctx->m_calls, &ctx->m_sigs, &ctx->m_max, &ctx->m_beq, &ctx->m_host_sigs, &ctx->m_host_ns,
+                  &ctx->m_h2d, &ctx->m_d2h, &ctx->m_located, &ctx->m_fallback, &ctx->groups, &ctx->groups_failed,
+                  &ctx->subgroups, &ctx->subgroups_failed})
+    a->store(0);
+  uint64_t h = 0, m = 0;
+  for (auto &d : ctx->devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    h += d->khits;
+    m += d->kmisses;
+  }
+  ctx->khits_base = h;
+  ctx->kmiss_base = m;
+  return 0;
+}
+
 int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kind, const uint8_t *d_pk,
                                   const uint8_t *d_sig, const uint8_t *d_msg, const uint32_t *d_msg_off, uint32_t n,
                                   int8_t *d_status, void *stream) {
@@ -1587,6 +1699,7 @@ int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kin
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
   const LaunchOpts o = make_opts(ctx, 0, n);
+  ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc = launch_mixed(*dev, o, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
   return rc != 0 ? rc : TMV_NOT_ALL;
@@ -1605,6 +1718,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
+  ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   uint8_t *out = reinterpret_cast<uint8_t *>(d_status);
   int rc;
@@ -1660,6 +1774,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
   const uint32_t n = (uint32_t)N;
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
+  ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc;
   Workspace *ws = reserve_work(*dev, n, false, s, &rc, o.batch_eq ? &o.p : nullptr);
@@ -1827,6 +1942,7 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
   const LaunchOpts o = make_opts(ctx, 0, n, false, true);
+  ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc = launch_ed25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, d_valid, s);
   return rc != 0 ? rc : TMV_NOT_ALL;

@@ -114,12 +114,16 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
                                 uint8_t *out, int aligned, hipStream_t stream, const uint8_t *sub_ok = nullptr,
                                 const uint32_t *fail_list = nullptr, const uint32_t *fail_count = nullptr,
                                 const uint32_t *fb_list = nullptr, const uint32_t *fb_count = nullptr);
-// k_msm_subcheck runs before the per-entry fallback for groups of 2^m_log2
-// (default m >= 256; TMV_SUBCHECK=0 never, =1 always).
+// Default for MsmParams::sub: k_msm_subcheck runs before the per-entry
+// fallback for groups of 2^m_log2 (m >= 256; TMV_SUBCHECK=0 never, =1 always;
+// tmv_set_batch_options can override it per context).
 bool subcheck_enabled(uint32_t m_log2);
 // Launches of at least this many entries use the located fallback
 // (TMV_LOCATE_MIN, 0 = never).
 uint32_t locate_min_entries();
+// Whether a batch-equation launch of n entries with these parameters runs
+// the located fallback (tmv_metrics reads its counters).
+bool locate_enabled(uint32_t n, const MsmParams &p);
 hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
                             uint8_t *out, hipStream_t stream);
 

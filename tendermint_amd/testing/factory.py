@@ -121,7 +121,8 @@ class Batch:
         pos = np.arange(int(off[-1]), dtype=np.int64) - np.repeat(off[:-1].astype(np.int64), lens) + \
             np.repeat(starts, lens)
         return Batch(self.pk.reshape(-1, 32)[idx].reshape(-1), self.sig.reshape(-1, 64)[idx].reshape(-1),
-                     self.msg[pos] if len(pos) else np.zeros(0, np.uint8), off, [self.kinds[i] for i in idx])
+                     self.msg[pos] if len(pos) else np.zeros(0, np.uint8), off,
+                     [self.kinds[i] for i in idx] if self.kinds else [])
 
     def tile(self, n: int) -> "Batch":
         """Repeat entries cyclically up to n (throughput runs on >10k)."""

@@ -17,6 +17,7 @@
 #include "../../include/tmverify.h"
 #include "../../tendermint_amd/csrc/host/tm_light.h"
 #include "../../tendermint_amd/csrc/host/shard_plan.h"
+#include "../../tendermint_amd/csrc/host/shard_run.h"
 #include "../../tendermint_amd/csrc/host/wait.h"
 #include "../../tendermint_amd/csrc/host/tm_types.h"
 #include "../../tendermint_amd/csrc/sha512_dev.h"
@@ -95,21 +96,75 @@ int commitcheck_poll(int ready_after, int fail, int64_t timeout_ms, double *elap
 
 const char *tmv_last_error(void) { return "fake device error"; }
 
+// Simulated devices: a context of g_devices devices runs every batch through
+// the runtime's shard plan and launch / harvest order (host/shard_plan.h,
+// host/shard_run.h) -- a launch computes its chunk into the lane's buffer
+// (device memory), a harvest copies it to the caller's vector (the D2H) --
+// and logs each step, so a multi-device context's placement is checked on
+// the CPU.
+static uint32_t g_devices = 1, g_chunk = 262144, g_lanes = 2;
+static std::vector<uint32_t> g_steps;  // (kind 0 launch / 1 harvest, device, lane, lo, hi) per step
+
+void commitcheck_set_devices(uint32_t devices, uint32_t host_chunk, uint32_t lanes) {
+  g_devices = devices ? devices : 1;
+  g_chunk = host_chunk;
+  g_lanes = lanes ? lanes : 1;
+  g_steps.clear();
+}
+
+// Copies up to cap steps (5 words each) and clears the log; returns the count.
+uint32_t commitcheck_steps(uint32_t *out, uint32_t cap) {
+  const uint32_t n = (uint32_t)(g_steps.size() / 5);
+  for (uint32_t i = 0; i < std::min(n, cap) * 5; i++) out[i] = g_steps[i];
+  g_steps.clear();
+  return n;
+}
+}
+
+template <class F>
+static void run_devices(uint32_t n, int8_t *status_out, F status_of) {
+  const tmh::ShardPlan plan = tmh::plan_shards(n, g_devices, g_chunk);
+  struct Lane {
+    uint32_t lo = 0, n = 0;
+    std::vector<int8_t> buf;
+  };
+  std::vector<std::vector<Lane>> lanes(plan.shards, std::vector<Lane>(g_lanes));
+  tmh::run_shard_plan(
+      plan, g_lanes,
+      [&](uint32_t s, uint32_t l, bool ok) -> int {
+        Lane &ln = lanes[s][l];
+        if (!ln.n) return 0;
+        if (ok) std::memcpy(status_out + ln.lo, ln.buf.data(), ln.n);
+        g_steps.insert(g_steps.end(), {1u, s, l, ln.lo, ln.lo + ln.n});
+        ln.n = 0;
+        return 0;
+      },
+      [&](uint32_t s, uint32_t l, uint32_t lo, uint32_t hi) -> int {
+        Lane &ln = lanes[s][l];
+        ln.buf.resize(hi - lo);
+        for (uint32_t i = lo; i < hi; i++) ln.buf[i - lo] = status_of(i);
+        ln.lo = lo;
+        ln.n = hi - lo;
+        g_steps.insert(g_steps.end(), {0u, s, l, lo, hi});
+        return 0;
+      });
+}
+
+extern "C" {
+
 int tmv_verify_batch_ex(tmv_ctx *, uint8_t key_kind, uint32_t, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
   if (g_fail_next) { const int rc = g_fail_next; g_fail_next = 0; return rc; }
   commitcheck_backend_calls++;
   commitcheck_entries_verified += (int)n;
-  const Bytes dummy_pk;
-  bool all = n > 0;
-  for (uint32_t i = 0; i < n; i++) {
+  run_devices(n, status_out, [&](uint32_t i) -> int8_t {
     const Bytes key(pk + 32 * i, pk + 32 * i + 32);
-    status_out[i] = g_skip_hash ? 1
-                                : fake_status(key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, key,
-                                              Bytes(msg + msg_off[i], msg + msg_off[i + 1]),
-                                              Bytes(sig + 64 * i, sig + 64 * i + 64));
-    all = all && status_out[i] == 1;
-  }
+    return g_skip_hash ? 1
+                       : fake_status(key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, key,
+                                     Bytes(msg + msg_off[i], msg + msg_off[i + 1]), Bytes(sig + 64 * i, sig + 64 * i + 64));
+  });
+  bool all = n > 0;
+  for (uint32_t i = 0; i < n; i++) all = all && status_out[i] == 1;
   return all ? TMV_ALL_VALID : TMV_NOT_ALL;
 }
 
@@ -142,16 +197,17 @@ int tmv_verify_votes(tmv_ctx *, uint8_t key_kind, uint32_t, const tmv_vote_templ
   if (g_fail_next) { const int rc = g_fail_next; g_fail_next = 0; return rc; }
   commitcheck_backend_calls++;
   commitcheck_entries_verified += (int)n;
-  bool all = n > 0;
-  for (uint32_t i = 0; i < n; i++) {
+  for (uint32_t i = 0; i < n; i++)
+    if ((votes[i].tmpl & ~TMV_VOTE_WITH_BLOCK) >= n_tmpl) return TMV_ERR_ARG;
+  run_devices(n, status_out, [&](uint32_t i) -> int8_t {
     const uint32_t t = votes[i].tmpl & ~TMV_VOTE_WITH_BLOCK;
-    if (t >= n_tmpl) return TMV_ERR_ARG;
     const Bytes key(pk + 32 * i, pk + 32 * i + 32);
-    status_out[i] = g_skip_hash ? 1
-                                : fake_status(key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, key,
-                                              vote_message(tmpl[t], votes[i]), Bytes(sig + 64 * i, sig + 64 * i + 64));
-    all = all && status_out[i] == 1;
-  }
+    return g_skip_hash ? 1
+                       : fake_status(key_kind == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519, key,
+                                     vote_message(tmpl[t], votes[i]), Bytes(sig + 64 * i, sig + 64 * i + 64));
+  });
+  bool all = n > 0;
+  for (uint32_t i = 0; i < n; i++) all = all && status_out[i] == 1;
   return all ? TMV_ALL_VALID : TMV_NOT_ALL;
 }
 

@@ -202,3 +202,69 @@ def test_blocksync_uses_stored_last_commit(fake, monkeypatch):
     got = _replay(fake, vals, blocks[3:], wrong, 100, monkeypatch)
     assert got[0] == 0 and got[1][0] == 4 and "wrong block ID" in got[1][1]
     assert _replay(fake, vals, blocks[3:], blocks[2].block_id, 100, monkeypatch) == (6, None)
+
+
+def _failing_provider(blocks, fail):
+    by_h = {lb.height: lb for lb in blocks}
+    asked = []
+
+    def get(h):
+        asked.append(h)
+        if h in fail:
+            raise RuntimeError("provider: no light block at height %d" % h)
+        return by_h[h]
+    return get, asked
+
+
+def test_skipping_speculative_provider_failure_is_harmless(fake):
+    """A provider that fails on every height only the speculation asks for
+    (the reference's bisection never requests them) leaves the trace
+    unchanged."""
+    trusted, blocks = make_light_chain(30, 20, rotate=1, seed=230)
+    now = _now(blocks)
+    conv = CF.OracleBlocks()
+    by_h = {lb.height: lb for lb in blocks}
+    oracle_asked = []
+
+    def oprov(h):
+        oracle_asked.append(h)
+        return conv(by_h[h])
+    want = L.verify_skipping(conv(trusted), conv(blocks[-1]), oprov, PERIOD, now[0] * L.NS + now[1], DRIFT)
+    assert want[1] is None and len(want[0]) > 2
+    prov, asked = _failing_provider(blocks, set())
+    chains.verify_skipping(None, trusted, blocks[-1], prov, PERIOD, now, DRIFT, verify_many=fake.light_verify_many)
+    extra = sorted(set(asked) - set(oracle_asked))
+    assert extra, "the speculation asked for no pivot beyond the reference's"
+    prov, _ = _failing_provider(blocks, set(extra))
+    trace, err = chains.verify_skipping(None, trusted, blocks[-1], prov, PERIOD, now, DRIFT,
+                                        verify_many=fake.light_verify_many)
+    assert err is None and trace == want[0]
+
+
+def test_skipping_required_provider_failure_matches_oracle(fake):
+    """A provider error on a pivot the reference does request is returned as
+    ErrVerificationFailed{verified, pivot, err} (light/client.go:706-709)."""
+    trusted, blocks = make_light_chain(30, 20, rotate=1, seed=230)
+    now = _now(blocks)
+    conv = CF.OracleBlocks()
+    by_h = {lb.height: lb for lb in blocks}
+    oracle_asked = []
+
+    def oprov(h):
+        oracle_asked.append(h)
+        return conv(by_h[h])
+    L.verify_skipping(conv(trusted), conv(blocks[-1]), oprov, PERIOD, now[0] * L.NS + now[1], DRIFT)
+    bad = oracle_asked[len(oracle_asked) // 2]
+
+    def oprov_bad(h):
+        if h == bad:
+            raise RuntimeError("provider: no light block at height %d" % h)
+        return conv(by_h[h])
+    want = L.verify_skipping(conv(trusted), conv(blocks[-1]), oprov_bad, PERIOD, now[0] * L.NS + now[1], DRIFT)
+    assert want[0] is None and want[1][1] == bad
+    prov, _ = _failing_provider(blocks, {bad})
+    trace, err = chains.verify_skipping(None, trusted, blocks[-1], prov, PERIOD, now, DRIFT,
+                                        verify_many=fake.light_verify_many)
+    assert trace is None
+    assert (err.from_height, err.to_height, err.kind, err.reason) == \
+        (want[1][0], want[1][1], want[1][2].kind, want[1][2].text)

@@ -341,3 +341,71 @@ def test_multi_batch_launch_over_64(bctx):
             assert np.array_equal(out.cpu().numpy().astype(np.uint8), ref), flags
     with pytest.raises(N.NativeError):
         bctx.verify_batches_device(0, ED, BEQ, [N.BatchRef(0, 0, 0, 0, 0, 0, 0)] * 257)
+
+
+def _located_case(n=150_000 + 91, m=256):
+    """n honest commit signatures (tiled) with bad entries placed so that
+    some groups of m hold one bad entry and some two (R byte flips: R still
+    decodes, the equation fails)."""
+    b = make_commit_batch(1500, seed=23).tile(n)
+    sig = b.sig.copy()
+    singles = [0, m + m - 1, 5 * m + 17, 9 * m + 200, 40 * m + 3, n - 2]
+    pairs = [(12 * m + 1, 12 * m + 9), (30 * m + 100, 30 * m + 101)]
+    for i in singles + [x for p in pairs for x in p]:
+        sig[64 * i + 5] ^= 0x10
+    return b, sig, singles, pairs
+
+
+@pytest.mark.parametrize("m_log2,c", [(8, 8), (8, 6), (10, 9), (7, 6)])
+def test_located_pass_width_and_metrics(bctx, m_log2, c):
+    """the located pass's weights z (j + 1) < 2^(128 + m_log2) need
+    ceil((129 + m_log2) / c) windows.  With groups of 256 / 1024 (sub-group
+    checks off) the located pass must still name every single bad entry:
+    tmv_metrics counts one located group and one per-entry verification per
+    single-bad group, and whole groups only for the two-bad ones; the vector
+    equals the oracle's."""
+    m = 1 << m_log2
+    b, sig, singles, pairs = _located_case(m=m)
+    n = b.n
+    bctx.set_batch_options(group_log2=m_log2, window_bits=c, seed=SEED, stats=True, subcheck=False)
+    bctx.metrics_reset()
+    try:
+        ok, st = bctx.verify_batch_ex(ED, BEQ, b.pk, sig, b.msg, b.off)
+        met = bctx.metrics()
+    finally:
+        bctx.set_batch_options(seed=SEED, stats=True)
+    ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
+    assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
+    bad_groups = {i // m for i in singles} | {p[0] // m for p in pairs}
+    assert met["groups_failed"] == len(bad_groups)
+    assert met["located_groups"] == len(singles)
+    whole = sum(min(m, n - (p[0] // m) * m) for p in pairs)
+    assert met["fallback_signatures"] == len(singles) + whole
+    assert met["calls"] == 1 and met["signatures"] == n and met["batch_eq_signatures"] == n
+    assert met["h2d_bytes"] >= b.pk.nbytes + sig.nbytes + b.msg.nbytes and met["d2h_bytes"] == n
+    assert met["host_signatures"] == n and met["verifies_per_s_host"] > 0
+
+
+def test_metrics_counts_calls_and_resets(bctx):
+    """tmv_metrics: calls, entries, the largest call and the batch-equation
+    share over host-buffer and device-resident calls; reset zeroes them."""
+    import torch
+    bctx.metrics_reset()
+    b = make_c2_batch(3000, seed=77)
+    bctx.verify_batch_ex(ED, N.TMV_FLAG_PER_ENTRY, b.pk, b.sig, b.msg, b.off)
+    bctx.verify_batch_ex(ED, BEQ, b.pk, b.sig, b.msg, b.off)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(getattr(b, k)).to(dev) for k in ("pk", "sig", "msg")}
+    off = torch.from_numpy(b.off.view(np.int32)).to(dev)
+    out = torch.zeros(b.n, dtype=torch.int8, device=dev)
+    bctx.verify_batch_device_ex(0, ED, BEQ, 0, t["pk"].data_ptr(), t["sig"].data_ptr(), t["msg"].data_ptr(),
+                                off.data_ptr(), 1000, out.data_ptr())
+    torch.cuda.synchronize()
+    met = bctx.metrics()
+    assert (met["calls"], met["signatures"], met["max_batch"]) == (3, 7000, 3000)
+    assert met["batch_eq_signatures"] == 4000 and met["host_signatures"] == 6000
+    assert met["groups"] >= (3000 + 63) // 64 and met["groups_failed"] >= 1
+    assert met["fallback_signatures"] >= met["groups_failed"]
+    bctx.metrics_reset()
+    met = bctx.metrics()
+    assert all(v == 0 for k, v in met.items() if k not in ("key_cache_hits", "key_cache_misses"))

@@ -141,3 +141,26 @@ def test_cpu_batch_verifier_matches_per_entry():
     for batch in (1, 50, 1200):
         ok, v, failed = C.ed25519_batch_verify_voi(c.pk, c.sig, c.msg, c.off, threads=3, batch=batch)
         assert np.array_equal(v, ref) and not ok and failed >= 1
+
+
+def test_commit_cpu_baseline_matches_oracle():
+    """bench.py's C1 CPU baseline (oracle_verify_commit_cpu): the sign-bytes
+    it builds are the votes' (the honest C1 commit verifies) and a corrupted
+    vote is found at its index, as the per-entry oracle finds it."""
+    import numpy as np
+
+    import oracle_c
+    from tendermint_amd.testing.bulk import commit_vote_head
+    from tendermint_amd.testing.factory import make_c1_commit
+    from tendermint_amd.types.canonical import BlockID, PartSetHeader
+    vals, bid, commit = make_c1_commit(40)
+    head = commit_vote_head(3, 0, BlockID(bid.hash, PartSetHeader(bid.psh_total, bid.psh_hash)))
+    pk = np.frombuffer(b"".join(v.pub_key for v in vals.validators), np.uint8)
+    sig = np.frombuffer(b"".join(s.signature for s in commit.signatures), np.uint8).copy()
+    secs = [s.timestamp[0] for s in commit.signatures]
+    nanos = [s.timestamp[1] for s in commit.signatures]
+    assert oracle_c.CommitCPU(head, "test_chain_id", secs, nanos, pk, sig)()
+    sig[64 * 17 + 40] ^= 4
+    c = oracle_c.CommitCPU(head, "test_chain_id", secs, nanos, pk, sig)
+    assert not c() and list(np.flatnonzero(c.out[:40] == 0)) == [17]
+    assert not oracle_c.CommitCPU(head, "other_chain", secs, nanos, pk, sig)()
