@@ -47,7 +47,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from tendermint_amd import _native as N  # noqa: E402
-from tendermint_amd.shard import all_gather_validity  # noqa: E402
+from tendermint_amd.shard import all_gather_statuses, all_gather_validity  # noqa: E402
 from tendermint_amd import host as H  # noqa: E402
 from tendermint_amd.testing.factory import Batch, make_c1_commit, make_c2_batch  # noqa: E402
 
@@ -167,26 +167,6 @@ def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: i
         if best is None or cost < best:
             best, c = cost, cc
     return m, c
-
-
-def _rocprof_avg_ms(steps: int):
-    """rocprofv3 --kernel-trace average of the primary k_msm_accum dispatches
-    in the timed region of a traced run of this bench command (committed:
-    profiles/r02_final/accum_trace_avg.json, tools/trace_kernel_avg.py), next
-    to the live value that run printed."""
-    path = os.path.join(REPO, "profiles", "r02_final", "accum_trace_avg.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except Exception:
-        return None
-    key = "bench --steps 20 --warmup 5" if steps <= 20 else "bench --steps 48 --warmup 8 --no-extras"
-    if key not in d:
-        return None
-    e = d[key]
-    return {"command": key, "avg_ms": e["rocprof_kernel_trace"]["primary_avg_ms"],
-            "dispatches": e["rocprof_kernel_trace"]["primary_dispatches"],
-            "live_avg_ms_same_run": e["live_avg_launch_ms"], "source": "profiles/r02_final/accum_trace_avg.json"}
 
 
 def host_cpu_info():
@@ -381,6 +361,97 @@ class _HostEvent:
         return (other.t - self.t) * 1e3
 
 
+def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method):
+    """The whole pipeline against SURVEY 8(d)'s canonical unit: verifies/s x
+    2.7e5 int32 products per single-verify-equivalent signature / the
+    multiply peak.  The batch equation executes fewer products than that
+    unit, so the ratio can exceed 1: it is reported as canonical_ratio, never
+    as the roofline fraction."""
+    out = {"canonical_ratio": round(gpu_rate * MULS_PER_SIG / peak, 4),
+           "canonical_note": "verifies/s of this GPU x 2.7e5 canonical products per signature (SURVEY 8(d)) / peak: "
+                             "the batch equation does less work than a single verify, so this ratio exceeds 1 and is "
+                             "not a roofline fraction",
+           "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if method == "batch"
+                      else "k_prep + k_verify_quad"),
+           "launch_avg_ms": round(launch_ms, 4),
+           "traffic_per_step": pmc.get("hbm_bytes_per_step"),
+           "traffic_note": pmc.get("note"),
+           "executed": pmc.get("executed"),
+           "pmc_kernels": _pmc_kernels(method),
+           "peak": round(peak / 1e12, 4), "unit": "Tmul/s"}
+    ex = pmc.get("executed") or {}
+    if ex.get("int64_lane_ops_per_sig"):
+        out["executed_frac"] = round(gpu_rate * ex["int64_lane_ops_per_sig"] / peak, 4)
+    return out
+
+
+DOMINANT_FILE = os.path.join("profiles", "r03", "dominant_kernel.json")
+
+
+def _dominant_file():
+    try:
+        with open(os.path.join(REPO, DOMINANT_FILE)) as f:
+            return json.load(f)
+    except Exception:
+        return {}
+
+
+def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, ms_per_step):
+    """roofline for the dominant kernel, k_msm_accum<16> (bucket sums; the
+    largest share of the pipeline's VALU work): its algorithmic products per
+    launch (SURVEY 8(d)'s per-unit work: one mixed addition = 7 field
+    multiplications x 100 int32 products per bucket entry, x the expected
+    entries per signature x the launch's signatures) over its own launch
+    duration -- the five launches run alone after the timed region, bracketed
+    by HIP events on their stream (tmv_kernel_timing), so no other launch
+    shares the chip -- against the measured v_mad_i64_i32 peak.  The
+    committed rocprofv3 --kernel-trace --stats of bench.py --inflight 1 (one
+    launch at a time) gives the same kernel's average dispatch
+    (profiles/r03/dominant_kernel.json); traffic = its HBM bytes per launch
+    from PMC passes at this launch size (256 x 10k)."""
+    m_grp, c_win = msm_shape(K * n, args.group_log2, args.window)
+    per_launch = K * n * accum_entries_per_sig(m=m_grp, c=c_win) * ACCUM_PRODUCTS_PER_ENTRY
+    alone = ktimes_alone.get("k_msm_accum", (0, 0))
+    ov_ms, ov_cnt = ktimes["k_msm_accum"]
+    own_ms = alone[0] / alone[1] if alone[1] else None
+    dfile = _dominant_file()
+    rp = dfile.get("rocprof_alone")
+    if own_ms is None and rp:  # --no-extras: the committed rocprof figure
+        own_ms = rp["avg_ms"]
+    achieved = per_launch / (own_ms * 1e-3) if own_ms else None
+    r = {"bound": "valu-int-mul",
+         "kernel": "k_msm_accum<16>",
+         "achieved": round(achieved / 1e12, 4) if achieved else None,
+         "peak": round(peak / 1e12, 4), "unit": "Tmul/s",
+         "frac": round(achieved / peak, 4) if achieved else None,
+         "traffic": dfile.get("traffic_bytes_per_launch"),
+         "traffic_note": dfile.get("traffic_note"),
+         "avg_launch_ms": round(own_ms, 4) if own_ms else None,
+         "ms_per_step": round(ms_per_step, 4),
+         "timing": "HIP events on the stream of each k_msm_accum launch, five launches of the bench's size run alone "
+                   "after the timed region (tmv_kernel_timing); one per step, so its own time per step is "
+                   "avg_launch_ms <= ms_per_step",
+         "algorithmic_products_per_launch": round(per_launch),
+         "msm_shape": {"group": m_grp, "window_bits": c_win},
+         "algorithmic_note": f"{K} x {n} signatures x expected bucket entries per signature (nonzero signed "
+                             f"{c_win}-bit digits of z and z k mod l, + the group's B scalar over {m_grp}; simulated "
+                             "recoding) x 7 field multiplications x 100 int32 products (SURVEY 8(d) unit)",
+         "peak_from": "measured v_mad_i64_i32 rate, 16 waves/SIMD (tools/occbench.hip, profiles/occbench_r01.json)",
+         "rocprof": rp,
+         "under_overlap": {"avg_launch_ms": round(ov_ms / ov_cnt, 4), "launches": ov_cnt,
+                           "note": f"the timed region's launches ({args.inflight} in flight share the chip, so a "
+                                   "launch's span is stretched; not the kernel's own time)"},
+         "other_kernels_alone_ms": {k: round(v[0] / v[1], 4) for k, v in ktimes_alone.items()
+                                    if v[1] and k != "k_msm_accum"},
+         "pipeline": pipeline}
+    ex = dfile.get("executed_int64_lane_ops_per_launch")
+    if ex and own_ms:
+        r["executed_frac"] = round(ex / (own_ms * 1e-3) / peak, 4)
+        r["executed_note"] = ("PMC SQ_INSTS_VALU_INT64 lane-ops per launch (products and the 64-bit carry adds / "
+                              "shifts) / own duration / peak v_mad_i64_i32 rate")
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -443,6 +514,11 @@ def main():
         sync = torch.cuda.synchronize
         Stream, Event, stream_ctx = torch.cuda.Stream, torch.cuda.Event, torch.cuda.stream
     flags = N.TMV_FLAG_BATCH_EQUATION if args.method == "batch" else N.TMV_FLAG_PER_ENTRY
+    key_kind = N.TMV_KIND_ED25519
+    # the exchange: packed bitmaps where statuses are 0 / 1 (ed25519); kinds
+    # whose statuses carry deferred Add errors (sr25519: -1 / -2) gather the
+    # int8 statuses themselves (shard.all_gather_statuses)
+    gather_fn = all_gather_validity if key_kind == N.TMV_KIND_ED25519 else all_gather_statuses
     batch = batches[0]
     n = batch.n
     expect_valid = [sum(k in VALID_KINDS for k in b.kinds) for b in batches]
@@ -462,9 +538,12 @@ def main():
         return out
     streams = [Stream(dev) for _ in range(F)]
     comm = Stream(dev) if world > 1 else None
+    # every resident batch's known vector (factory kinds: 9,950 valid of 10k);
+    # the timed launches' vectors are compared with it entry by entry
+    want_status = [torch.tensor([1 if k in VALID_KINDS else 0 for k in b.kinds], dtype=torch.int8, device=dev)
+                   for b in batches]
     if stub:  # the statuses the engine would write, per resident batch
-        stub_status = [torch.tensor([1 if k in VALID_KINDS else 0 for k in b.kinds], dtype=torch.int8)
-                       for b in batches]
+        stub_status = want_status
     gathered = {}
 
     def launch(i, first, kk, ev_pair=None, gather=True):
@@ -476,7 +555,7 @@ def main():
             for j in range(kk):
                 d_valid[f][j * n:(j + 1) * n] = stub_status[(first + j) % R]
         else:
-            ctx.verify_batches_device(gpu, N.TMV_KIND_ED25519, flags, refs(f, first, kk), st.cuda_stream)
+            ctx.verify_batches_device(gpu, key_kind, flags, refs(f, first, kk), st.cuda_stream)
         if ev_pair is not None:
             ev_pair[1].record(st)
         if world > 1 and gather:
@@ -484,7 +563,7 @@ def main():
             # issue order on one stream, after this launch
             comm.wait_stream(st)
             with stream_ctx(comm):
-                gathered[f] = all_gather_validity(d_valid[f][:kk * n], [kk * n] * world)
+                gathered[f] = gather_fn(d_valid[f][:kk * n], [kk * n] * world)
             st.wait_stream(comm)
 
     def run(sizes_, evs=None):
@@ -518,15 +597,18 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = statistics.mean(a.elapsed_time(b) for a, b in evs)
-    # the last launch on each stream left its vectors: every C2 batch has its
-    # factory-known number of valid signatures (9,950 of 10k: 100 edge cases,
-    # 50 of them valid)
+    # the last launch on each stream left its vectors: every C2 batch's vector
+    # equals its factory-known per-entry kinds (9,950 of 10k valid: 100 edge
+    # cases, 50 of them valid under ZIP-215)
     valid, first = [], 0
     for i, kk in enumerate(sizes):
         f = i % F
         if i >= len(sizes) - F:
             for j in range(kk):
-                v = int((d_valid[f][j * n:(j + 1) * n] == 1).sum().item())
+                got = d_valid[f][j * n:(j + 1) * n]
+                assert torch.equal(got, want_status[(first + j) % R]), \
+                    f"launch {i} batch {j}: vector differs from the factory's known per-entry kinds"
+                v = int((got == 1).sum().item())
                 assert v == expect_valid[(first + j) % R], (v, expect_valid[(first + j) % R])
                 valid.append(v)
             if world > 1:  # the gathered vector holds every rank's copy of this launch
@@ -619,7 +701,6 @@ def main():
         value = total / elapsed
         gpu_rate = n * n_batches / elapsed  # this rank
         peak = _load_peak()
-        achieved = gpu_rate * MULS_PER_SIG
         pmc = _load_pmc(args.method, K)
         result = {
             "metric": METRIC,
@@ -643,78 +724,11 @@ def main():
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "valid_per_batch": valid[0],
             **extras,
-            "roofline": {"bound": "valu-int-mul", "achieved": round(achieved / 1e12, 4),
-                         "peak": round(peak / 1e12, 4), "unit": "Tmul/s", "frac": round(achieved / peak, 4),
-                         "achieved_from": "verifies/s of this GPU over the timed region x 2.7e5 canonical int32 "
-                                          "products per verified signature (SURVEY 8(d): single-verify equivalent); "
-                                          "independent of how launches overlap",
-                         "work_per_sig": "2.7e5 int32 products (SURVEY 8(d))",
-                         "peak_from": "measured v_mad_i64_i32 rate, 16 waves/SIMD (tools/occbench.hip, "
-                                      "profiles/occbench_r01.json)",
-                         "kernel": ("batch-equation pipeline k_prep..k_verify_quad" if args.method == "batch"
-                                    else "k_prep + k_verify_quad"),
-                         "launch_avg_ms": round(launch_ms, 4),
-                         "traffic": pmc.get("hbm_bytes_per_step"),
-                         "traffic_note": pmc.get("note"),
-                         "executed": pmc.get("executed"),
-                         "pmc_kernels": _pmc_kernels(args.method)},
+            "roofline": _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, args.method),
         }
-        ex = pmc.get("executed") or {}
-        if ex.get("int64_lane_ops_per_sig"):
-            result["roofline"]["executed_frac"] = round(gpu_rate * ex["int64_lane_ops_per_sig"] / peak, 4)
-            result["roofline"]["executed_frac_note"] = (
-                "verifies/s x PMC SQ_INSTS_VALU_INT64 lane-ops per signature / peak v_mad_i64_i32 rate: the 64-bit "
-                "VALU ops executed (multiply products plus 64-bit carry adds/shifts) as a share of the multiply peak; "
-                "an upper bound on the multiply share, independent of the canonical work figure")
         if ktimes.get("k_msm_accum", (0, 0))[1] and args.method == "batch":
-            ms, cnt = ktimes["k_msm_accum"]
-            avg = ms / cnt
-            m_grp, c_win = msm_shape(K * n, args.group_log2, args.window)
-            per_launch = K * n * accum_entries_per_sig(m=m_grp, c=c_win) * ACCUM_PRODUCTS_PER_ENTRY
-            acc = per_launch / (avg * 1e-3)
-            kp = pmc.get("kernels", {}).get("tmv::k_msm_accum<16>", {})
-            alone = ktimes_alone.get("k_msm_accum", (0, 0))
-            dk = {"kernel": "k_msm_accum<16> (bucket sums; the largest share of the pipeline's VALU work)",
-                  "avg_launch_ms": round(avg, 4), "launches": cnt,
-                  "timing": "HIP events on the launch's stream around every k_msm_accum launch of the timed region "
-                            "(tmv_kernel_timing); launches in flight share the chip, so this is the kernel's "
-                            "duration under the bench's overlap",
-                  "avg_launch_ms_alone": round(alone[0] / alone[1], 4) if alone[1] else None,
-                  "algorithmic_products_per_launch": round(per_launch),
-                  "msm_shape": {"group": m_grp, "window_bits": c_win},
-                  "algorithmic_note": f"{K} x {n} signatures x expected bucket entries per signature (nonzero signed "
-                                      f"{c_win}-bit digits of z and z k mod l, + the group's B scalar over {m_grp}; "
-                                      "simulated recoding) x 7 field multiplications x 100 int32 products",
-                  "achieved": round(acc / 1e12, 4), "peak": round(peak / 1e12, 4), "unit": "Tmul/s",
-                  "frac": round(acc / peak, 4),
-                  "frac_alone": round(per_launch / (alone[0] / alone[1] * 1e-3) / peak, 4) if alone[1] else None,
-                  "other_kernels_avg_ms": {k: round(v[0] / v[1], 4) for k, v in ktimes.items()
-                                           if v[1] and k != "k_msm_accum"},
-                  "rocprof": _rocprof_avg_ms(steps)}
-            if kp.get("SQ_INSTS_VALU_INT64"):
-                scale = K / pmc.get("batches_per_launch", 32)
-                dk["executed_int64_lane_ops_per_launch"] = int(kp["SQ_INSTS_VALU_INT64"] * 64 * scale)
-                dk["executed_frac"] = round(dk["executed_int64_lane_ops_per_launch"] / (avg * 1e-3) / peak, 4)
-                if alone[1]:
-                    dk["executed_frac_alone"] = round(
-                        dk["executed_int64_lane_ops_per_launch"] / (alone[0] / alone[1] * 1e-3) / peak, 4)
-                try:  # share of the 64-bit VALU ops that are v_mad_i64_i32 (static ISA mix, tools/isa_mix.py)
-                    with open(os.path.join(REPO, "profiles", "r02_close", "isa_mix_accum.json")) as f:
-                        share = json.load(f)["mad_share_of_int64"]
-                    dk["mad_share_of_int64_ops"] = share
-                    if alone[1]:
-                        dk["mad_frac_alone"] = round(dk["executed_frac_alone"] * share, 4)
-                    dk["executed_note"] = (
-                        "executed_* = PMC SQ_INSTS_VALU_INT64 lane-ops per launch / duration / peak v_mad_i64_i32 "
-                        "rate; the 64-bit adds and shifts of the carry chains issue faster than the mads, so it can "
-                        "exceed 1; mad_frac_alone counts only the v_mad_i64_i32 share (static ISA mix, "
-                        "profiles/r02_close/isa_mix_accum.json)")
-                except Exception:
-                    pass
-                dk["traffic_bytes_per_launch"] = int((kp.get("hbm_read_bytes", 0) + kp.get("hbm_write_bytes", 0)) *
-                                                     scale)
-                dk["traffic_GBps"] = round(dk["traffic_bytes_per_launch"] / (avg * 1e-3) / 1e9, 1)
-            result["roofline"]["dominant_kernel"] = dk
+            result["roofline"] = _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps,
+                                                    result["roofline"], elapsed / steps * 1e3)
         if stub:
             result["data"] = "CPU STUB (--cpu-stub): control-flow check only, no verification, not a measurement"
         if world == 1 and not args.no_cpu_baseline and not stub:

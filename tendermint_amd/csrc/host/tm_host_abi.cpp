@@ -146,7 +146,7 @@ tmv_batch *tmv_batch_new(tmv_ctx *ctx, uint8_t key_kind) {
 int tmv_batch_add(tmv_batch *b, uint8_t key_kind, const uint8_t *pk, size_t pk_len, const uint8_t *msg,
                   size_t msg_len, const uint8_t *sig, size_t sig_len, char *err, size_t err_cap) {
   if (!b) return TMV_ERR_ARG;
-  tmh::PubKey key{to_kind(key_kind), bytes_of(pk, pk_len)};
+  tmh::PubKey key{to_kind(key_kind), tmh::ByteView(pk, pk_len)};
   tmh::Error e = b->impl->Add(key, bytes_of(msg, msg_len), bytes_of(sig, sig_len));
   if (e) {
     put_err(err, err_cap, *e);
@@ -297,7 +297,7 @@ struct GpuBackend {
       for (size_t i = c * kChunk; i < std::min(es.size(), c * kChunk + kChunk); i++) {
         const tmh::SigEntry &e = es[i].entry();
         uint8_t k = e.kind == tmh::KeyType::Ed25519 ? 0 : (e.kind == tmh::KeyType::Sr25519 ? 1 : 2);
-        if (e.pk->size() != 32 || e.sig_len != 64) k = 2;
+        if (e.pk.size() != 32 || e.sig_len != 64) k = 2;
         pb.cls[i] = k;
         k0 += k == 0;
         k1 += k == 1;
@@ -334,7 +334,7 @@ struct GpuBackend {
           const VoteRef &r = es[kidx[t]];
           const tmh::SigEntry &e = r.entry();
           const tmh::CommitSig &cs = r.pl->commit->signatures[(size_t)r.pl->sig_idx[r.e]];
-          std::memcpy(&pb.pk[32 * t], e.pk->data(), 32);
+          std::memcpy(&pb.pk[32 * t], e.pk.data(), 32);
           std::memcpy(&pb.sig[64 * t], e.sig, 64);
           pb.votes[t] = tmv_vote{cs.timestamp.seconds, cs.timestamp.nanos,
                                  ent_tmpl[kidx[t]] |
@@ -382,8 +382,8 @@ std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n
   vs->validators.resize(n_vals);
   for (uint32_t i = 0; i < n_vals; i++) {
     tmh::Validator &v = vs->validators[i];
-    v.address = bytes_of(vals[i].address, vals[i].address_len);
-    v.pub_key = tmh::PubKey{to_kind(vals[i].key_kind), bytes_of(vals[i].pub_key, vals[i].pub_key_len)};
+    v.address = tmh::ByteView(vals[i].address, vals[i].address_len);
+    v.pub_key = tmh::PubKey{to_kind(vals[i].key_kind), tmh::ByteView(vals[i].pub_key, vals[i].pub_key_len)};
     v.voting_power = vals[i].voting_power;
     v.proposer_priority = vals[i].proposer_priority;
   }
@@ -411,7 +411,7 @@ std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit) {
 }
 
 int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
-                   size_t err_stride, uint8_t *not_enough) {
+                   size_t err_stride, uint8_t *not_enough, const Converted *conv) {
   if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
   for (uint32_t j = 0; j < n_jobs; j++)
     if (jobs[j].mode < 0 || jobs[j].mode > 2) return TMV_ERR_ARG;
@@ -434,13 +434,33 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
       jc[j] = it->second;
     }
   }
-  std::vector<std::unique_ptr<tmh::ValidatorSet>> vsets(vsrc.size());
-  std::vector<std::unique_ptr<tmh::Commit>> commits(csrc.size());
+  // owned conversions (own_*) and the objects the checks read (vsets /
+  // commits: the owned ones or the caller's already converted ones)
+  std::vector<std::unique_ptr<tmh::ValidatorSet>> own_v(vsrc.size());
+  std::vector<std::unique_ptr<tmh::Commit>> own_c(csrc.size());
+  std::vector<const tmh::ValidatorSet *> vsets(vsrc.size(), nullptr);
+  std::vector<const tmh::Commit *> commits(csrc.size(), nullptr);
   parallel_for(vsrc.size() + csrc.size(), 4, [&](size_t i) {
-    if (i < vsrc.size())
-      vsets[i] = vals_of(vsrc[i]->vals, vsrc[i]->n_vals, vsrc[i]->proposer_index);
-    else
-      commits[i - vsrc.size()] = commit_of(csrc[i - vsrc.size()]->commit);
+    if (i < vsrc.size()) {
+      if (conv) {
+        auto it = conv->vals.find(vsrc[i]->vals);
+        if (it != conv->vals.end() && it->second->Size() == vsrc[i]->n_vals &&
+            it->second->proposer == vsrc[i]->proposer_index) {
+          vsets[i] = it->second;
+          return;
+        }
+      }
+      own_v[i] = vals_of(vsrc[i]->vals, vsrc[i]->n_vals, vsrc[i]->proposer_index);
+      vsets[i] = own_v[i].get();
+    } else {
+      const size_t c = i - vsrc.size();
+      if (conv) {
+        auto it = conv->commits.find(csrc[c]->commit);
+        if (it != conv->commits.end()) { commits[c] = it->second; return; }
+      }
+      own_c[c] = commit_of(csrc[c]->commit);
+      commits[c] = own_c[c].get();
+    }
   });
   tm.mark("convert");
   std::vector<tmh::CommitPlan> plans(n_jobs);
@@ -448,8 +468,8 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
     const tmv_commit_job &jb = jobs[j];
     const tmh::BlockID bid = jb.block_id ? block_id_of(*jb.block_id) : tmh::BlockID{};
     plans[j] = tmh::CommitVerifier::Plan((tmh::CommitVerifier::Mode)jb.mode, jb.chain_id ? jb.chain_id : "",
-                                         jv[j] == SIZE_MAX ? nullptr : vsets[jv[j]].get(), bid, jb.height,
-                                         jc[j] == SIZE_MAX ? nullptr : commits[jc[j]].get(), jb.trust_num,
+                                         jv[j] == SIZE_MAX ? nullptr : vsets[jv[j]], bid, jb.height,
+                                         jc[j] == SIZE_MAX ? nullptr : commits[jc[j]], jb.trust_num,
                                          jb.trust_den);
   });
   tm.mark("plan");
@@ -497,7 +517,7 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
         uint32_t &u = sl[(size_t)pl.sig_idx[e]];
         if (u != UINT32_MAX) {
           const tmh::CommitPlan &fpl = plans[first[u].first];  // first occurrence of u
-          if (fpl.entries[first[u].second].pk == en.pk && (&fpl == &pl || fpl.chain_id == pl.chain_id)) {
+          if (fpl.entries[first[u].second].pk.data() == en.pk.data() && (&fpl == &pl || fpl.chain_id == pl.chain_id)) {
             where[joff[j] + e] = u;
             continue;
           }
@@ -558,9 +578,9 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
   tm.mark("finish");
   // the converted sets, commits and plans are ~10^5 small heap objects per
   // window; freed on one thread they took ~7 ms of a C3 window
-  parallel_for(std::max(vsets.size(), std::max(commits.size(), (size_t)n_jobs)), 16, [&](size_t i) {
-    if (i < vsets.size()) vsets[i].reset();
-    if (i < commits.size()) commits[i].reset();
+  parallel_for(std::max(own_v.size(), std::max(own_c.size(), (size_t)n_jobs)), 16, [&](size_t i) {
+    if (i < own_v.size()) own_v[i].reset();
+    if (i < own_c.size()) own_c[i].reset();
     if (i < n_jobs) plans[i] = tmh::CommitPlan();
   });
   return bad;

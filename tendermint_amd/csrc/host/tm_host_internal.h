@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <memory>
 #include <string>
+#include <unordered_map>
 
 #include "../../../include/tmhost.h"
 #include "pool.h"
@@ -45,10 +46,18 @@ tmh::BlockID block_id_of(const tmv_block_id &b);
 std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index);
 std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit);
 
+// Validator sets and commits a caller has already converted (the light
+// layer), looked up by the C struct they came from, so verify_commits does
+// not convert them again.
+struct Converted {
+  std::unordered_map<const void *, const tmh::ValidatorSet *> vals;  // key: tmv_commit_job::vals
+  std::unordered_map<const void *, const tmh::Commit *> commits;     // key: tmv_commit_job::commit
+};
+
 // tmv_verify_commits, plus not_enough[j] = 1 when job j's error is
 // types.ErrNotEnoughVotingPowerSigned (may be NULL).
 int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
-                   size_t err_stride, uint8_t *not_enough);
+                   size_t err_stride, uint8_t *not_enough, const Converted *conv = nullptr);
 
 // Run fn(i) for i in [0, n) on the host worker pool (serial when small).
 template <class F>

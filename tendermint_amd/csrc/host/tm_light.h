@@ -140,7 +140,9 @@ struct Header {
   int64_t height = 0;
   Timestamp time;
   BlockID last_block_id;
-  Bytes last_commit_hash, data_hash, validators_hash, next_validators_hash, consensus_hash, app_hash,
+  // views into the caller's tmv_header (no copies: a light window converts
+  // ~10^3 headers per call)
+  ByteView last_commit_hash, data_hash, validators_hash, next_validators_hash, consensus_hash, app_hash,
       last_results_hash, evidence_hash, proposer_address;
 };
 
@@ -166,7 +168,7 @@ inline void AppendHeaderLeaves(const Header &h, Bytes &blob, std::vector<uint32_
     put(tmp, (size_t)(PutUvarintP(tmp + 1, n) - tmp));
     put(p, n);
   };
-  auto cdc_bytes = [&](const Bytes &b) {  // gogotypes.BytesValue, nil when empty
+  auto cdc_bytes = [&](ByteView b) {  // gogotypes.BytesValue, nil when empty
     if (!b.empty()) bytes_field(0x0a, b.data(), b.size());
     end();
   };
@@ -315,7 +317,7 @@ inline Bytes ValidatorSetHashHost(const ValidatorSet &vs) {
 }
 
 // ---------------------------------------------------------------- ValidateBasic
-inline Error ValidateHash(const Bytes &h) {
+inline Error ValidateHash(ByteView h) {
   if (!h.empty() && h.size() != kHashSize)
     return "expected size to be " + std::to_string(kHashSize) + " bytes, got " + std::to_string(h.size()) + " bytes";
   return std::nullopt;

@@ -22,7 +22,7 @@ using namespace tmh_internal;
 
 namespace {
 
-tmh::Bytes bytes_of(const tmv_bytes &b) { return tmh_internal::bytes_of(b.p, b.len); }
+tmh::ByteView bytes_of(const tmv_bytes &b) { return tmh::ByteView(b.p, b.len); }
 
 std::unique_ptr<tmh::Header> header_of(const tmv_header &h) {
   auto o = std::make_unique<tmh::Header>();
@@ -258,7 +258,15 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
   std::vector<uint8_t> cne(cj.size());
   std::vector<char> cerr(cj.size() * kStride);
   if (!cj.empty()) {
-    rc = verify_commits(ctx, cj.data(), (uint32_t)cj.size(), cres.data(), cerr.data(), kStride, cne.data());
+    // the sets and commits converted above are the ones the checks read
+    Converted conv;
+    conv.vals.reserve(vsets.size());
+    for (size_t i = 0; i < vsets.size(); i++)
+      if (vsets[i]) conv.vals.emplace(V.src[i]->vals, vsets[i].get());
+    conv.commits.reserve(commits.size());
+    for (size_t i = 0; i < commits.size(); i++)
+      if (commits[i]) conv.commits.emplace(C.src[i], commits[i].get());
+    rc = verify_commits(ctx, cj.data(), (uint32_t)cj.size(), cres.data(), cerr.data(), kStride, cne.data(), &conv);
     if (rc < 0) {
       if (errs && err_stride) put_err(errs, err_stride, std::string(cerr.data()));
       return rc;

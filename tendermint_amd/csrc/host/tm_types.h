@@ -47,7 +47,14 @@ struct ByteView {
   const uint8_t *data() const { return p; }
   size_t size() const { return n; }
   bool empty() const { return n == 0; }
+  const uint8_t *begin() const { return p; }
+  const uint8_t *end() const { return p + n; }
   bool operator==(const ByteView &o) const { return n == o.n && (n == 0 || std::memcmp(p, o.p, n) == 0); }
+  bool operator!=(const ByteView &o) const { return !(*this == o); }
+  bool operator<(const ByteView &o) const {  // lexicographic, as bytes.Compare / a Bytes comparison
+    const int c = std::memcmp(p, o.p, std::min(n, o.n));
+    return c < 0 || (c == 0 && n < o.n);
+  }
 };
 
 // ---------------------------------------------------------------- Go-style formatting
@@ -110,9 +117,11 @@ inline std::string CanonicalTime(const Timestamp &t) {
 // ---------------------------------------------------------------- keys
 enum class KeyType : uint8_t { Ed25519 = 0, Sr25519 = 1, Other = 255 };
 
+// A public key: its type and a view of its bytes (the caller's tmv_validator
+// / tmv_batch_add arguments, which outlive the call that reads them).
 struct PubKey {
   KeyType type = KeyType::Ed25519;
-  Bytes bytes;
+  ByteView bytes;
   std::string Type() const {
     return type == KeyType::Ed25519 ? "ed25519" : type == KeyType::Sr25519 ? "sr25519" : "other";
   }
@@ -354,8 +363,10 @@ struct Commit {
   }
 };
 
+// Views into the caller's tmv_validator array: converting a validator set
+// allocates nothing per validator.
 struct Validator {
-  Bytes address;
+  ByteView address;
   PubKey pub_key;
   int64_t voting_power = 0;
   int64_t proposer_priority = 0;
@@ -386,7 +397,7 @@ struct ValidatorSet {
   // types/validator_set.go:267-274 (linear scan, like the reference)
   std::pair<int32_t, const Validator *> GetByAddress(ByteView addr) const {
     for (size_t i = 0; i < validators.size(); i++)
-      if (ByteView(validators[i].address) == addr) return {(int32_t)i, &validators[i]};
+      if (validators[i].address == addr) return {(int32_t)i, &validators[i]};
     return {-1, nullptr};
   }
   // types/validator_set.go:322-344: highest priority, ties to the smaller address
@@ -499,7 +510,7 @@ constexpr int kBatchVerifyThreshold = 2;  // types/validation.go:12
 // from the commit's template (tmv_verify_votes).
 struct SigEntry {
   KeyType kind;
-  const Bytes *pk;
+  ByteView pk;  // the validator's key (entries of one key share its data pointer)
   uint32_t sig_len;
   const uint8_t *sig;
 };
@@ -562,7 +573,7 @@ struct CommitVerifier {
         seen[vi] = (int)idx;
         val = v;
       }
-      SigEntry e{val->pub_key.type, &val->pub_key.bytes, 0, nullptr};
+      SigEntry e{val->pub_key.type, val->pub_key.bytes, 0, nullptr};
       if (pl.batch) {
         AddCheck ac = CheckAdd(bkind, val->pub_key, cs.signature);
         if (ac.sync) {  // bv.Add error, returned verbatim (:211-213)

@@ -230,7 +230,7 @@ int tmv_validator_set_hashes(tmv_ctx *, const uint8_t *pk, const uint8_t *key_ki
     for (uint32_t i = set_off[s]; i < set_off[s + 1]; i++) {
       Validator v;
       v.pub_key = PubKey{key_kind[i] == TMV_KIND_SR25519 ? KeyType::Sr25519 : KeyType::Ed25519,
-                         Bytes(pk + 32 * i, pk + 32 * i + 32)};
+                         ByteView(pk + 32 * i, 32)};
       v.voting_power = power[i];
       vs.validators.push_back(v);
     }

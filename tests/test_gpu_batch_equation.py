@@ -345,14 +345,15 @@ def test_multi_batch_launch_over_64(bctx):
 
 def _located_case(n=150_000 + 91, m=256):
     """n honest commit signatures (tiled) with bad entries placed so that
-    some groups of m hold one bad entry and some two (R byte flips: R still
-    decodes, the equation fails)."""
+    some groups of m hold one bad entry and some two (S's low bit flipped: S
+    stays canonical and R, A still decode, so every bad entry passes the
+    pre-checks and fails only the equation)."""
     b = make_commit_batch(1500, seed=23).tile(n)
     sig = b.sig.copy()
     singles = [0, m + m - 1, 5 * m + 17, 9 * m + 200, 40 * m + 3, n - 2]
     pairs = [(12 * m + 1, 12 * m + 9), (30 * m + 100, 30 * m + 101)]
     for i in singles + [x for p in pairs for x in p]:
-        sig[64 * i + 5] ^= 0x10
+        sig[64 * i + 32] ^= 0x01
     return b, sig, singles, pairs
 
 
