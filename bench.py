@@ -676,8 +676,9 @@ def main():
         h2d = hb.pk.nbytes + hb.sig.nbytes + hb.msg.nbytes + hb.off.nbytes
         extras["end_to_end_h2d_bytes_per_sig"] = round(h2d / hb.n, 1)
         extras["end_to_end_h2d_GBps"] = round(h2d / statistics.median(e2e) / 1e9, 2)
-        extras["end_to_end_note"] = (f"{hb.n} host-resident signatures per call (pinned staging + PCIe + kernels + "
-                                     "D2H); never the headline value")
+        extras["end_to_end_note"] = (f"{hb.n} host-resident signatures per call (the caller's pages pinned part by "
+                                     "part and DMA'd directly, TMV_REGISTER; + kernels + D2H); never the headline "
+                                     "value")
         # p50 / p99 of types.VerifyCommit on a 150-validator commit (C1): the
         # C++ L3 path (sign-bytes, tally, batch verifier, error mapping) +
         # H2D + GPU kernels + D2H, through tmv_verify_commit.

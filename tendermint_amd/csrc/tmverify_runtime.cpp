@@ -198,6 +198,13 @@ struct HostLane {
   // `join` orders the launch's tail after them
   hipStream_t helper = nullptr;
   hipEvent_t join = nullptr;
+  // caller pages pinned for the chunk in flight (streamed path, direct DMA);
+  // unregistered when the chunk is harvested
+  std::vector<void *> pinned;
+  void unpin() {
+    for (void *p : pinned) (void)hipHostUnregister(p);
+    pinned.clear();
+  }
 };
 constexpr int kLanes = 4;  // streams per device; TMV_HOST_LANES of them carry chunks
 
@@ -279,6 +286,13 @@ int g_mixed_two = 1;               // TMV_MIXED_TWO=0: a mixed launch's two kind
 // with 32k / 128k, 6.1 with 16k / 32k; one stream 6.05-6.3; unstreamed
 // (two lanes of 80k chunks) 6.9 ms
 uint32_t g_stream_first = 32768, g_stream_part = 65536, g_stream_chunk = 1u << 21;
+// Streamed parts DMA straight from the caller's buffers: each part pins the
+// whole pages of its pk / sig / msg spans (hipHostRegister, disjoint page
+// ranges part to part) while earlier parts run, and only the bytes outside
+// them (< 4 KiB per span and part) go through the lane's pinned staging
+// (TMV_REGISTER=0: stage everything).  A span whose pages cannot be pinned
+// (already pinned, read-only mapping, ...) is staged.
+int g_register = 1;
 
 void read_env() {
   static std::once_flag once;
@@ -316,6 +330,8 @@ void read_env() {
     if (sf) g_stream_first = std::max<uint32_t>(1, (uint32_t)strtoul(sf, nullptr, 10));
     const char *sp = getenv("TMV_STREAM_PART");
     if (sp) g_stream_part = std::max<uint32_t>(1, (uint32_t)strtoul(sp, nullptr, 10));
+    const char *rg = getenv("TMV_REGISTER");
+    if (rg) g_register = atoi(rg);
     const char *sc = getenv("TMV_STREAM_CHUNK");
     if (sc) g_stream_chunk = std::max<uint32_t>(2048, (uint32_t)strtoul(sc, nullptr, 10));
   });
@@ -1194,13 +1210,53 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       if (hipStreamCreateWithFlags(&ln.helper, hipStreamNonBlocking) != hipSuccess) ln.helper = nullptr;
       else if (hipEventCreateWithFlags(&ln.join, hipEventDisableTiming) != hipSuccess) ln.join = nullptr;
     }
+    bool pin_ok = g_register != 0;
+    double pin_ms = 0;
+    ln.unpin();
     const PartFeeder feed = [&](uint32_t a, uint32_t b, hipEvent_t *ready) -> int {
       for (uint32_t i = a; i <= b; i++) off[i] = msg_off[lo + i] - base;
       const size_t m0 = off[a], m1 = off[b];
-      const CopySpan sp[3] = {{h + L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a)},
-                              {h + L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a)},
-                              {h + L.msg + m0, msg + base + m0, m1 - m0}};
-      par_memcpy_spans(sp, 3);
+      // per span: [dst offset, caller bytes, length]; then the pinned middle
+      struct Span {
+        size_t at;
+        const uint8_t *src;
+        size_t len;
+        size_t d0, d1;  // [d0, d1): DMA'd from the caller's pinned pages
+      } sp[3] = {{L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a), 0, 0},
+                 {L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a), 0, 0},
+                 {L.msg + m0, msg + base + m0, m1 - m0, 0, 0}};
+      constexpr uintptr_t kPage = 4096;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (Span &x : sp) {
+        if (!pin_ok || x.len < 4 * kPage) continue;
+        // pages [floor(start), floor(end)) -- part 0 from ceil(start), so no
+        // page outside the caller's span is pinned; consecutive parts' page
+        // ranges are disjoint
+        const uintptr_t s0 = (uintptr_t)x.src, s1 = s0 + x.len;
+        const uintptr_t r0 = a == 0 ? (s0 + kPage - 1) & ~(kPage - 1) : s0 & ~(kPage - 1);
+        const uintptr_t r1 = s1 & ~(kPage - 1);
+        if (r1 <= r0 + kPage) continue;
+        if (hipHostRegister(reinterpret_cast<void *>(r0), r1 - r0, hipHostRegisterDefault) != hipSuccess) {
+          (void)hipGetLastError();
+          pin_ok = false;  // stage the rest of the chunk
+          continue;
+        }
+        ln.pinned.push_back(reinterpret_cast<void *>(r0));
+        x.d0 = std::max(s0, r0) - s0;
+        x.d1 = r1 - s0;
+      }
+      pin_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      CopySpan cs[6];
+      size_t ncs = 0;
+      for (const Span &x : sp) {
+        if (x.d1 == 0) {
+          cs[ncs++] = {h + x.at, x.src, x.len};
+          continue;
+        }
+        if (x.d0) cs[ncs++] = {h + x.at, x.src, x.d0};
+        if (x.d1 < x.len) cs[ncs++] = {h + x.at + x.d1, x.src + x.d1, x.len - x.d1};
+      }
+      par_memcpy_spans(cs, ncs);
       if (part >= ln.part_ready.size()) {
         hipEvent_t ev;
         hipError_t ce = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -1209,14 +1265,21 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       }
       hipEvent_t ev = ln.part_ready[part++];
       hipError_t ce;
-      const size_t offs[4][2] = {{L.pk + 32ull * a, 32ull * (b - a)}, {L.sig + 64ull * a, 64ull * (b - a)},
-                                 {L.off + 4ull * a, 4ull * (b - a + 1)}, {L.msg + m0, m1 - m0}};
-      for (const auto &c : offs) {
-        if (c[1] && (ce = hipMemcpyAsync(dd + c[0], h + c[0], c[1], hipMemcpyHostToDevice, ln.copy)) != hipSuccess) {
+      auto h2d = [&](size_t at, const void *src, size_t len) -> bool {
+        if (!len) return true;
+        if ((ce = hipMemcpyAsync(dd + at, src, len, hipMemcpyHostToDevice, ln.copy)) != hipSuccess) {
           set_error("hipMemcpyAsync(H2D)", ce);
-          return TMV_ERR_LAUNCH;
+          return false;
         }
-        ctx->m_h2d += c[1];
+        ctx->m_h2d += len;
+        return true;
+      };
+      if (!h2d(L.off + 4ull * a, h + L.off + 4ull * a, 4ull * (b - a + 1))) return TMV_ERR_LAUNCH;
+      for (const Span &x : sp) {
+        const bool ok = x.d1 == 0 ? h2d(x.at, h + x.at, x.len)
+                                  : h2d(x.at, h + x.at, x.d0) && h2d(x.at + x.d0, x.src + x.d0, x.d1 - x.d0) &&
+                                        h2d(x.at + x.d1, h + x.at + x.d1, x.len - x.d1);
+        if (!ok) return TMV_ERR_LAUNCH;
       }
       if ((ce = hipEventRecord(ev, ln.copy)) != hipSuccess) {
         set_error("part event", ce);
@@ -1230,11 +1293,12 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
                                n, static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed,
                                g_stream_two ? ln.helper : nullptr, g_stream_two ? ln.join : nullptr);
     if (rc != 0) {  // parts already enqueued still use the lane's buffers: drain before returning
-      (void)wait_stream(d, ln.copy);
+      const bool drained = wait_stream(d, ln.copy) == hipSuccess;
       if (ln.helper) (void)wait_stream(d, ln.helper);
-      (void)wait_stream(d, ln.stream);
+      if (wait_stream(d, ln.stream) == hipSuccess && drained) ln.unpin();
       return rc;
     }
+    if (tm.on) fprintf(stderr, "[tmv_engine] pinning %9.3f ms (%zu ranges)\n", pin_ms, ln.pinned.size());
     tm.mark("parts staged + launched", n);
     if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
       set_error("hipMemcpyAsync(D2H)", e);
@@ -1437,6 +1501,8 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
           std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
           if (ctx->stats) collect_stats(ctx, d, ln.stream);
         }
+        // the chunk's copies are done (its stream waited on every part's copy)
+        if (r == 0 && (ok || !d.faulted)) ln.unpin();
         ln.n = 0;
         return r;
       },

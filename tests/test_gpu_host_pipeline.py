@@ -90,6 +90,7 @@ def test_chunked_host_batches(chunk, capacity, extra):
 
 BIG = r"""
 import json, sys, numpy as np
+import torch  # before the engine's HIP init (pinned buffer below)
 sys.path.insert(0, '.')
 from tendermint_amd import _native as N
 from tendermint_amd.testing.factory import Batch, make_c2_batch
@@ -102,15 +103,38 @@ for reps in (20, 3):  # 200k: parts of 16k + 3 x 64k + a ragged tail; 30k: two p
     for _ in range(2):
         ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, hb.pk, hb.sig, hb.msg, hb.off)
         assert np.array_equal(st.astype(np.uint8), np.tile(bits, reps)), reps
+# caller buffers at odd addresses (pinned pages start past each span's
+# head, the bytes around them staged) and a buffer that is already pinned
+# (its registration fails: staged)
+def shifted(a, k):
+    buf = np.zeros(a.nbytes + 64, np.uint8)
+    v = buf[k:k + a.nbytes]
+    v[:] = a.reshape(-1).view(np.uint8)
+    return v.view(a.dtype).reshape(a.shape)
+hb = Batch.concat([b] * 20)
+want = np.tile(bits, 20)
+ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, shifted(hb.pk, 1), shifted(hb.sig, 3),
+                             shifted(hb.msg, 5), hb.off)
+assert np.array_equal(st.astype(np.uint8), want)
+assert torch.cuda.is_available()
+pinned_sig = torch.from_numpy(hb.sig.copy()).pin_memory().numpy()
+ctx.metrics_reset()
+ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, hb.pk, pinned_sig, hb.msg, hb.off)
+assert np.array_equal(st.astype(np.uint8), want)
+assert ctx.metrics()["h2d_bytes"] == hb.pk.nbytes + hb.sig.nbytes + hb.msg.nbytes + hb.off.nbytes
 print("ok")
 """
 
 
-def test_streamed_c2_host_batches():
+@pytest.mark.parametrize("register", ["1", "0"])
+def test_streamed_c2_host_batches(register):
     """The driver-sized host batch (BASELINE C2 tiled to 200k and 30k entries)
     streamed with the default parts: the vector equals the committed C2
-    bitmap repeated, twice in a row on the same lane."""
+    bitmap repeated, twice in a row on the same lane; with the caller's pages
+    pinned part by part (TMV_REGISTER=1, misaligned and already-pinned
+    buffers included) and with everything staged."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, "-c", BIG], cwd=root, capture_output=True, text=True, timeout=600)
+    env = dict(os.environ, TMV_REGISTER=register)
+    out = subprocess.run([sys.executable, "-c", BIG], cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "ok" in out.stdout

@@ -1,5 +1,5 @@
 """End-to-end (host buffers: pinned staging + PCIe + kernels + D2H) rate of
-the bench's 320k-signature C2 call under the current TMV_* environment
+the bench's 640k-signature C2 call (64 batches) under the current TMV_* environment
 (development tool).  The batch is generated once and cached in /tmp, so a
 shell loop can A/B runtime knobs in separate processes:
 
@@ -10,7 +10,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 from concurrent.futures import ProcessPoolExecutor
 import numpy as np
 
-CACHE = "/tmp/tmv_e2e_c2x32.npz"
+CACHE = "/tmp/tmv_e2e_c2x64.npz"
+NB = 64
 
 
 def _c2(seed):
@@ -22,7 +23,7 @@ def _c2(seed):
 def main():
     if not os.path.exists(CACHE):
         with ProcessPoolExecutor(8) as ex:
-            parts = list(ex.map(_c2, [0xED25519 + j for j in range(32)]))
+            parts = list(ex.map(_c2, [0xED25519 + j for j in range(NB)]))
         from tendermint_amd.testing.factory import Batch
         hb = Batch.concat([Batch(pk, sig, msg, off) for pk, sig, msg, off in parts])
         np.savez(CACHE, pk=hb.pk, sig=hb.sig, msg=hb.msg, off=hb.off)
@@ -37,10 +38,12 @@ def main():
         t = time.perf_counter()
         ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, pk, sig, msg, off)
         ts.append(time.perf_counter() - t)
-        assert int((st == 1).sum()) == 32 * 9950
+        assert int((st == 1).sum()) == NB * 9950
     m = statistics.median(ts[2:])
     env = {k: v for k, v in os.environ.items() if k.startswith("TMV_")}
-    print(json.dumps({"env": env, "n": n, "median_ms": round(m * 1e3, 3), "e2e_verifies_per_s": round(n / m)}))
+    h2d = pk.nbytes + sig.nbytes + msg.nbytes + off.nbytes
+    print(json.dumps({"env": env, "n": n, "median_ms": round(m * 1e3, 3), "e2e_verifies_per_s": round(n / m),
+                      "h2d_GBps": round(h2d / m / 1e9, 2), "metrics": ctx.metrics()}))
 
 
 if __name__ == "__main__":

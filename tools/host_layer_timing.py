@@ -31,7 +31,7 @@ vals, blocks = Fa.make_block_chain(a.blocks, 175)
 jobs = []
 for i in range(1, len(blocks) - 1):
     f = blocks[i]
-    jobs.append(H.CommitJob(H.MODE_LIGHT, "test_chain_id", vals, f.block_id, f.height, f.commit))
+    jobs.append(H.CommitJob(H.MODE_LIGHT, "test_chain_id", vals, f.block_id, f.height, blocks[i + 1].last_commit))
     jobs.append(H.CommitJob(H.MODE_FULL, "test_chain_id", vals, blocks[i - 1].block_id, f.height - 1, f.last_commit))
 pj = H.PreparedJobs(jobs)
 ts = []
