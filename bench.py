@@ -78,7 +78,7 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-PMC_DIRS = ("r02_final", "r02_close", "r02", "r01_close")  # newest first
+PMC_DIRS = ("r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
 
 
 def _load_pmc(method: str, batches_per_step: int = 32):
@@ -98,8 +98,11 @@ def _load_pmc(method: str, batches_per_step: int = 32):
         out = dict(pmc)
         if "hbm_bytes_per_launch" in pmc:
             out["hbm_bytes_per_step"] = int(pmc["hbm_bytes_per_launch"] * batches_per_step / per_launch)
+            fac = pmc.get("fetch_factors")
+            how = (f"FETCH_SIZE x calibrated factors {fac} (tools/fetchbench.hip)" if fac
+                   else "FETCH_SIZE x2 gfx950 correction")
             out["note"] = (f"HBM bytes per step ({batches_per_step} x 10k signatures) from PMC (profiles/{d}/{name}: "
-                           f"FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, launches of {per_launch} batches); "
+                           f"{how} + WRITE_SIZE, launches of {per_launch} batches); "
                            f"algorithmic input bytes per step = {batches_per_step} x 10k x ~222 B")
         out["source"] = f"profiles/{d}/{name}"
         return out
