@@ -16,67 +16,75 @@ namespace {
 
 thread_local bool t_in_pool = false;  // a pool worker, or a caller running a pool job
 
+// Jobs run side by side: every caller drains its own job and idle workers
+// join whichever posted job still has indices left (up to its helper
+// count), so two host-layer calls on different threads -- one planning a
+// window while the other waits on the GPU -- both get workers.
 class WorkerPool {
  public:
   explicit WorkerPool(size_t workers) {
-    for (size_t w = 0; w < workers; w++) std::thread([this, w] { loop(w); }).detach();
+    for (size_t w = 0; w < workers; w++) std::thread([this] { loop(); }).detach();
     nworkers_ = workers;
   }
 
   size_t workers() const { return nworkers_; }
 
-  // false: busy (the caller runs the loop itself)
-  bool run(size_t n, size_t helpers, void (*fn)(void *, size_t), void *ctx) {
-    std::unique_lock<std::mutex> job_lock(job_mu_, std::try_to_lock);
-    if (!job_lock.owns_lock()) return false;
+  void run(size_t n, size_t helpers, void (*fn)(void *, size_t), void *ctx) {
+    Job job;
+    job.fn = fn;
+    job.ctx = ctx;
+    job.n = n;
+    job.want = helpers;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      fn_ = fn;
-      ctx_ = ctx;
-      n_ = n;
-      next_.store(0, std::memory_order_relaxed);
-      want_ = helpers;
-      pending_ = helpers;
-      gen_++;
+      jobs_.push_back(&job);
     }
     cv_.notify_all();
     t_in_pool = true;
-    drain();
+    drain(job);
     t_in_pool = false;
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return pending_ == 0; });
-    return true;
+    // no helper can join once the job is off the list; wait for those in it
+    jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
+    done_cv_.wait(lk, [&] { return job.helpers == 0; });
   }
 
  private:
-  void drain() {
-    for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < n_;) fn_(ctx_, i);
+  struct Job {
+    void (*fn)(void *, size_t) = nullptr;
+    void *ctx = nullptr;
+    size_t n = 0, want = 0, helpers = 0;  // helpers: workers inside drain (under mu_)
+    std::atomic<size_t> next{0};
+  };
+
+  static void drain(Job &j) {
+    for (size_t i; (i = j.next.fetch_add(1, std::memory_order_relaxed)) < j.n;) j.fn(j.ctx, i);
   }
 
-  void loop(size_t w) {
+  Job *pick() {  // under mu_
+    for (Job *j : jobs_)
+      if (j->helpers < j->want && j->next.load(std::memory_order_relaxed) < j->n) return j;
+    return nullptr;
+  }
+
+  void loop() {
     t_in_pool = true;
-    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (w >= want_) continue;  // not needed for this job
-      }
-      drain();
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) done_cv_.notify_one();
+      Job *j;
+      cv_.wait(lk, [&] { return (j = pick()) != nullptr; });
+      j->helpers++;
+      lk.unlock();
+      drain(*j);
+      lk.lock();
+      if (--j->helpers == 0) done_cv_.notify_all();
     }
   }
 
-  std::mutex job_mu_;  // one job at a time
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  void (*fn_)(void *, size_t) = nullptr;
-  void *ctx_ = nullptr;
-  size_t n_ = 0, want_ = 0, pending_ = 0, nworkers_ = 0;
-  std::atomic<size_t> next_{0};
-  uint64_t gen_ = 0;
+  std::vector<Job *> jobs_;
+  size_t nworkers_ = 0;
 };
 
 WorkerPool &pool() {
@@ -97,9 +105,11 @@ size_t pool_threads() {
 
 void pool_for(size_t n, size_t max_threads, void (*fn)(void *, size_t), void *ctx) {
   const size_t nt = std::min({max_threads, n, pool_threads()});
-  if (nt <= 1 || t_in_pool || !pool().run(n, std::min(nt - 1, pool().workers()), fn, ctx)) {
+  if (nt <= 1 || t_in_pool) {
     for (size_t i = 0; i < n; i++) fn(ctx, i);
+    return;
   }
+  pool().run(n, std::min(nt - 1, pool().workers()), fn, ctx);
 }
 
 }  // namespace tmh

@@ -2,8 +2,8 @@
 // loops (packing, planning, key lookups, staging copies).  Spawning and
 // joining 15 threads costs ~0.2-0.5 ms, several times per commit window;
 // the pool's workers sleep on a condition variable between jobs instead.
-// One job runs at a time; a caller that finds the pool busy (another thread
-// inside the engine, or a loop nested in a pool job) runs its loop itself.
+// Jobs of different caller threads run side by side (idle workers join any
+// job with work left); a loop nested in a pool job runs on its thread.
 #pragma once
 #include <cstddef>
 #include <type_traits>

@@ -9,7 +9,10 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <string>
@@ -23,6 +26,83 @@
 #include "tm_types.h"
 
 namespace tmh_internal {
+
+uint32_t host_slice_jobs() {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("TMV_HOST_SLICE");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 512u;
+  }();
+  return v;
+}
+
+namespace {
+// The partner thread of run_sliced: runs one posted task at a time.
+class Partner {
+ public:
+  Partner() { std::thread([this] { loop(); }).detach(); }
+  void post(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(mu_);
+    task_ = std::move(f);
+    busy_ = true;
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [this] { return !busy_; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return (bool)task_; });
+      std::function<void()> f = std::move(task_);
+      task_ = nullptr;
+      lk.unlock();
+      f();
+      lk.lock();
+      busy_ = false;
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::function<void()> task_;
+  bool busy_ = false;
+};
+}  // namespace
+
+int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), void *ctx) {
+  const uint32_t target = host_slice_jobs();
+  if (!target || n_jobs < 2 * target) return run_slice(ctx, 0, n_jobs);
+  // one partner per process: concurrent sliced calls queue for it (the
+  // second caller runs its slices alone)
+  // never destroyed: the detached thread waits on its condition variable
+  // until exit (destroying it under a waiter blocks at exit)
+  static Partner *partner = new Partner;
+  static std::mutex *partner_mu = new std::mutex;
+  std::unique_lock<std::mutex> own(*partner_mu, std::try_to_lock);
+  const uint32_t ns = (n_jobs + target - 1) / target, per = (n_jobs + ns - 1) / ns;
+  std::atomic<uint32_t> next{0};
+  std::atomic<int> bad{0}, err{0};
+  auto work = [&] {
+    for (uint32_t k; (k = next.fetch_add(1)) < ns;) {
+      const uint32_t lo = k * per, hi = std::min(n_jobs, lo + per);
+      if (lo >= hi) continue;
+      const int r = run_slice(ctx, lo, hi);
+      if (r < 0) {
+        int z = 0;
+        err.compare_exchange_strong(z, r);
+      } else {
+        bad.fetch_add(r);
+      }
+    }
+  };
+  if (own.owns_lock()) partner->post(work);
+  work();
+  if (own.owns_lock()) partner->wait();
+  return err.load() ? err.load() : bad.load();
+}
 
 void put_err(char *err, size_t cap, const std::string &s) {
   if (!err || cap == 0) return;
@@ -247,36 +327,38 @@ struct GpuBackend {
     PackBuffers &pb = tls;  // the workers below must use this thread's buffers, not their own
     PhaseTimer tm("tmv_verify_commits");
     st.assign(es.size(), 0);
-    // one template per (commit object, chain_id)
+    // one template per (commit object, chain_id): entries come plan by plan,
+    // so the plans' runs are found first, each run's template is looked up
+    // once (serially: ~10^3 runs), and the entries are filled in parallel
     std::vector<tmh::VoteTemplate> tmpls;
     std::unordered_map<const tmh::CommitPlan *, uint32_t> plan_tmpl;
     std::unordered_map<const tmh::Commit *, std::vector<std::pair<const std::string *, uint32_t>>> by_commit;
     std::vector<uint32_t> ent_tmpl(es.size());
-    const tmh::CommitPlan *last = nullptr;  // entries come plan by plan
-    uint32_t last_t = 0;
+    std::vector<std::pair<size_t, uint32_t>> runs;  // (first entry, template) of each run of one plan
     for (size_t i = 0; i < es.size(); i++) {
       const tmh::CommitPlan *pl = es[i].pl;
-      if (pl != last) {
-        auto [it, fresh] = plan_tmpl.emplace(pl, 0);
-        if (fresh) {
-          auto &chains = by_commit[pl->commit];
-          uint32_t t = UINT32_MAX;
-          for (auto &c : chains)
-            if (*c.first == pl->chain_id) t = c.second;
-          if (t == UINT32_MAX) {
-            t = (uint32_t)tmpls.size();
-            const tmh::Commit &cm = *pl->commit;
-            tmpls.push_back(tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round,
-                                                    &cm.block_id));
-            chains.emplace_back(&pl->chain_id, t);
-          }
-          it->second = t;
+      if (i && pl == es[i - 1].pl) continue;
+      auto [it, fresh] = plan_tmpl.emplace(pl, 0);
+      if (fresh) {
+        auto &chains = by_commit[pl->commit];
+        uint32_t t = UINT32_MAX;
+        for (auto &c : chains)
+          if (*c.first == pl->chain_id) t = c.second;
+        if (t == UINT32_MAX) {
+          t = (uint32_t)tmpls.size();
+          const tmh::Commit &cm = *pl->commit;
+          tmpls.push_back(tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round,
+                                                  &cm.block_id));
+          chains.emplace_back(&pl->chain_id, t);
         }
-        last = pl;
-        last_t = it->second;
+        it->second = t;
       }
-      ent_tmpl[i] = last_t;
+      runs.emplace_back(i, it->second);
     }
+    runs.emplace_back(es.size(), 0u);
+    parallel_for(runs.size() - 1, 32, [&](size_t r) {
+      std::fill(ent_tmpl.begin() + runs[r].first, ent_tmpl.begin() + runs[r + 1].first, runs[r].second);
+    });
     tm.mark("b:tmpl");
     std::vector<tmv_vote_template> tv(tmpls.size());
     for (size_t t = 0; t < tmpls.size(); t++) {
@@ -563,18 +645,18 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
     if (errs && err_stride) put_err(errs, err_stride, tmv_last_error());
     return be.infra;
   }
-  int bad = 0;
-  std::vector<int8_t> buf;
-  for (uint32_t j = 0; j < n_jobs; j++) {
+  std::atomic<int> bad{0};
+  parallel_for(n_jobs, 64, [&](size_t j) {
+    static thread_local std::vector<int8_t> buf;
     buf.resize(joff[j + 1] - joff[j]);
     for (size_t e = 0; e < buf.size(); e++) buf[e] = st[where[joff[j] + e]];
     bool ne = false;
     tmh::Error e = tmh::CommitVerifier::Finish(plans[j], buf.data(), &ne);
     if (results) results[j] = e ? 1 : 0;
     if (not_enough) not_enough[j] = ne ? 1 : 0;
-    if (errs && err_stride) put_err(errs + (size_t)j * err_stride, err_stride, e ? *e : std::string());
-    bad += e ? 1 : 0;
-  }
+    if (errs && err_stride) put_err(errs + j * err_stride, err_stride, e ? *e : std::string());
+    if (e) bad.fetch_add(1, std::memory_order_relaxed);
+  });
   tm.mark("finish");
   // the converted sets, commits and plans are ~10^5 small heap objects per
   // window; freed on one thread they took ~7 ms of a C3 window
@@ -583,7 +665,7 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
     if (i < own_c.size()) own_c[i].reset();
     if (i < n_jobs) plans[i] = tmh::CommitPlan();
   });
-  return bad;
+  return bad.load();
 }
 
 }  // namespace tmh_internal
@@ -592,7 +674,22 @@ extern "C" {
 
 int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
                        size_t err_stride) {
-  return verify_commits(ctx, jobs, n_jobs, results, errs, err_stride, nullptr);
+  if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
+  struct Call {
+    tmv_ctx *ctx;
+    const tmv_commit_job *jobs;
+    int32_t *results;
+    char *errs;
+    size_t stride;
+  } c{ctx, jobs, results, errs, err_stride};
+  const int rc = run_sliced(n_jobs, [](void *p, uint32_t lo, uint32_t hi) {
+    const Call &c = *static_cast<const Call *>(p);
+    const int r = verify_commits(c.ctx, c.jobs + lo, hi - lo, c.results ? c.results + lo : nullptr,
+                                 c.errs && c.stride ? c.errs + (size_t)lo * c.stride : nullptr, c.stride, nullptr);
+    if (r < 0 && lo && c.errs && c.stride) std::memcpy(c.errs, c.errs + (size_t)lo * c.stride, c.stride);
+    return r;
+  }, &c);
+  return rc;
 }
 
 int tmv_verify_vote_batch(tmv_ctx *ctx, const char *chain_id, const tmv_vote_in *votes, uint32_t n,

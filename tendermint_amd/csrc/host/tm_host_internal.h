@@ -65,4 +65,19 @@ void parallel_for(size_t n, size_t min_per_thread, F fn) {
   tmh::parallel_for_n(n, n / std::max<size_t>(1, min_per_thread), fn);
 }
 
+// Jobs per slice of a large tmv_verify_commits / tmv_light_verify_many call
+// (TMV_HOST_SLICE; 0 = no slicing).
+uint32_t host_slice_jobs();
+
+// Pipelined host layer: jobs [0, n_jobs) cut into slices that two threads
+// (the caller and a persistent partner thread) take in turn, each running
+// run_slice(lo, hi) -- a whole host-layer pass over those jobs.  The engine
+// serialises calls per device, so while one slice's engine call holds the
+// GPU the other slice's host phases (convert, hash packing, plan, dedup,
+// sign-bytes templates, packing) run: window k + 1 is prepared while window
+// k verifies.  Every job's result is its own (sharing only saves work), so
+// slicing changes no result.  Returns the sum of the slices' returns, or the
+// first negative one.
+int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), void *ctx);
+
 }  // namespace tmh_internal

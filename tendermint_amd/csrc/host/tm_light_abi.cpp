@@ -137,6 +137,9 @@ struct Interner {  // distinct C pointers -> dense indices
   }
 };
 
+int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                       size_t err_stride);
+
 }  // namespace
 
 extern "C" {
@@ -163,6 +166,29 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
   if (!ctx || (!jobs && n_jobs)) return TMV_ERR_ARG;
   for (uint32_t j = 0; j < n_jobs; j++)
     if (jobs[j].mode < TMV_LIGHT_VERIFY || jobs[j].mode > TMV_LIGHT_NON_ADJACENT) return TMV_ERR_ARG;
+  struct Call {
+    tmv_ctx *ctx;
+    const tmv_light_job *jobs;
+    int32_t *results;
+    char *errs;
+    size_t stride;
+  } c{ctx, jobs, results, errs, err_stride};
+  return run_sliced(n_jobs, [](void *p, uint32_t lo, uint32_t hi) {
+    const Call &c = *static_cast<const Call *>(p);
+    const int r = light_verify_slice(c.ctx, c.jobs + lo, hi - lo, c.results ? c.results + lo : nullptr,
+                                     c.errs && c.stride ? c.errs + (size_t)lo * c.stride : nullptr, c.stride);
+    if (r < 0 && lo && c.errs && c.stride) std::memcpy(c.errs, c.errs + (size_t)lo * c.stride, c.stride);
+    return r;
+  }, &c);
+}
+
+}  // extern "C"
+
+namespace {
+
+// One pass of the light checks over jobs (tmv_light_verify_many's slices).
+int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs, int32_t *results, char *errs,
+                       size_t err_stride) {
   PhaseTimer tm("tmv_light_verify_many");
   const PhaseEnd tm_end{tm, "release"};
   // distinct headers, commits and validator sets, converted once
@@ -299,6 +325,10 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
   });
   return bad;
 }
+
+}  // namespace
+
+extern "C" {
 
 int tmv_light_verify(tmv_ctx *ctx, const tmv_light_job *job, char *err, size_t err_cap) {
   if (!job) return TMV_ERR_ARG;

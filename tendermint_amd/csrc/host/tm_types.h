@@ -525,7 +525,7 @@ struct CommitPlan {
   int64_t tallied = 0, needed = 0;
   std::vector<SigEntry> entries;     // in Add order
   std::vector<int> sig_idx;          // commit.Signatures index of each entry
-  std::vector<std::string> deferred_sig;
+  std::vector<std::string> deferred_sig;  // per entry when defer_add (sr25519 batch), else empty
   std::vector<uint8_t> crosses;      // single: this entry crosses the threshold (early ok)
   const Commit *commit = nullptr;
   std::string chain_id;              // the messages are this commit's votes on chain_id
@@ -555,6 +555,9 @@ struct CommitVerifier {
     }
     std::unordered_map<int32_t, int> seen;
     pl.entries.reserve(commit.signatures.size());
+    pl.sig_idx.reserve(commit.signatures.size());
+    pl.crosses.reserve(commit.signatures.size());
+    if (pl.defer_add) pl.deferred_sig.reserve(commit.signatures.size());
     for (size_t idx = 0; idx < commit.signatures.size(); idx++) {
       const CommitSig &cs = commit.signatures[idx];
       if (ignore(cs)) continue;
@@ -582,7 +585,7 @@ struct CommitVerifier {
         }
         e.sig = ac.sig64;
         e.sig_len = 64;
-        pl.deferred_sig.push_back(std::move(ac.deferred_sig));
+        if (pl.defer_add) pl.deferred_sig.push_back(std::move(ac.deferred_sig));  // sr25519 only
       } else {
         e.sig = cs.signature.data();
         e.sig_len = (uint32_t)cs.signature.size();

@@ -50,6 +50,13 @@ constexpr uint32_t kMsmWideRows = 65536;     // (group, window) rows from which 
 constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 8, 16 or 32
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
+// Buckets cut by chunk edges joined by k_msm_accum (neighbouring lanes of a
+// wave) and k_msm_join (the rest) before the running sums, which then read
+// whole buckets only.  -DTMV_NO_JOIN=1: k_msm_wpart joins them (round 2).
+#ifndef TMV_NO_JOIN
+#define TMV_NO_JOIN 0
+#endif
+constexpr bool kMsmJoin = !TMV_NO_JOIN;
 constexpr uint32_t kSubGroupLog2 = 3;        // k_msm_subcheck: 8 entries per sub-group
 constexpr uint32_t kSubGroup = 1u << kSubGroupLog2;
 
@@ -77,6 +84,12 @@ struct MsmParams {
   // (signed digits need one bit more, as WR for z < 2^128)
   TMV_HD uint32_t WL() const { return (129 + m_log2 + c - 1) / c; }
   TMV_HD uint32_t buckets_per_group() const { return W * H; }
+  // Bucket of (window w, |digit| - 1 = i) inside its group: window-major.
+  // (|digit|-major, so that k_msm_wpart's lanes -- one per window -- read
+  // adjacent buckets, measured slower: k_msm_sort's histogram and scatter
+  // lose more than the running sums gain, 122.0-122.8 vs 122.8-123.6 M/s,
+  // profiles/r03/ab_join_compact.txt.)
+  TMV_HD uint32_t bucket(uint32_t w, uint32_t i) const { return w * H + i; }
   TMV_HD uint32_t chunks_per_group() const { return cap / L; }
 
   static MsmParams make(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false) {
@@ -130,6 +143,7 @@ struct MsmWork {
   ge_p3 *bk_sum;       // groups x W x H: sums of buckets that fit in one chunk
   ge_p3 *part_first;   // chunks: run that began in an earlier chunk and ends here
   ge_p3 *part_last;    // chunks: run that continues into the next chunk
+  uint32_t *join_b;    // chunks: bucket whose chunk partials k_msm_join joins (the chunk of its last run), or kMsmEmpty
   ge_p3 *wpart;        // groups x W x P x 2: (T, U) of each window part
   ge_p3 *wsum;         // groups x W: window sums
   uint8_t *group_ok;   // groups
@@ -164,7 +178,8 @@ struct MsmWork {
     const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
     const size_t chunks = ent / p.L;
     size_t b = (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
-               2 * chunks * sizeof(ge_p3) + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 2 * G + 16 * 16;
+               2 * chunks * sizeof(ge_p3) + 4 * chunks + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 2 * G +
+               17 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
     else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
               G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16;
@@ -185,6 +200,7 @@ struct MsmWork {
     w.bk_sum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + bk * sizeof(ge_p3));
     w.part_first = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.part_last = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
+    w.join_b = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * chunks);
     w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.P * sizeof(ge_p3));
     w.wsum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * sizeof(ge_p3));
     w.group_ok = b + o; o = up(o + G);

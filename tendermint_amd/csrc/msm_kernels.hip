@@ -127,7 +127,7 @@ __device__ __forceinline__ void for_each_digit(const uint32_t *s, uint32_t windo
   int carry = 0;
   for (uint32_t w = 0; w < windows; w++) {
     const int d = window_digit<NW>(s, w, p.c, w + 1 == windows, carry);
-    if (d != 0) f(w * p.H + (uint32_t)((d < 0 ? -d : d) - 1), d < 0);
+    if (d != 0) f(p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1)), d < 0);
   }
 }
 
@@ -409,11 +409,19 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 
 // One lane per chunk of L sorted entries: sums each run of equal
 // bucket ids with mixed additions.  A run that is the whole bucket goes to
-// bk_sum; a run cut by the chunk's end goes to part_last, one cut by its
-// start to part_first (k_msm_wpart joins them).
+// bk_sum.  A bucket cut by chunk edges: the lane whose run opens it holds
+// the open run at its chunk's end, the lane whose chunk it ends in holds
+// its first run.  When those are neighbouring lanes of one wave (a bucket
+// over two chunks -- nearly every cut bucket: chunks hold 16 entries, the
+// mean bucket 4-8), the second lane leaves its run in LDS and the first
+// adds it after the loop and stores the whole bucket: no partials leave the
+// wave.  The rest (a wave's edge, buckets over three or more chunks) keep
+// their runs in part_last / part_first and name the bucket in join_b at the
+// chunk of its last run, for k_msm_join.
 template <int L>
 __global__ void __launch_bounds__(256)
 k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  __shared__ ge_p3 first_run[256];  // a lane's first run, joined by its wave neighbour (40 KB)
   // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD a
   // contiguous range of the LIVE chunks so a group's points stay in one L2
   // (mixed batches size the grid for n but use only their kind's groups)
@@ -427,6 +435,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t g = t / cpg;
   if (g >= live_groups) return;
   const uint32_t base = t * L;
+  const uint32_t lane = threadIdx.x & 63;
   uint32_t bk[L], pt[L];
   {
     const uint4 *b4 = reinterpret_cast<const uint4 *>(mw.ent_bk + base);
@@ -438,12 +447,23 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       pt[4 * q] = y.x; pt[4 * q + 1] = y.y; pt[4 * q + 2] = y.z; pt[4 * q + 3] = y.w;
     }
   }
-  if (bk[0] == kMsmEmpty) return;
+  if (bk[0] == kMsmEmpty) {  // padding: nothing to join (k_msm_join reads every live chunk's word)
+    if (kMsmJoin) mw.join_b[t] = kMsmEmpty;
+    return;
+  }
+  uint32_t join = kMsmEmpty;  // this chunk's join_b
   auto flush = [&](uint32_t b, uint32_t rs, uint32_t re, const ge_p3 &acc) {
     const uint32_t bs = mw.bk_start[b], be = bs + mw.bk_cnt[b];
-    if (rs == bs && re == be) mw.bk_sum[b] = acc;
-    else if (re == base + L && re < be) mw.part_last[t] = acc;
-    else mw.part_first[t] = acc;
+    if (rs == bs && re == be) {
+      mw.bk_sum[b] = acc;
+    } else if (re == base + L && re < be) {
+      mw.part_last[t] = acc;  // (the open run at the chunk's end: see below)
+    } else if (kMsmJoin && lane != 0 && bs >= base - L) {  // ends here, opened by the previous lane
+      first_run[threadIdx.x] = acc;
+    } else {
+      mw.part_first[t] = acc;
+      join = b;
+    }
   };
   // every lane's first run starts at entry 0: take that point as the
   // accumulator (one multiply) instead of adding it to the identity (seven)
@@ -478,7 +498,58 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     ge_p1p1_to_p3(acc, r);
     j = q + 1;
   }
-  flush(cur, rs, base + j, acc);
+  // the last run: whole, ending in this chunk, or open at the chunk's end
+  const uint32_t bs = mw.bk_start[cur], be = bs + mw.bk_cnt[cur];
+  const uint32_t re = base + j;
+  const bool open = re == base + L && re < be;
+  const bool join_next = kMsmJoin && open && bs >= base && lane != 63 && be <= base + 2 * L;
+  if (!open) flush(cur, rs, re, acc);
+  else if (!join_next) mw.part_last[t] = acc;
+  // the first runs are in LDS: wave-local exchange, no workgroup barrier
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (join_next) {
+    p3_add(acc, first_run[threadIdx.x + 1]);
+    mw.bk_sum[cur] = acc;
+  }
+  if (kMsmJoin) mw.join_b[t] = join;
+}
+
+// The buckets accumulation could not join inside a wave (about 1% of the
+// chunks name one): bucket value from its chunk partials (part_last of every
+// chunk but its last, part_first of the last).  Each wave scans
+// kJoinScan x 64 chunks' join_b words (coalesced), gathers the named
+// buckets into a wave-local LDS list and joins them 64 at a time, so the
+// grid is small and no wave walks the join for one lane.
+constexpr uint32_t kJoinScan = 16;
+__global__ void __launch_bounds__(256)
+k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  __shared__ uint32_t list[4][kJoinScan * 64];
+  const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
+  const uint32_t chunks = live_groups * p.chunks_per_group();
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t c0 = (blockIdx.x * 4 + wv) * kJoinScan * 64;
+  if (c0 >= chunks) return;  // wave-uniform
+  uint32_t cnt = 0;
+  for (uint32_t k = 0; k < kJoinScan; k++) {
+    const uint32_t t = c0 + k * 64 + lane;
+    const uint32_t b = t < chunks ? mw.join_b[t] : kMsmEmpty;
+    const uint64_t m = __ballot(b != kMsmEmpty);
+    if (b != kMsmEmpty) list[wv][cnt + __popcll(m & ((1ull << lane) - 1))] = b;
+    cnt += __popcll(m);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (uint32_t i = lane; i < cnt; i += 64) {
+    const uint32_t b = list[wv][i];
+    ge_p3 B;
+    bucket_value(mw, p.L, b, B, mw.bk_cnt[b], mw.bk_start[b]);
+    mw.bk_sum[b] = B;
+  }
 }
 
 // Window parts: lane (g, w, q) sums buckets [q s, (q+1) s) of window w with
@@ -495,16 +566,24 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   bool u_set = false, t_set = false;
   // the next bucket's count and start are loaded one iteration ahead, so
   // only its point load is exposed
-  const uint32_t b0 = g * p.W * p.H + wdx * p.H + part * s;
-  uint32_t cnt = mw.bk_cnt[b0 + s - 1], bst = mw.bk_start[b0 + s - 1];
+  const uint32_t gb = g * p.W * p.H, i0 = part * s;
+  uint32_t cnt = mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 1)], bst = mw.bk_start[gb + p.bucket(wdx, i0 + s - 1)];
   for (int i = (int)s - 1; i >= 0; i--) {
     ge_p3 B;
     const uint32_t c_i = cnt, s_i = bst;
     if (i > 0) {
-      cnt = mw.bk_cnt[b0 + (uint32_t)i - 1];
-      bst = mw.bk_start[b0 + (uint32_t)i - 1];
+      const uint32_t bn = gb + p.bucket(wdx, i0 + (uint32_t)i - 1);
+      cnt = mw.bk_cnt[bn];
+      bst = mw.bk_start[bn];
     }
-    if (bucket_value(mw, p.L, b0 + (uint32_t)i, B, c_i, s_i)) {
+    const uint32_t bb = gb + p.bucket(wdx, i0 + (uint32_t)i);
+    bool nz = c_i != 0;
+    if (kMsmJoin) {
+      if (nz) B = mw.bk_sum[bb];  // whole: joined by k_msm_accum or k_msm_join
+    } else {
+      nz = bucket_value(mw, p.L, bb, B, c_i, s_i);
+    }
+    if (nz) {
       if (u_set) p3_add(U, B);
       else { U = B; u_set = true; }
     }
@@ -904,6 +983,12 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
   hipError_t e;
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
+  if (kMsmJoin) {
+    const uint64_t per_block = 4ull * kJoinScan * 64;
+    hipLaunchKernelGGL(k_msm_join, dim3((uint32_t)((chunks + per_block - 1) / per_block)), dim3(256), 0, stream,
+                       count_ptr, n, mw, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
   tk = timed ? ktimer::begin(ktimer::kWpart, stream) : nullptr;
   hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
@@ -932,7 +1017,7 @@ static int subcheck_mode() {
 // k_msm_sort workgroup size for groups <= 256 entries: 64 by default
 // (TMV_SORT_BLOCK=256: the old 256).  A 64-entry group in a 256-thread
 // workgroup left 3 of 4 waves idle but resident through the sort's LDS
-// phases; C2 bench (3,072 steps, tools/gpu_ab_env.sh): 80.4 / 80.7 ->
+// phases; C2 bench (3,072 steps, round 1, one GPU call): 80.4 / 80.7 ->
 // 84.8 / 84.7 M/s.
 static int sort_block() {
   static const int bs = [] {
@@ -1005,6 +1090,7 @@ static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0)
   mw.bk_sum += g0 * wh;
   mw.part_first += g0 * p.chunks_per_group();
   mw.part_last += g0 * p.chunks_per_group();
+  mw.join_b += g0 * p.chunks_per_group();
   mw.wpart += g0 * p.W * 2ull * p.P;
   mw.wsum += g0 * p.W;
   mw.group_ok += g0;

@@ -870,7 +870,7 @@ template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *
                                                const uint32_t *, const uint32_t *);
 
 // Decode and hash blocks in one launch (default; TMV_PREP_FUSED=0: two
-// kernels).  Measured in one GPU call (tools/gpu_ab_env.sh): one 10k batch
+// kernels).  Measured in one GPU call (round 2): one 10k batch
 // 1.047 -> 0.987 ms through the batch equation, 0.546 -> 0.491 ms per entry;
 // the 32-batch bench unchanged (77.1-77.8 M/s either way).
 static bool prep_fused() {
