@@ -183,7 +183,8 @@ def test_verify_many_equals_single_fake(fake):
 
 def test_verify_many_equals_single_fake_large(fake):
     """Large enough (≈15k entries) for the multi-threaded packing and the
-    shared-commit dedup slots of tmv_verify_commits."""
+    shared-commit dedup slots of tmv_verify_commits, and for its pipelined
+    slices (3000 jobs = 6 slices of 500 on two threads, TMV_HOST_SLICE)."""
     jobs = F.random_jobs("fake", 3000, seed=9)
     many = F.fake_verify_commits(fake, jobs)
     single = [F.single_result(fake, jb) for jb in jobs]
@@ -191,9 +192,11 @@ def test_verify_many_equals_single_fake_large(fake):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scheme", ["ed25519", "sr25519"])
-def test_verify_many_equals_single_gpu(ctx, scheme):
-    jobs = F.random_jobs(scheme, 80, seed=6)
+@pytest.mark.parametrize("scheme,n", [("ed25519", 80), ("sr25519", 80), ("ed25519", 1100)])
+def test_verify_many_equals_single_gpu(ctx, scheme, n):
+    """1,100 jobs: three pipelined slices (TMV_HOST_SLICE), two engine calls
+    in flight from two threads."""
+    jobs = F.random_jobs(scheme, n, seed=6)
     g = F.GpuBackend(ctx, scheme)
     many = H.verify_commits(ctx, jobs)
     single = [F.single_result(g, jb) for jb in jobs]

@@ -121,7 +121,11 @@ pinned_sig = torch.from_numpy(hb.sig.copy()).pin_memory().numpy()
 ctx.metrics_reset()
 ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, hb.pk, pinned_sig, hb.msg, hb.off)
 assert np.array_equal(st.astype(np.uint8), want)
-assert ctx.metrics()["h2d_bytes"] == hb.pk.nbytes + hb.sig.nbytes + hb.msg.nbytes + hb.off.nbytes
+# every byte crosses once, except the one offset two streamed parts share
+# (each part carries its own [a, b] offsets; at most 64 parts)
+payload = hb.pk.nbytes + hb.sig.nbytes + hb.msg.nbytes + hb.off.nbytes
+h2d = ctx.metrics()["h2d_bytes"]
+assert payload <= h2d <= payload + 4 * 64, (h2d, payload)
 print("ok")
 """
 
