@@ -27,12 +27,14 @@
 
 namespace tmh_internal {
 
+// Default 2,048 jobs: slicing only calls of >= 4,096 jobs keeps every
+// slice's engine call large (a C4 window of 1,200 jobs cut into three ran
+// its GPU work at half the rate: 35k-signature key-merged launches are
+// latency-bound, and the engine serialises calls per device).  Read on every
+// call (tests change it).
 uint32_t host_slice_jobs() {
-  static const uint32_t v = [] {
-    const char *e = std::getenv("TMV_HOST_SLICE");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 512u;
-  }();
-  return v;
+  const char *e = std::getenv("TMV_HOST_SLICE");
+  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
 }
 
 namespace {

@@ -66,6 +66,35 @@ struct alignas(16) niels_pt {
   int32_t pad[2];
 };
 
+// Points of the batch equation are stored as (+P, -P) pairs (pts[2 i] and
+// pts[2 i + 1] for point i), so a sorted entry's (index << 1 | negate) word
+// is its slot and the bucket sums load the signed point as it is -- no
+// per-entry swap and negation.  -DTMV_NIELS_PAIR=0: one slot per point.
+#ifndef TMV_NIELS_PAIR
+#define TMV_NIELS_PAIR 0
+#endif
+constexpr uint32_t kNielsPer = TMV_NIELS_PAIR ? 2 : 1;
+
+// -P of a Niels point: (y - x, y + x, -2dxy)
+TMV_HD niels_pt niels_negate(const niels_pt &p) {
+  niels_pt r;
+  r.ypx = p.ymx;
+  r.ymx = p.ypx;
+  fe_neg(r.xy2d, p.xy2d);
+  r.pad[0] = r.pad[1] = 0;
+  return r;
+}
+
+// Store point i's Niels form (and, paired, its negation).
+TMV_HD void niels_store(niels_pt *pts, uint64_t i, const niels_pt &p) {
+  if (kNielsPer == 2) {
+    pts[2 * i] = p;
+    pts[2 * i + 1] = niels_negate(p);
+  } else {
+    pts[i] = p;
+  }
+}
+
 struct MsmParams {
   uint32_t m_log2;   // group size = 1 << m_log2 (>= 5, so a 16-signature quad block never spans groups)
   uint32_t c;        // window bits
@@ -135,7 +164,7 @@ struct MsmParams {
 
 // Device workspace of the batch check (all per launch stream).
 struct MsmWork {
-  niels_pt *pts;       // 2n+1: [2e] = -R_e, [2e+1] = -A_e, [2n] = B
+  niels_pt *pts;       // points 2n+1: [2e] = -R_e, [2e+1] = -A_e, [2n] = B; kNielsPer slots each
   uint32_t *ent_pt;    // groups x cap: point index << 1 | negate
   uint32_t *ent_bk;    // groups x cap: global bucket id, kMsmEmpty for padding
   uint32_t *bk_start;  // groups x W x H: first sorted slot of the bucket
@@ -177,7 +206,7 @@ struct MsmWork {
   static size_t bytes(uint32_t n, const MsmParams &p) {
     const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
     const size_t chunks = ent / p.L;
-    size_t b = (2ull * n + 1) * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
+    size_t b = (2ull * n + 1) * kNielsPer * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
                2 * chunks * sizeof(ge_p3) + 4 * chunks + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 2 * G +
                17 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
@@ -192,7 +221,7 @@ struct MsmWork {
     const size_t chunks = ent / p.L;
     MsmWork w;
     size_t o = 0;
-    w.pts = reinterpret_cast<niels_pt *>(b + o); o = up(o + (2ull * n + 1) * sizeof(niels_pt));
+    w.pts = reinterpret_cast<niels_pt *>(b + o); o = up(o + (2ull * n + 1) * kNielsPer * sizeof(niels_pt));
     w.ent_pt = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * ent);
     w.ent_bk = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * ent);
     w.bk_start = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * bk);

@@ -201,7 +201,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     bp.ypx = btab_q[1];
     bp.xy2d = btab_q[2];
     bp.pad[0] = bp.pad[1] = 0;
-    mw.pts[mw.n_pts] = bp;
+    niels_store(mw.pts, mw.n_pts, bp);
     if (mw.fail_count) *mw.fail_count = 0;  // k_msm_horner appends the failing groups
   }
   if (e0 >= cnt) return;  // block-uniform
@@ -379,32 +379,62 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   }
   __syncthreads();
 
-  // pass 2: scatter (point index << 1 | negate); stored points are -R, -A, +B
+  // pass 2: scatter (point index << 1 | negate); stored points are -R, -A, +B.
+  // Window by window: a window's H buckets are one contiguous slot range, so
+  // its entries are placed in LDS first and then stored in order -- coalesced
+  // lines, where scattering each entry straight to memory left partly
+  // written lines behind (3.4x the sorted bytes in WRITE_SIZE).
   uint32_t *ent_pt = mw.ent_pt + gbase;
   uint32_t *ent_bk = mw.ent_bk + gbase;
+  const uint32_t wcap = 2 * p.m() + 1;  // entries one window can hold: m R + m A digits + B
+  uint32_t *st_pt = scan + BS + 1, *st_bk = st_pt + wcap;
+  int cz[R], cw[R], cb = 0;  // per-scalar digit carries, window to window
 #pragma unroll
-  for (int r = 0; r < R; r++) {
-    if (!live[r]) continue;
-    const uint32_t e = e0 + tid + r * BS;
-    for_each_digit<ZW>(z[r], WRz, p, [&](uint32_t bk, bool neg) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);  // < cap: checked above
-      ent_pt[pos] = ((KM ? e : 2 * e) << 1) | (neg ? 1u : 0u);
-      ent_bk[pos] = bbase + bk;
-    });
-    if (!KM) for_each_digit<8>(wv[r], p.W, p, [&](uint32_t bk, bool neg) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);  // < cap: checked above
-      ent_pt[pos] = ((2 * e + 1) << 1) | (neg ? 1u : 0u);
-      ent_bk[pos] = bbase + bk;
-    });
+  for (int r = 0; r < R; r++) cz[r] = cw[r] = 0;
+  const uint32_t total = scan[BS];
+  for (uint32_t w = 0; w < p.W; w++) {
+    const uint32_t wbeg = hist[p.bucket(w, 0)];
+    const uint32_t wend = w + 1 < p.W ? hist[p.bucket(w + 1, 0)] : total;
+    __syncthreads();  // bounds read (and the previous window stored) before the cursors move
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (!live[r]) continue;
+      const uint32_t e = e0 + tid + r * BS;
+      if (w < WRz) {
+        const int d = window_digit<ZW>(z[r], w, p.c, w + 1 == WRz, cz[r]);
+        if (d != 0) {
+          const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
+          const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;  // < cap: checked above
+          st_pt[pos] = ((KM ? e : 2 * e) << 1) | (d < 0 ? 1u : 0u);
+          st_bk[pos] = bbase + bk;
+        }
+      }
+      if (!KM) {
+        const int d = window_digit<8>(wv[r], w, p.c, w + 1 == p.W, cw[r]);
+        if (d != 0) {
+          const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
+          const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;
+          st_pt[pos] = ((2 * e + 1) << 1) | (d < 0 ? 1u : 0u);
+          st_bk[pos] = bbase + bk;
+        }
+      }
+    }
+    if (!KM && tid == 0) {
+      const int d = window_digit<8>(bsc, w, p.c, w + 1 == p.W, cb);
+      if (d != 0) {
+        const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
+        const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;
+        st_pt[pos] = (mw.n_pts << 1) | (d < 0 ? 1u : 0u);
+        st_bk[pos] = bbase + bk;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < wend - wbeg; i += BS) {
+      ent_pt[wbeg + i] = st_pt[i];
+      ent_bk[wbeg + i] = st_bk[i];
+    }
   }
-  if (!KM && tid == 0) {
-    for_each_digit<8>(bsc, p.W, p, [&](uint32_t bk, bool neg) {
-      const uint32_t pos = atomicAdd(&hist[bk], 1u);  // < cap: checked above
-      ent_pt[pos] = (mw.n_pts << 1) | (neg ? 1u : 0u);
-      ent_bk[pos] = bbase + bk;
-    });
-  }
-  for (uint32_t t = scan[BS] + tid; t < p.cap; t += BS) ent_bk[t] = kMsmEmpty;
+  for (uint32_t t = total + tid; t < p.cap; t += BS) ent_bk[t] = kMsmEmpty;
 }
 
 // One lane per chunk of L sorted entries: sums each run of equal
@@ -468,7 +498,10 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   // every lane's first run starts at entry 0: take that point as the
   // accumulator (one multiply) instead of adding it to the identity (seven)
   ge_p3 acc;
-  {
+  if (kNielsPer == 2) {  // the signed point's own slot
+    const niels_pt P = mw.pts[pt[0]];
+    niels_to_p3(acc, P.ypx, P.ymx);
+  } else {
     const niels_pt P = mw.pts[pt[0] >> 1];
     const bool neg = pt[0] & 1;
     niels_to_p3(acc, neg ? P.ymx : P.ypx, neg ? P.ypx : P.ymx);
@@ -486,13 +519,20 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       cur = bk[q];
       rs = base + q;
     }
-    const niels_pt P = mw.pts[pt[q] >> 1];
     ge_precomp np;
-    const bool neg = pt[q] & 1;
-    np.ypx = neg ? P.ymx : P.ypx;
-    np.ymx = neg ? P.ypx : P.ymx;
-    fe_neg(np.xy2d, P.xy2d);
-    fe_cmov(np.xy2d, P.xy2d, !neg);
+    if (kNielsPer == 2) {
+      const niels_pt P = mw.pts[pt[q]];
+      np.ypx = P.ypx;
+      np.ymx = P.ymx;
+      np.xy2d = P.xy2d;
+    } else {
+      const niels_pt P = mw.pts[pt[q] >> 1];
+      const bool neg = pt[q] & 1;
+      np.ypx = neg ? P.ymx : P.ypx;
+      np.ymx = neg ? P.ypx : P.ymx;
+      fe_neg(np.xy2d, P.xy2d);
+      fe_cmov(np.xy2d, P.xy2d, !neg);
+    }
     ge_p1p1 r;
     ge_madd(r, acc, np);
     ge_p1p1_to_p3(acc, r);
@@ -878,7 +918,7 @@ k_msm_subcheck(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx
     const uint32_t e = e0 + jj;
 #pragma unroll 1
     for (int ra = 0; ra < 2; ra++) {
-      const niels_pt &np = mw.pts[2ull * e + ra];
+      const niels_pt &np = mw.pts[(2ull * e + ra) * kNielsPer];
       fe E, H, P;
       fe_sub(E, np.ypx, np.ymx);
       fe_add(H, np.ypx, np.ymx);
@@ -964,6 +1004,12 @@ k_msm_subcheck(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx
     ok = quad::is_identity_times8(acc);
   }
   if (live && c == 0) mw.sub_ok[e0 >> kSubGroupLog2] = ok ? 1 : 0;
+}
+
+// Dynamic LDS of k_msm_sort: the bucket counters / cursors, the scalar
+// reduction, the scan, and one window's staged entries (point, bucket).
+static size_t sort_smem(const MsmParams &p, uint32_t bs) {
+  return ((size_t)p.W * p.H + bs * 9 + bs + 1 + 2 * (2 * p.m() + 1)) * sizeof(uint32_t);
 }
 
 // Bucket sums, window parts and window sums (shared by both forms).
@@ -1081,7 +1127,7 @@ static Ed25519Work work_view(Ed25519Work w, uint64_t e0) {
 }
 static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0) {
   const uint64_t e0 = g0 << p.m_log2, wh = (uint64_t)p.W * p.H;
-  mw.pts += 2 * e0;
+  mw.pts += 2 * e0 * kNielsPer;
   mw.n_pts = (uint32_t)(2ull * n - 2 * e0);  // B keeps the launch's slot 2n
   mw.ent_pt += g0 * p.cap;
   mw.ent_bk += g0 * p.cap;
@@ -1112,11 +1158,11 @@ static hipError_t launch_sort_buckets(const uint8_t *sig, const uint32_t *idx, c
   // groups of <= 256 entries: 64-thread workgroups (4 entries per thread at
   // most), so a 64-entry group no longer parks 192 idle lanes
   if (p.m_log2 <= 8 && sort_block() == 64) {
-    const size_t smem = ((size_t)p.W * p.H + 64 * 9 + 64 + 1) * sizeof(uint32_t);
+    const size_t smem = sort_smem(p, 64);
     hipLaunchKernelGGL((k_msm_sort<SR, false, 64>), dim3(p.groups), dim3(64), smem, stream, sig, idx, count_ptr, n,
                        w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr, e_base);
   } else {
-    const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+    const size_t smem = sort_smem(p, kMsmSortBlock);
     hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx,
                        count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr,
                        e_base);
@@ -1153,11 +1199,11 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     // second MSM over the failing groups (slot f = f-th failing group), then
     // the search, then one-by-one verification of the listed entries only
     if (p.m_log2 <= 8 && sort_block() == 64) {
-      const size_t smem = ((size_t)p.W * p.H + 64 * 9 + 64 + 1) * sizeof(uint32_t);
+      const size_t smem = sort_smem(p, 64);
       hipLaunchKernelGGL((k_msm_sort<SR, false, 64, true>), dim3(p.groups), dim3(64), smem, stream, sig, idx,
                          count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
     } else {
-      const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+      const size_t smem = sort_smem(p, kMsmSortBlock);
       hipLaunchKernelGGL((k_msm_sort<SR, false, kMsmSortBlock, true>), dim3(p.groups), dim3(kMsmSortBlock), smem,
                          stream, sig, idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr,
                          0u);
@@ -1215,7 +1261,7 @@ hipError_t launch_batch_check_part(bool sr, const uint8_t *pk, const uint8_t *si
   const uint64_t E = e0;
   if (prep_only) {  // the sort and bucket stages run later over the whole launch
     Ed25519Work v = work_view(w, E);
-    v.niels = mw.pts + 2 * E;
+    v.niels = mw.pts + 2 * E * kNielsPer;
     if (sr) return launch_prep<true>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, prefix,
                                      v, aligned, stream);
     return launch_prep<false>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, prefix, v,
@@ -1325,7 +1371,7 @@ static hipError_t launch_km(const uint8_t *pk, const uint8_t *sig, const uint8_t
   w.niels = mw.pts;
   hipError_t e = launch_prep_cached<SR>(pk, sig, msg, msg_off, runs.order, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
-  const size_t smem = ((size_t)p.W * p.H + kMsmSortBlock * 9 + kMsmSortBlock + 1) * sizeof(uint32_t);
+  const size_t smem = sort_smem(p, kMsmSortBlock);
   hipLaunchKernelGGL((k_msm_sort<SR, true>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, runs.order, nullptr,
                      n, w, mw, p, seed, nullptr, aligned, key_slot, kt.ok, nullptr, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -219,7 +219,8 @@ struct Device {
   // different caller streams run concurrently (the context's own stream is
   // one of them)
   std::unordered_map<hipStream_t, std::unique_ptr<Workspace>> ws;
-  hipEvent_t work_done = nullptr;        // orders key-build staging reuse
+  hipEvent_t work_done = nullptr;        // after the latest k_key_build (cumulative: each build waits on the last)
+  hipEvent_t kbuild_copied = nullptr;    // the latest build's keys left the pinned staging
   tmv::fe *d_bcomb = nullptr;            // 32 x 128 CachedQ: (m+1) 256^j B (key-cached path)
   // expanded-key cache (device table + host LRU index)
   tmv::KeyTable kt{nullptr, nullptr};
@@ -724,6 +725,9 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     d.klru.splice(d.klru.begin(), d.klru, d.kpos[slot]);
     d.khits++;
   }
+  // tables built by earlier batches (possibly on other streams, not waited
+  // for on the host) are complete before this batch's kernels read them
+  (void)hipStreamWaitEvent(s, d.work_done, 0);
   if (n_miss == 0) return 0;
   // new keys may evict slots: let chunks still in flight on other lanes finish
   for (HostLane &l : d.lane)
@@ -779,6 +783,9 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   const uint32_t m = (uint32_t)miss_idx.size();
   if (m) {
     const size_t bytes = 32ull * m + 4ull * m + 64;
+    // the previous build's copy must have left the staging before it is
+    // rewritten (or regrown); its kernel need not have finished
+    if (d.kbuild_copied && (e = wait_event(d, d.kbuild_copied)) != hipSuccess) return wait_rc(e);
     if ((e = d.h_kbuild.ensure(bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
     if (bytes > d.d_kbuild.cap) {
       if ((e = wait_event(d, d.work_done)) != hipSuccess) return wait_rc(e);
@@ -793,14 +800,21 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
       set_error("hipMemcpyAsync(keys)", e);
       return TMV_ERR_LAUNCH;
     }
+    if (!d.kbuild_copied && (e = hipEventCreateWithFlags(&d.kbuild_copied, hipEventDisableTiming)) != hipSuccess) {
+      d.kbuild_copied = nullptr;
+      set_error("hipEventCreate", e);
+      return TMV_ERR_NO_DEVICE;
+    }
+    (void)hipEventRecord(d.kbuild_copied, s);
     uint8_t *dk = static_cast<uint8_t *>(d.d_kbuild.ptr);
     if ((e = tmv::launch_key_build(sr, dk, reinterpret_cast<uint32_t *>(dk + soff), m, d.kt, s)) != hipSuccess) {
       set_error("k_key_build launch", e);
       return TMV_ERR_LAUNCH;
     }
-    // the pinned staging is reused by the next build: wait for this copy
+    // no host wait: this stream's kernels follow the build in order, later
+    // batches on other streams wait on work_done (above), the next build
+    // waits for kbuild_copied before reusing the staging
     (void)hipEventRecord(d.work_done, s);
-    if ((e = wait_event(d, d.work_done)) != hipSuccess) return wait_rc(e);
   }
   return 0;
 }
@@ -1108,6 +1122,7 @@ void tmv_close(tmv_ctx *ctx) {
       if (ks.helper) (void)hipStreamDestroy(ks.helper);
     }
     d->ws.clear();
+    if (d->work_done) (void)hipEventSynchronize(d->work_done);  // the last key build (not waited for on the host)
     d->d_kbuild.release();
     d->h_kbuild.release();
     if (d->kt.tab) (void)hipFree(d->kt.tab);
@@ -1116,6 +1131,7 @@ void tmv_close(tmv_ctx *ctx) {
     if (d->d_prefix) (void)hipFree(d->d_prefix);
     if (d->d_btab_q) (void)hipFree(d->d_btab_q);
     if (d->work_done) (void)hipEventDestroy(d->work_done);
+    if (d->kbuild_copied) (void)hipEventDestroy(d->kbuild_copied);
     if (d->d_btable) (void)hipFree(d->d_btable);
     for (int l = 1; l < kLanes; l++)
       if (d->lane[l].stream) (void)hipStreamDestroy(d->lane[l].stream);

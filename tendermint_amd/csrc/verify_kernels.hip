@@ -86,7 +86,7 @@ __device__ __forceinline__ void prep_decode_block(uint32_t bx, const uint8_t *__
     fe_add(t, P.Y, P.X); fe_carry(np.ymx, t);
     fe_mul(t, P.T, consts::d2()); fe_neg(np.xy2d, t);
     np.pad[0] = np.pad[1] = 0;
-    w.niels[2ull * e + (isA ? 1 : 0)] = np;
+    niels_store(w.niels, 2ull * e + (isA ? 1 : 0), np);
   }
   fe *dst = (isA ? w.negA : w.Rc) + 4ull * e;
   if (isA || SR) {
@@ -491,7 +491,7 @@ k_prep_cached(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, c
     fe_add(t, P.Y, P.X); fe_carry(np.ymx, t);
     fe_mul(t, P.T, consts::d2()); fe_neg(np.xy2d, t);
     np.pad[0] = np.pad[1] = 0;
-    w.niels[e] = np;
+    niels_store(w.niels, e, np);
   }
   fe *dst = w.Rc + 4ull * e;
   if (SR) {

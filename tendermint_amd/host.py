@@ -410,10 +410,12 @@ class PreparedJobs:
 
     def decode(self) -> List[Optional[str]]:
         out = []
+        buf = None  # one copy of the error buffer (ctypes' .raw copies all of it on every access)
         for j in range(self.n):
             if self.results[j]:
-                raw = self.errs.raw[j * self.stride:(j + 1) * self.stride]
-                out.append(raw.split(b"\0", 1)[0].decode())
+                if buf is None:
+                    buf = self.errs.raw
+                out.append(buf[j * self.stride:(j + 1) * self.stride].split(b"\0", 1)[0].decode())
             else:
                 out.append(None)
         return out
@@ -610,10 +612,15 @@ class PreparedLightJobs:
 
     def decode(self) -> List[Tuple[int, Optional[str]]]:
         out = []
+        buf = None  # one copy of the error buffer (ctypes' .raw copies all of it on every access)
         for j in range(self.n):
             kind = self.results[j]
-            raw = self.errs.raw[j * self.stride:(j + 1) * self.stride].split(b"\0", 1)[0].decode()
-            out.append((kind, raw if kind != LIGHT_OK else None))
+            if kind == LIGHT_OK:
+                out.append((kind, None))
+                continue
+            if buf is None:
+                buf = self.errs.raw
+            out.append((kind, buf[j * self.stride:(j + 1) * self.stride].split(b"\0", 1)[0].decode()))
         return out
 
 

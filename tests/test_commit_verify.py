@@ -181,10 +181,13 @@ def test_verify_many_equals_single_fake(fake):
     assert sum(r is None for r in many) > 20 and sum(r is not None for r in many) > 20
 
 
-def test_verify_many_equals_single_fake_large(fake):
+@pytest.mark.parametrize("slice_jobs", ["0", "500"])
+def test_verify_many_equals_single_fake_large(fake, slice_jobs, monkeypatch):
     """Large enough (≈15k entries) for the multi-threaded packing and the
-    shared-commit dedup slots of tmv_verify_commits, and for its pipelined
-    slices (3000 jobs = 6 slices of 500 on two threads, TMV_HOST_SLICE)."""
+    shared-commit dedup slots of tmv_verify_commits; in one pass and in
+    pipelined slices (3000 jobs = 6 slices of 500 taken by two threads,
+    TMV_HOST_SLICE)."""
+    monkeypatch.setenv("TMV_HOST_SLICE", slice_jobs)
     jobs = F.random_jobs("fake", 3000, seed=9)
     many = F.fake_verify_commits(fake, jobs)
     single = [F.single_result(fake, jb) for jb in jobs]
@@ -193,9 +196,10 @@ def test_verify_many_equals_single_fake_large(fake):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scheme,n", [("ed25519", 80), ("sr25519", 80), ("ed25519", 1100)])
-def test_verify_many_equals_single_gpu(ctx, scheme, n):
-    """1,100 jobs: three pipelined slices (TMV_HOST_SLICE), two engine calls
-    in flight from two threads."""
+def test_verify_many_equals_single_gpu(ctx, scheme, n, monkeypatch):
+    """1,100 jobs in three pipelined slices (TMV_HOST_SLICE=400): two host
+    threads, engine calls from both."""
+    monkeypatch.setenv("TMV_HOST_SLICE", "400")
     jobs = F.random_jobs(scheme, n, seed=6)
     g = F.GpuBackend(ctx, scheme)
     many = H.verify_commits(ctx, jobs)

@@ -248,9 +248,12 @@ def test_host_layer_mutations_match_oracle(fake_real):
     assert len(seen) >= 15, seen
 
 
-def test_host_layer_many_equals_single(fake_real):
+@pytest.mark.parametrize("slice_jobs", ["0", "7"])
+def test_host_layer_many_equals_single(fake_real, slice_jobs, monkeypatch):
     """A window of jobs in one tmv_light_verify_many call (shared headers and
-    sets, one signature batch) returns what each job returns alone."""
+    sets, one signature batch) returns what each job returns alone -- in one
+    pass and in pipelined slices of 7 jobs on two threads (TMV_HOST_SLICE)."""
+    monkeypatch.setenv("TMV_HOST_SLICE", slice_jobs)
     from tendermint_amd import host as H
     jobs = []
     for c in HOST_CASES:
