@@ -637,6 +637,25 @@ def main():
         ctx.kernel_timing(False)
         ktimes_alone.update({k: ctx.kernel_timing_read(k) for k in TIMED_KERNELS})
         extras["launch_alone_ms"] = round(statistics.median(alone), 4)
+        # sustained: the timed region's pattern (F launches in flight) for
+        # ~TMV_BENCH_SUSTAIN_S seconds -- a steadier rate than K steps, and a
+        # GPU busy long enough for an outside utilisation sampler to see
+        sustain_s = float(os.environ.get("TMV_BENCH_SUSTAIN_S", "3"))
+        if sustain_s > 0:
+            sync(dev)
+            t1, nl = time.perf_counter(), 0
+            while True:
+                for _ in range(4 * F):
+                    launch(nl, (nl * K) % R, K, gather=False)
+                    nl += 1
+                sync(dev)
+                if time.perf_counter() - t1 >= sustain_s:
+                    break
+            dt = time.perf_counter() - t1
+            extras["sustained_verifies_per_s"] = round(nl * K * n / dt, 1)
+            extras["sustained_seconds"] = round(dt, 3)
+            extras["sustained_note"] = (f"{nl} launches of {K} C2 batches, {F} in flight, one device sync per "
+                                        f"{4 * F} launches (rank 0, after the timed region; not the headline value)")
         # single-batch latency (one 10k batch per launch, one at a time), with
         # the runtime's own choice for a batch this size (flags 0: per entry
         # below TMV_MSM_MIN) and through the batch equation

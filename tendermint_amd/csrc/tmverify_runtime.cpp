@@ -219,7 +219,7 @@ struct Device {
   // different caller streams run concurrently (the context's own stream is
   // one of them)
   std::unordered_map<hipStream_t, std::unique_ptr<Workspace>> ws;
-  hipEvent_t work_done = nullptr;        // after the latest k_key_build (cumulative: each build waits on the last)
+  hipEvent_t work_done = nullptr;        // after the latest key-table build (cumulative: each build waits on the last)
   hipEvent_t kbuild_copied = nullptr;    // the latest build's keys left the pinned staging
   tmv::fe *d_bcomb = nullptr;            // 32 x 128 CachedQ: (m+1) 256^j B (key-cached path)
   // expanded-key cache (device table + host LRU index)
@@ -782,11 +782,14 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   }
   const uint32_t m = (uint32_t)miss_idx.size();
   if (m) {
-    const size_t bytes = 32ull * m + 4ull * m + 64;
+    // keys, slots, then the row-base scratch of the two-launch build
+    const size_t soff = (32ull * m + 15) & ~size_t(15), boff = (soff + 4ull * m + 15) & ~size_t(15);
+    const size_t bytes = boff + tmv::key_build_scratch(m);
+    const size_t hbytes = soff + 4ull * m;
     // the previous build's copy must have left the staging before it is
     // rewritten (or regrown); its kernel need not have finished
     if (d.kbuild_copied && (e = wait_event(d, d.kbuild_copied)) != hipSuccess) return wait_rc(e);
-    if ((e = d.h_kbuild.ensure(bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+    if ((e = d.h_kbuild.ensure(hbytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
     if (bytes > d.d_kbuild.cap) {
       if ((e = wait_event(d, d.work_done)) != hipSuccess) return wait_rc(e);
       if ((e = d.d_kbuild.ensure(bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
@@ -794,7 +797,6 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     (void)hipStreamWaitEvent(s, d.work_done, 0);
     uint8_t *h = static_cast<uint8_t *>(d.h_kbuild.ptr);
     for (uint32_t t = 0; t < m; t++) std::memcpy(h + 32ull * t, pk + 32ull * miss_idx[t], 32);
-    const size_t soff = (32ull * m + 15) & ~size_t(15);
     std::memcpy(h + soff, miss_slot.data(), 4ull * m);
     if ((e = hipMemcpyAsync(d.d_kbuild.ptr, h, soff + 4ull * m, hipMemcpyHostToDevice, s)) != hipSuccess) {
       set_error("hipMemcpyAsync(keys)", e);
@@ -807,8 +809,9 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     }
     (void)hipEventRecord(d.kbuild_copied, s);
     uint8_t *dk = static_cast<uint8_t *>(d.d_kbuild.ptr);
-    if ((e = tmv::launch_key_build(sr, dk, reinterpret_cast<uint32_t *>(dk + soff), m, d.kt, s)) != hipSuccess) {
-      set_error("k_key_build launch", e);
+    if ((e = tmv::launch_key_build(sr, dk, reinterpret_cast<uint32_t *>(dk + soff), m, d.kt,
+                                   reinterpret_cast<tmv::fe *>(dk + boff), s)) != hipSuccess) {
+      set_error("key-table build launch", e);
       return TMV_ERR_LAUNCH;
     }
     // no host wait: this stream's kernels follow the build in order, later

@@ -47,8 +47,10 @@ struct KeyTable {
   static size_t bytes_per_key() { return (size_t)kKeyRowsEntries * 4 * sizeof(fe); }
 };
 
+// bases: scratch of key_build_scratch(m) bytes (the row bases, P3Q)
 hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
-                            hipStream_t stream);
+                            fe *bases, hipStream_t stream);
+inline size_t key_build_scratch(uint32_t m) { return (size_t)m * 64 * 4 * sizeof(fe); }
 // fused_max: batches up to this size use the one-kernel latency form
 // (k_verify_cached_fused), larger ones k_prep_cached + k_verify_comb.
 hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,

@@ -401,11 +401,19 @@ __global__ void k_partition(const uint8_t *__restrict__ kind, uint32_t n, uint32
 // of -A: row i holds (m+1) 16^i (-A), m < 8, in CachedQ layout (80 KB/key),
 // so [k](-A) needs 64 table additions and no doublings.
 
-// One quad per key: decode (every lane redundantly), then 64 rows of
-// multiples with 4 doublings between rows.
+// Key tables are built in two launches, so a batch of new keys (a light
+// client's window brings one per height) is not one long chain per key:
+//   k_key_bases  one quad per key: decode (every lane redundantly), then the
+//                64 row bases 16^i (-A) -- the 252-doubling chain, each base
+//                to a P3Q scratch and its 1x entry to the table;
+//   k_key_rows   one quad per (key, row): multiples 2..8 of the row base
+//                (one doubling, six additions).
+// One quad per key doing both took a ~700-operation chain (64 rows x (1
+// doubling + 6 additions + 4 doublings)).
 template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
-k_key_build(const uint8_t *__restrict__ keys, const uint32_t *__restrict__ slots, uint32_t m, KeyTable kt) {
+k_key_bases(const uint8_t *__restrict__ keys, const uint32_t *__restrict__ slots, uint32_t m, KeyTable kt,
+            fe *__restrict__ bases) {
   const int c = threadIdx.x & 3;
   const uint32_t raw = blockIdx.x * kQuadSigs + (threadIdx.x >> 2);
   const bool live = raw < m;
@@ -423,19 +431,13 @@ k_key_build(const uint8_t *__restrict__ keys, const uint32_t *__restrict__ slots
   else fe_neg(P, A.T);
   const uint32_t slot = slots[e];
   fe *row = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
-  fe r, Pm, Q, Q0;
+  fe *base = bases + (size_t)e * 64 * 4;
+  fe r, Q0;
   for (int i = 0; i < 64; i++) {
     quad::to_cached(Q0, P);
-    if (live) row[(i * 8 + 0) * 4 + c] = Q0;
-    quad::dbl(r, P);
-    quad::p1p1_to_p3(Pm, r);
-    quad::to_cached(Q, Pm);
-    if (live) row[(i * 8 + 1) * 4 + c] = Q;
-    for (int t = 2; t < 8; t++) {
-      quad::add(r, Pm, Q0);
-      quad::p1p1_to_p3(Pm, r);
-      quad::to_cached(Q, Pm);
-      if (live) row[(i * 8 + t) * 4 + c] = Q;
+    if (live) {
+      base[i * 4 + c] = P;
+      row[(i * 8 + 0) * 4 + c] = Q0;
     }
     if (i < 63) {
 #pragma unroll
@@ -446,6 +448,29 @@ k_key_build(const uint8_t *__restrict__ keys, const uint32_t *__restrict__ slots
     }
   }
   if (live && c == 0) kt.ok[slot] = ok ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(kQuadBlock)
+k_key_rows(const uint32_t *__restrict__ slots, uint32_t m, KeyTable kt, const fe *__restrict__ bases) {
+  const int c = threadIdx.x & 3;
+  const uint32_t raw = blockIdx.x * kQuadSigs + (threadIdx.x >> 2);  // (key, row)
+  const bool live = raw < 64 * m;
+  const uint32_t q = live ? raw : 64 * m - 1;
+  const uint32_t e = q >> 6, i = q & 63;
+  const fe P = bases[((size_t)e * 64 + i) * 4 + c];
+  fe *row = kt.tab + (size_t)slots[e] * kKeyRowsEntries * 4 + (size_t)i * 8 * 4;
+  fe r, Pm, Q, Q0;
+  quad::to_cached(Q0, P);
+  quad::dbl(r, P);
+  quad::p1p1_to_p3(Pm, r);
+  quad::to_cached(Q, Pm);
+  if (live) row[1 * 4 + c] = Q;
+  for (int t = 2; t < 8; t++) {
+    quad::add(r, Pm, Q0);
+    quad::p1p1_to_p3(Pm, r);
+    quad::to_cached(Q, Pm);
+    if (live) row[t * 4 + c] = Q;
+  }
 }
 
 // Lanes [0, m) decode R, [m, 2m) compute the challenge (SHA-512 or merlin).
@@ -715,11 +740,15 @@ k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict_
 }
 
 hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
-                            hipStream_t stream) {
+                            fe *bases, hipStream_t stream) {
   if (m == 0) return hipSuccess;
   const uint32_t blocks = (m + kQuadSigs - 1) / kQuadSigs;
-  if (sr) hipLaunchKernelGGL(k_key_build<true>, dim3(blocks), dim3(kQuadBlock), 0, stream, keys, slots, m, kt);
-  else hipLaunchKernelGGL(k_key_build<false>, dim3(blocks), dim3(kQuadBlock), 0, stream, keys, slots, m, kt);
+  if (sr) hipLaunchKernelGGL(k_key_bases<true>, dim3(blocks), dim3(kQuadBlock), 0, stream, keys, slots, m, kt, bases);
+  else hipLaunchKernelGGL(k_key_bases<false>, dim3(blocks), dim3(kQuadBlock), 0, stream, keys, slots, m, kt, bases);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t rblocks = (uint32_t)((64ull * m + kQuadSigs - 1) / kQuadSigs);
+  hipLaunchKernelGGL(k_key_rows, dim3(rblocks), dim3(kQuadBlock), 0, stream, slots, m, kt, (const fe *)bases);
   return hipGetLastError();
 }
 
