@@ -1405,7 +1405,8 @@ hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, co
 hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                     const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
                                     Ed25519Work w_ed, Ed25519Work w_sr, MsmWork m_ed, MsmWork m_sr,
-                                    const MsmParams &p, const MsmSeed &seed_ed, const MsmSeed &seed_sr,
+                                    const MsmParams &p, const MsmParams &p_sr, const MsmSeed &seed_ed,
+                                    const MsmSeed &seed_sr,
                                     uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, int8_t *status,
                                     hipStream_t stream, const KindStreams *ks) {
   if (n == 0) return hipSuccess;
@@ -1422,8 +1423,8 @@ hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, cons
     if ((e = hipStreamWaitEvent(ks->helper, ks->fork, 0)) != hipSuccess) return e;
     s_sr = ks->helper;
   }
-  e = launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p, seed_sr, out,
-                         s_sr);
+  e = launch_check<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, m_sr, p_sr, seed_sr,
+                         out, s_sr);
   if (e != hipSuccess) return e;
   e = launch_check<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, m_ed, p, seed_ed, out,
                           stream);

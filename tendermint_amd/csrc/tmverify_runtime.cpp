@@ -177,6 +177,7 @@ struct Workspace {
   const uint8_t *group_ok[2] = {nullptr, nullptr};
   const uint8_t *sub_ok[2] = {nullptr, nullptr};  // sub-group verdicts (k_msm_subcheck), if it ran
   uint32_t groups = 0, m_log2 = 0, n = 0;
+  uint32_t m_log2_sr = 0;  // mixed: the sr25519 half's group size (m_log2 is the ed25519 half's)
   const uint32_t *counts = nullptr;  // mixed launches: per-kind entry counts on the device
   const uint32_t *loc[2] = {nullptr, nullptr};  // located pass ran: its (slots, fb_count, found) words
 };
@@ -449,7 +450,8 @@ struct Layout {
 // these parameters and this randomness.
 struct LaunchOpts {
   bool batch_eq = false;
-  tmv::MsmParams p{};
+  tmv::MsmParams p{};      // single-kind launches; the ed25519 half of a mixed one
+  tmv::MsmParams p_sr{};   // the sr25519 half of a mixed launch
   tmv::MsmSeed seed[2]{};  // [kind]
 };
 
@@ -494,6 +496,11 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
   {
     std::lock_guard<std::mutex> lk(ctx->opt_mu);  // tmv_set_batch_options writes these
     o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged, ed_only, ctx->msm_sub);
+    // mixed launches: each kind's half its own group size -- ed25519 takes
+    // the located-fallback groups of 128 at the size ed25519-only launches
+    // do, sr25519 keeps 64 (msm_params); both stay the caller's when set
+    o.p_sr = o.p;
+    if (!merged && !ed_only) o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, false, true, ctx->msm_sub);
     fixed = ctx->fixed_seed;
     if (fixed) std::memcpy(key, ctx->seed, 32);
   }
@@ -525,7 +532,8 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
     uint32_t c[2];
     if (hipMemcpy(c, w.counts, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) return;
     for (int k = 0; k < 2; k++) {
-      live[k] = (c[k] + (1u << w.m_log2) - 1) >> w.m_log2;
+      const uint32_t ml = k ? w.m_log2_sr : w.m_log2;
+      live[k] = (c[k] + (1u << ml) - 1) >> ml;
       live_n[k] = c[k];
     }
   } else {
@@ -533,6 +541,7 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
   }
   for (int k = 0; k < 2; k++) {
     if (!w.group_ok[k] || !live[k]) continue;
+    const uint32_t mlog = k ? w.m_log2_sr : w.m_log2;
     std::vector<uint8_t> ok(live[k]);
     if (hipMemcpy(ok.data(), w.group_ok[k], live[k], hipMemcpyDeviceToHost) != hipSuccess) return;
     uint64_t failed = 0;
@@ -545,13 +554,13 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
       ctx->m_fallback += lc[1];
       ctx->m_located += lc[2];
     } else if (failed && !w.sub_ok[k]) {  // every entry of a failing group
-      const uint32_t m = 1u << w.m_log2, nk = w.counts ? live_n[k] : w.n;
+      const uint32_t m = 1u << mlog, nk = w.counts ? live_n[k] : w.n;
       for (uint32_t g = 0; g < live[k]; g++)
         if (!ok[g]) ctx->m_fallback += std::min<uint32_t>(m, nk - g * m);
     }
     if (!w.sub_ok[k] || !failed) continue;
     // sub-groups of the failing groups (the only ones k_msm_subcheck writes)
-    const uint32_t per = 1u << (w.m_log2 - tmv::kSubGroupLog2);
+    const uint32_t per = 1u << (mlog - tmv::kSubGroupLog2);
     std::vector<uint8_t> sub((size_t)live[k] * per);
     if (hipMemcpy(sub.data(), w.sub_ok[k], sub.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
     uint64_t sfail = 0;
@@ -825,7 +834,7 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
 // The workspace of stream s, big enough for n entries, with this launch
 // ordered after the previous user of that workspace.  Caller holds d.mu.
 static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s, int *rc,
-                               const tmv::MsmParams *mp = nullptr) {
+                               const tmv::MsmParams *mp = nullptr, const tmv::MsmParams *mp2 = nullptr) {
   auto &slot = d.ws[s];
   if (!slot) {
     slot = std::make_unique<Workspace>();
@@ -836,8 +845,9 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
   const size_t need = tmv::Ed25519Work::bytes(n);
   const size_t idx_need = 2ull * 4 * n + 64;
   const size_t msm_need = mp ? tmv::MsmWork::bytes(n, *mp) : 0;
+  const size_t msm2_need = mp ? tmv::MsmWork::bytes(n, mp2 ? *mp2 : *mp) : 0;
   if (need > w.work.cap || (mixed && (need > w.work2.cap || idx_need > w.idx.cap)) || msm_need > w.msm.cap ||
-      (mixed && msm_need > w.msm2.cap)) {
+      (mixed && msm2_need > w.msm2.cap)) {
     hipError_t e = wait_event(d, w.done);  // old buffers may still be in use
     if (e != hipSuccess) { *rc = wait_rc(e); return nullptr; }
     if ((e = w.work.ensure(need, false)) != hipSuccess) { set_error("hipMalloc(work)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
@@ -847,7 +857,7 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
     }
     if (msm_need) {
       if ((e = w.msm.ensure(msm_need, false)) != hipSuccess) { set_error("hipMalloc(msm)", e); *rc = TMV_ERR_NOMEM; return nullptr; }
-      if (mixed && (e = w.msm2.ensure(msm_need, false)) != hipSuccess) {
+      if (mixed && (e = w.msm2.ensure(msm2_need, false)) != hipSuccess) {
         set_error("hipMalloc(msm2)", e);
         *rc = TMV_ERR_NOMEM;
         return nullptr;
@@ -914,7 +924,7 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   ws->sub_ok[0] = o.p.sub ? mw.sub_ok : nullptr;
   ws->sub_ok[1] = nullptr;
   ws->groups = (n + o.p.m() - 1) >> o.p.m_log2;
-  ws->m_log2 = o.p.m_log2;
+  ws->m_log2 = ws->m_log2_sr = o.p.m_log2;
   ws->n = n;
   ws->counts = nullptr;
   ws->loc[0] = tmv::locate_enabled(n, o.p) ? mw.loc_count : nullptr;
@@ -939,7 +949,7 @@ static int launch_sr25519(Device &d, const LaunchOpts &o, const uint8_t *pk, con
 static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
   int rc;
-  Workspace *ws = reserve_work(d, n, true, s, &rc, o.batch_eq ? &o.p : nullptr);
+  Workspace *ws = reserve_work(d, n, true, s, &rc, o.batch_eq ? &o.p : nullptr, o.batch_eq ? &o.p_sr : nullptr);
   if (!ws) return rc;
   tmv::Ed25519Work w1 = tmv::Ed25519Work::carve(ws->work.ptr, n);
   tmv::Ed25519Work w2 = tmv::Ed25519Work::carve(ws->work2.ptr, n);
@@ -948,7 +958,7 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
   hipError_t e;
   if (o.batch_eq) {
     tmv::MsmWork m1 = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
-    tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p);
+    tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p_sr);
     read_env();
     tmv::KindStreams &ks = ws->kinds;
     if (g_mixed_two && !ks.helper) {
@@ -957,18 +967,19 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
       if (hipEventCreateWithFlags(&ks.join, hipEventDisableTiming) != hipSuccess) ks.join = nullptr;
     }
     e = tmv::launch_mixed_batch_check(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, m1, m2, o.p,
-                                      o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s,
+                                      o.p_sr, o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s,
                                       g_mixed_two ? &ks : nullptr);
     ws->group_ok[0] = m1.group_ok;
     ws->group_ok[1] = m2.group_ok;
     ws->sub_ok[0] = o.p.sub ? m1.sub_ok : nullptr;
-    ws->sub_ok[1] = o.p.sub ? m2.sub_ok : nullptr;
+    ws->sub_ok[1] = o.p_sr.sub ? m2.sub_ok : nullptr;
     ws->groups = o.p.groups;
-    ws->m_log2 = o.p.m_log2;
+    ws->m_log2 = ws->m_log2_sr = o.p.m_log2;
+    ws->m_log2_sr = o.p_sr.m_log2;
     ws->n = n;
     ws->counts = counts;
     ws->loc[0] = tmv::locate_enabled(n, o.p) ? m1.loc_count : nullptr;
-    ws->loc[1] = tmv::locate_enabled(n, o.p) ? m2.loc_count : nullptr;
+    ws->loc[1] = tmv::locate_enabled(n, o.p_sr) ? m2.loc_count : nullptr;
   } else {
     e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed, idx_sr,
                                  status, s);
@@ -1008,7 +1019,7 @@ static int launch_key_merged(Device &d, const LaunchOpts &o, bool sr, const uint
   ws->group_ok[1] = nullptr;
   ws->sub_ok[0] = ws->sub_ok[1] = nullptr;
   ws->groups = o.p.groups;
-  ws->m_log2 = o.p.m_log2;
+  ws->m_log2 = ws->m_log2_sr = o.p.m_log2;
   ws->n = n;
   ws->counts = nullptr;
   ws->loc[0] = ws->loc[1] = nullptr;  // the key-cached comb fallback checks every entry of a failing group

@@ -92,7 +92,8 @@ hipError_t launch_batch_check_tail(bool sr, const uint8_t *pk, const uint8_t *si
                                    Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
                                    uint8_t *out, hipStream_t stream, bool after_prep = false);
 // Mixed batch through the batch equation: partition, then one pipeline per
-// kind; with ks, the sr25519 pipeline runs on ks->helper (forked after the
+// kind (p: the ed25519 half's parameters, p_sr: the sr25519 half's); with
+// ks, the sr25519 pipeline runs on ks->helper (forked after the
 // partition, joined back into `stream` at the end).
 struct KindStreams {
   hipStream_t helper;
@@ -101,9 +102,9 @@ struct KindStreams {
 hipError_t launch_mixed_batch_check(const uint8_t *kind, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                     const uint32_t *msg_off, uint32_t n, const fe *btab_q, const strobe_t *prefix,
                                     Ed25519Work w_ed, Ed25519Work w_sr, MsmWork m_ed, MsmWork m_sr,
-                                    const MsmParams &p, const MsmSeed &seed_ed, const MsmSeed &seed_sr,
-                                    uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, int8_t *status,
-                                    hipStream_t stream, const KindStreams *ks = nullptr);
+                                    const MsmParams &p, const MsmParams &p_sr, const MsmSeed &seed_ed,
+                                    const MsmSeed &seed_sr, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
+                                    int8_t *status, hipStream_t stream, const KindStreams *ks = nullptr);
 
 // Pieces of the pipelines, shared with msm_kernels.hip.
 template <bool SR>

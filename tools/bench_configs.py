@@ -110,7 +110,10 @@ if "5" in only:
     do = t(b.off.view(np.int32))
     st = torch.cuda.Stream()
     ref = None
-    c5_methods = [("per-entry", N.TMV_FLAG_PER_ENTRY, 0), ("batch m=32", N.TMV_FLAG_BATCH_EQUATION, 5),
+    # "batch default": the runtime's own group sizes (ed25519 half 128 with the
+    # located fallback, sr25519 half 64); "batch m=..": both halves forced
+    c5_methods = [("per-entry", N.TMV_FLAG_PER_ENTRY, 0), ("batch default", N.TMV_FLAG_BATCH_EQUATION, 0),
+                  ("batch m=32", N.TMV_FLAG_BATCH_EQUATION, 5),
                   ("batch m=64", N.TMV_FLAG_BATCH_EQUATION, 6), ("batch m=128", N.TMV_FLAG_BATCH_EQUATION, 7),
                   ("batch m=256", N.TMV_FLAG_BATCH_EQUATION, 8)]
     if a.c5_methods:
