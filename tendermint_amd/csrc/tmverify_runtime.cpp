@@ -450,8 +450,8 @@ struct Layout {
 // these parameters and this randomness.
 struct LaunchOpts {
   bool batch_eq = false;
-  tmv::MsmParams p{};      // single-kind launches; the ed25519 half of a mixed one
-  tmv::MsmParams p_sr{};   // the sr25519 half of a mixed launch
+  tmv::MsmParams p{};      // single-kind launches; the sr25519 half of a mixed one
+  tmv::MsmParams p_ed{};   // the ed25519 half of a mixed launch
   tmv::MsmSeed seed[2]{};  // [kind]
 };
 
@@ -499,8 +499,7 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
     // mixed launches: each kind's half its own group size -- ed25519 takes
     // the located-fallback groups of 128 at the size ed25519-only launches
     // do, sr25519 keeps 64 (msm_params); both stay the caller's when set
-    o.p_sr = o.p;
-    if (!merged && !ed_only) o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, false, true, ctx->msm_sub);
+    o.p_ed = merged || ed_only ? o.p : msm_params(n, ctx->msm_m_log2, ctx->msm_c, false, true, ctx->msm_sub);
     fixed = ctx->fixed_seed;
     if (fixed) std::memcpy(key, ctx->seed, 32);
   }
@@ -949,7 +948,7 @@ static int launch_sr25519(Device &d, const LaunchOpts &o, const uint8_t *pk, con
 static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *off, uint32_t n, int8_t *status, hipStream_t s) {
   int rc;
-  Workspace *ws = reserve_work(d, n, true, s, &rc, o.batch_eq ? &o.p : nullptr, o.batch_eq ? &o.p_sr : nullptr);
+  Workspace *ws = reserve_work(d, n, true, s, &rc, o.batch_eq ? &o.p_ed : nullptr, o.batch_eq ? &o.p : nullptr);
   if (!ws) return rc;
   tmv::Ed25519Work w1 = tmv::Ed25519Work::carve(ws->work.ptr, n);
   tmv::Ed25519Work w2 = tmv::Ed25519Work::carve(ws->work2.ptr, n);
@@ -957,8 +956,8 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
   uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n;
   hipError_t e;
   if (o.batch_eq) {
-    tmv::MsmWork m1 = tmv::MsmWork::carve(ws->msm.ptr, n, o.p);
-    tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p_sr);
+    tmv::MsmWork m1 = tmv::MsmWork::carve(ws->msm.ptr, n, o.p_ed);
+    tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p);
     read_env();
     tmv::KindStreams &ks = ws->kinds;
     if (g_mixed_two && !ks.helper) {
@@ -966,20 +965,20 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
       if (hipEventCreateWithFlags(&ks.fork, hipEventDisableTiming) != hipSuccess) ks.fork = nullptr;
       if (hipEventCreateWithFlags(&ks.join, hipEventDisableTiming) != hipSuccess) ks.join = nullptr;
     }
-    e = tmv::launch_mixed_batch_check(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, m1, m2, o.p,
-                                      o.p_sr, o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s,
+    e = tmv::launch_mixed_batch_check(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, m1, m2, o.p_ed,
+                                      o.p, o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s,
                                       g_mixed_two ? &ks : nullptr);
     ws->group_ok[0] = m1.group_ok;
     ws->group_ok[1] = m2.group_ok;
-    ws->sub_ok[0] = o.p.sub ? m1.sub_ok : nullptr;
-    ws->sub_ok[1] = o.p_sr.sub ? m2.sub_ok : nullptr;
-    ws->groups = o.p.groups;
-    ws->m_log2 = ws->m_log2_sr = o.p.m_log2;
-    ws->m_log2_sr = o.p_sr.m_log2;
+    ws->sub_ok[0] = o.p_ed.sub ? m1.sub_ok : nullptr;
+    ws->sub_ok[1] = o.p.sub ? m2.sub_ok : nullptr;
+    ws->groups = o.p_ed.groups;
+    ws->m_log2 = o.p_ed.m_log2;
+    ws->m_log2_sr = o.p.m_log2;
     ws->n = n;
     ws->counts = counts;
-    ws->loc[0] = tmv::locate_enabled(n, o.p) ? m1.loc_count : nullptr;
-    ws->loc[1] = tmv::locate_enabled(n, o.p_sr) ? m2.loc_count : nullptr;
+    ws->loc[0] = tmv::locate_enabled(n, o.p_ed) ? m1.loc_count : nullptr;
+    ws->loc[1] = tmv::locate_enabled(n, o.p) ? m2.loc_count : nullptr;
   } else {
     e = tmv::launch_mixed_verify(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, counts, idx_ed, idx_sr,
                                  status, s);
