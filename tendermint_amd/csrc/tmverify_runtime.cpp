@@ -283,11 +283,13 @@ int g_stream = 1;
 bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
 int g_stream_two = 1;              // TMV_STREAM_TWO=0: every part on the lane's stream
 int g_mixed_two = 1;               // TMV_MIXED_TWO=0: a mixed launch's two kind pipelines on one stream
-// 320k C2 entries end to end (tools/gpu_stream_check.sh, parts on two
-// streams): 5.7 ms with parts of 32k / 64k, 5.8 with 16k / 64k, 5.85-6.0
-// with 32k / 128k, 6.1 with 16k / 32k; one stream 6.05-6.3; unstreamed
-// (two lanes of 80k chunks) 6.9 ms
-uint32_t g_stream_first = 32768, g_stream_part = 65536, g_stream_chunk = 1u << 21;
+// Round 2, 320k C2 entries end to end (parts on two streams): 5.7 ms with
+// parts of 32k / 64k, 5.85-6.0 with 32k / 128k; one stream 6.05-6.3;
+// unstreamed (two lanes of 80k chunks) 6.9 ms.  Round 3 (faster kernels,
+// the caller's pages DMA'd directly), the bench's 640k entries: parts of
+// 128k 82.7-83.8 M/s, 64k 77.3-79.1, 256k 78.9-79.8; a first part of 16k
+// or 64k changes nothing (profiles/r03/e2e_parts.txt)
+uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 21;
 // Streamed parts DMA straight from the caller's buffers: each part pins the
 // whole pages of its pk / sig / msg spans (hipHostRegister, disjoint page
 // ranges part to part) while earlier parts run, and only the bytes outside
