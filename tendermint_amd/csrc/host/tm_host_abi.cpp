@@ -476,35 +476,6 @@ std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n
   return vs;
 }
 
-// Into an existing object, reusing its vectors' storage (per-thread pools).
-void vals_into(tmh::ValidatorSet &vs, const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index) {
-  vs.validators.resize(n_vals);
-  for (uint32_t i = 0; i < n_vals; i++) {
-    tmh::Validator &v = vs.validators[i];
-    v.address = tmh::ByteView(vals[i].address, vals[i].address_len);
-    v.pub_key = tmh::PubKey{to_kind(vals[i].key_kind), tmh::ByteView(vals[i].pub_key, vals[i].pub_key_len)};
-    v.voting_power = vals[i].voting_power;
-    v.proposer_priority = vals[i].proposer_priority;
-  }
-  vs.proposer = proposer_index;
-  vs.UpdateTotalVotingPower();
-}
-
-void commit_into(tmh::Commit &cm, const tmv_commit *commit) {
-  cm.height = commit->height;
-  cm.round = commit->round;
-  cm.block_id = block_id_of(commit->block_id);
-  cm.signatures.resize(commit->n_sigs);
-  for (uint32_t i = 0; i < commit->n_sigs; i++) {
-    const tmv_commit_sig &s = commit->sigs[i];
-    tmh::CommitSig &c = cm.signatures[i];
-    c.block_id_flag = (tmh::BlockIDFlag)s.block_id_flag;
-    c.validator_address = tmh::ByteView(s.validator_address, s.validator_address_len);
-    c.timestamp = tmh::Timestamp{s.ts_seconds, s.ts_nanos};
-    c.signature = tmh::ByteView(s.signature, s.signature_len);
-  }
-}
-
 std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit) {
   if (!commit) return nullptr;
   auto cm = std::make_unique<tmh::Commit>();
@@ -547,21 +518,10 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
       jc[j] = it->second;
     }
   }
-  // conversions into per-thread pools reused across calls (a C4 window is
-  // ~10^5 small heap objects: allocating and freeing them per window cost
-  // ~1.5 ms), and the objects the checks read (vsets / commits: pooled ones
-  // or the caller's already converted ones)
-  static thread_local std::vector<tmh::ValidatorSet> tls_v;
-  static thread_local std::vector<tmh::Commit> tls_c;
-  static thread_local std::vector<tmh::CommitPlan> tls_plans;
-  // references: inside the pool's lambdas a thread_local name would be the
-  // worker's own instance, these are this thread's
-  std::vector<tmh::ValidatorSet> &own_v = tls_v;
-  std::vector<tmh::Commit> &own_c = tls_c;
-  std::vector<tmh::CommitPlan> &plans = tls_plans;
-  if (own_v.size() < vsrc.size()) own_v.resize(vsrc.size());
-  if (own_c.size() < csrc.size()) own_c.resize(csrc.size());
-  if (plans.size() < n_jobs) plans.resize(n_jobs);
+  // owned conversions (own_*) and the objects the checks read (vsets /
+  // commits: the owned ones or the caller's already converted ones)
+  std::vector<std::unique_ptr<tmh::ValidatorSet>> own_v(vsrc.size());
+  std::vector<std::unique_ptr<tmh::Commit>> own_c(csrc.size());
   std::vector<const tmh::ValidatorSet *> vsets(vsrc.size(), nullptr);
   std::vector<const tmh::Commit *> commits(csrc.size(), nullptr);
   parallel_for(vsrc.size() + csrc.size(), 4, [&](size_t i) {
@@ -574,27 +534,27 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
           return;
         }
       }
-      vals_into(own_v[i], vsrc[i]->vals, vsrc[i]->n_vals, vsrc[i]->proposer_index);
-      vsets[i] = &own_v[i];
+      own_v[i] = vals_of(vsrc[i]->vals, vsrc[i]->n_vals, vsrc[i]->proposer_index);
+      vsets[i] = own_v[i].get();
     } else {
       const size_t c = i - vsrc.size();
       if (conv) {
         auto it = conv->commits.find(csrc[c]->commit);
         if (it != conv->commits.end()) { commits[c] = it->second; return; }
       }
-      commit_into(own_c[c], csrc[c]->commit);
-      commits[c] = &own_c[c];
+      own_c[c] = commit_of(csrc[c]->commit);
+      commits[c] = own_c[c].get();
     }
   });
   tm.mark("convert");
+  std::vector<tmh::CommitPlan> plans(n_jobs);
   parallel_for(n_jobs, 4, [&](size_t j) {
     const tmv_commit_job &jb = jobs[j];
     const tmh::BlockID bid = jb.block_id ? block_id_of(*jb.block_id) : tmh::BlockID{};
-    static thread_local std::string chain;
-    chain.assign(jb.chain_id ? jb.chain_id : "");
-    tmh::CommitVerifier::PlanInto(plans[j], (tmh::CommitVerifier::Mode)jb.mode, chain,
-                                  jv[j] == SIZE_MAX ? nullptr : vsets[jv[j]], bid, jb.height,
-                                  jc[j] == SIZE_MAX ? nullptr : commits[jc[j]], jb.trust_num, jb.trust_den);
+    plans[j] = tmh::CommitVerifier::Plan((tmh::CommitVerifier::Mode)jb.mode, jb.chain_id ? jb.chain_id : "",
+                                         jv[j] == SIZE_MAX ? nullptr : vsets[jv[j]], bid, jb.height,
+                                         jc[j] == SIZE_MAX ? nullptr : commits[jc[j]], jb.trust_num,
+                                         jb.trust_den);
   });
   tm.mark("plan");
   // dedupe identical entries across plans: same commit object and signature
@@ -700,7 +660,13 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
     if (e) bad.fetch_add(1, std::memory_order_relaxed);
   });
   tm.mark("finish");
-  // the pools keep their storage for the next call on this thread
+  // the converted sets, commits and plans are ~10^5 small heap objects per
+  // window; freed on one thread they took ~7 ms of a C3 window
+  parallel_for(std::max(own_v.size(), std::max(own_c.size(), (size_t)n_jobs)), 16, [&](size_t i) {
+    if (i < own_v.size()) own_v[i].reset();
+    if (i < own_c.size()) own_c[i].reset();
+    if (i < n_jobs) plans[i] = tmh::CommitPlan();
+  });
   return bad.load();
 }
 

@@ -45,9 +45,6 @@ tmh::Bytes bytes_of(const uint8_t *p, size_t n);
 tmh::BlockID block_id_of(const tmv_block_id &b);
 std::unique_ptr<tmh::ValidatorSet> vals_of(const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index);
 std::unique_ptr<tmh::Commit> commit_of(const tmv_commit *commit);
-// the same conversions into existing objects (their storage reused)
-void vals_into(tmh::ValidatorSet &vs, const tmv_validator *vals, uint32_t n_vals, int32_t proposer_index);
-void commit_into(tmh::Commit &cm, const tmv_commit *commit);
 
 // Validator sets and commits a caller has already converted (the light
 // layer), looked up by the C struct they came from, so verify_commits does

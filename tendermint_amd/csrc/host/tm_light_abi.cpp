@@ -24,7 +24,8 @@ namespace {
 
 tmh::ByteView bytes_of(const tmv_bytes &b) { return tmh::ByteView(b.p, b.len); }
 
-void header_into(tmh::Header *o, const tmv_header &h) {
+std::unique_ptr<tmh::Header> header_of(const tmv_header &h) {
+  auto o = std::make_unique<tmh::Header>();
   o->version_block = h.version_block;
   o->version_app = h.version_app;
   o->chain_id = h.chain_id ? h.chain_id : "";
@@ -40,11 +41,6 @@ void header_into(tmh::Header *o, const tmv_header &h) {
   o->last_results_hash = bytes_of(h.last_results_hash);
   o->evidence_hash = bytes_of(h.evidence_hash);
   o->proposer_address = bytes_of(h.proposer_address);
-}
-
-std::unique_ptr<tmh::Header> header_of(const tmv_header &h) {
-  auto o = std::make_unique<tmh::Header>();
-  header_into(o.get(), h);
   return o;
 }
 
@@ -213,39 +209,15 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
     r.tv = V(jb.trusted_vals);
     r.uv = V(jb.untrusted_vals);
   }
-  // conversions into per-thread pools reused across calls (no allocation per
-  // window once warm; references, so the pool's workers write this thread's
-  // instances); a null source leaves its slot unused
-  static thread_local std::vector<tmh::Header> tls_h;
-  static thread_local std::vector<tmh::Commit> tls_c;
-  static thread_local std::vector<tmh::ValidatorSet> tls_v;
-  static thread_local std::vector<tmh::LightPlan> tls_plans;
-  std::vector<tmh::Header> &hpool = tls_h;
-  std::vector<tmh::Commit> &cpool = tls_c;
-  std::vector<tmh::ValidatorSet> &vpool = tls_v;
-  if (hpool.size() < H.src.size()) hpool.resize(H.src.size());
-  if (cpool.size() < C.src.size()) cpool.resize(C.src.size());
-  if (vpool.size() < V.src.size()) vpool.resize(V.src.size());
-  std::vector<tmh::Header *> headers(H.src.size(), nullptr);
-  std::vector<tmh::Commit *> commits(C.src.size(), nullptr);
-  std::vector<tmh::ValidatorSet *> vsets(V.src.size(), nullptr);
+  std::vector<std::unique_ptr<tmh::Header>> headers(H.src.size());
+  std::vector<std::unique_ptr<tmh::Commit>> commits(C.src.size());
+  std::vector<std::unique_ptr<tmh::ValidatorSet>> vsets(V.src.size());
   const size_t nh = headers.size(), nc = commits.size();
   parallel_for(nh + nc + vsets.size(), 16, [&](size_t i) {
-    if (i < nh) {
-      header_into(&hpool[i], *H.src[i]);
-      headers[i] = &hpool[i];
-    } else if (i < nh + nc) {
-      if (C.src[i - nh]) {
-        commit_into(cpool[i - nh], C.src[i - nh]);
-        commits[i - nh] = &cpool[i - nh];
-      }
-    } else {
-      const tmv_validator_set *v = V.src[i - nh - nc];
-      if (v->vals) {
-        vals_into(vpool[i - nh - nc], v->vals, v->n_vals, v->proposer_index);
-        vsets[i - nh - nc] = &vpool[i - nh - nc];
-      }
-    }
+    if (i < nh) headers[i] = header_of(*H.src[i]);
+    else if (i < nh + nc) commits[i - nh] = commit_of(C.src[i - nh]);
+    else vsets[i - nh - nc] = vals_of(V.src[i - nh - nc]->vals, V.src[i - nh - nc]->n_vals,
+                                      V.src[i - nh - nc]->proposer_index);
   });
   tm.mark("convert");
   // hashes the checks may need: Header.Hash of untrusted headers,
@@ -257,10 +229,10 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
   }
   std::vector<const tmh::Header *> hq(nh, nullptr);
   for (size_t i = 0; i < nh; i++)
-    if (need_h[i]) hq[i] = headers[i];
+    if (need_h[i]) hq[i] = headers[i].get();
   std::vector<const tmh::ValidatorSet *> vq(vsets.size(), nullptr);
   for (size_t i = 0; i < vsets.size(); i++)
-    if (need_v[i]) vq[i] = vsets[i];
+    if (need_v[i]) vq[i] = vsets[i].get();
   std::vector<tmh::Bytes> hh, vh;
   int rc = header_hashes(ctx, hq, hh);
   tm.mark("hdr hash");
@@ -272,19 +244,18 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
   }
   // non-signature checks, in the reference's order
   static const tmh::Bytes kNone;
-  std::vector<tmh::LightPlan> &plans = tls_plans;
-  if (plans.size() < n_jobs) plans.resize(n_jobs);
+  std::vector<tmh::LightPlan> plans(n_jobs);
   parallel_for(n_jobs, 16, [&](size_t j) {
     const tmv_light_job &jb = jobs[j];
     const Ref &r = refs[j];
     tmh::LightJob lj;
     lj.mode = (tmh::LightMode)jb.mode;
-    lj.trusted = tmh::SignedHeader{r.th == UINT32_MAX ? nullptr : headers[r.th],
-                                   r.tc == UINT32_MAX ? nullptr : commits[r.tc]};
-    lj.untrusted = tmh::SignedHeader{r.uh == UINT32_MAX ? nullptr : headers[r.uh],
-                                     r.uc == UINT32_MAX ? nullptr : commits[r.uc]};
-    lj.trusted_vals = r.tv == UINT32_MAX ? nullptr : vsets[r.tv];
-    lj.untrusted_vals = r.uv == UINT32_MAX ? nullptr : vsets[r.uv];
+    lj.trusted = tmh::SignedHeader{r.th == UINT32_MAX ? nullptr : headers[r.th].get(),
+                                   r.tc == UINT32_MAX ? nullptr : commits[r.tc].get()};
+    lj.untrusted = tmh::SignedHeader{r.uh == UINT32_MAX ? nullptr : headers[r.uh].get(),
+                                     r.uc == UINT32_MAX ? nullptr : commits[r.uc].get()};
+    lj.trusted_vals = r.tv == UINT32_MAX ? nullptr : vsets[r.tv].get();
+    lj.untrusted_vals = r.uv == UINT32_MAX ? nullptr : vsets[r.uv].get();
     lj.trusting_period_ns = jb.trusting_period_ns;
     lj.now = tmh::Timestamp{jb.now_seconds, jb.now_nanos};
     lj.max_clock_drift_ns = jb.max_clock_drift_ns;
@@ -317,10 +288,10 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
     Converted conv;
     conv.vals.reserve(vsets.size());
     for (size_t i = 0; i < vsets.size(); i++)
-      if (vsets[i]) conv.vals.emplace(V.src[i]->vals, vsets[i]);
+      if (vsets[i]) conv.vals.emplace(V.src[i]->vals, vsets[i].get());
     conv.commits.reserve(commits.size());
     for (size_t i = 0; i < commits.size(); i++)
-      if (commits[i]) conv.commits.emplace(C.src[i], commits[i]);
+      if (commits[i]) conv.commits.emplace(C.src[i], commits[i].get());
     rc = verify_commits(ctx, cj.data(), (uint32_t)cj.size(), cres.data(), cerr.data(), kStride, cne.data(), &conv);
     if (rc < 0) {
       if (errs && err_stride) put_err(errs, err_stride, std::string(cerr.data()));
@@ -344,7 +315,14 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
     bad += lr.kind != tmh::kLightOk;
   }
   tm.mark("finish");
-  // the pools keep their storage for the next call on this thread
+  // many small heap objects (validators, signatures, plans): freed in parallel
+  const size_t nrel = std::max({headers.size(), commits.size(), vsets.size(), (size_t)n_jobs});
+  parallel_for(nrel, 16, [&](size_t i) {
+    if (i < headers.size()) headers[i].reset();
+    if (i < commits.size()) commits[i].reset();
+    if (i < vsets.size()) vsets[i].reset();
+    if (i < n_jobs) plans[i] = tmh::LightPlan();
+  });
   return bad;
 }
 

@@ -663,50 +663,29 @@ struct CommitVerifier {
   static CommitPlan Plan(Mode mode, const std::string &chain_id, const ValidatorSet *vals, const BlockID &block_id,
                          int64_t height, const Commit *commit, int64_t num, int64_t den) {
     CommitPlan pl;
-    PlanInto(pl, mode, chain_id, vals, block_id, height, commit, num, den);
-    return pl;
-  }
-
-  // Plan into an existing plan, reusing its vectors' storage (the host layer
-  // keeps one plan per job slot per thread across calls: no allocation per
-  // window once warm).
-  static void PlanInto(CommitPlan &pl, Mode mode, const std::string &chain_id, const ValidatorSet *vals,
-                       const BlockID &block_id, int64_t height, const Commit *commit, int64_t num, int64_t den) {
-    pl.early.reset();
-    pl.batch = pl.defer_add = false;
-    pl.tallied = pl.needed = 0;
-    pl.entries.clear();
-    pl.sig_idx.clear();
-    pl.deferred_sig.clear();
-    pl.crosses.clear();
     pl.commit = commit;
-    pl.chain_id.assign(chain_id);
-    PlanBody(pl, mode, chain_id, vals, block_id, height, commit, num, den);
-  }
-
-  static void PlanBody(CommitPlan &pl, Mode mode, const std::string &chain_id, const ValidatorSet *vals,
-                       const BlockID &block_id, int64_t height, const Commit *commit, int64_t num, int64_t den) {
+    pl.chain_id = chain_id;
     if (mode == kLightTrusting) {
-      if (!vals) { pl.early = std::string("nil validator set"); return; }
-      if (den == 0) { pl.early = std::string("trustLevel has zero Denominator"); return; }
-      if (!commit) { pl.early = std::string("nil commit"); return; }
+      if (!vals) { pl.early = std::string("nil validator set"); return pl; }
+      if (den == 0) { pl.early = std::string("trustLevel has zero Denominator"); return pl; }
+      if (!commit) { pl.early = std::string("nil commit"); return pl; }
       auto [prod, overflow] = SafeMul(vals->TotalVotingPower(), num);
       if (overflow) {
         pl.early = std::string(
             "int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator");
-        return;
+        return pl;
       }
       pl.needed = prod / den;
       pl.batch = ShouldBatchVerify(*vals, *commit);
       PlanLoop(pl, chain_id, *vals, *commit, IgnoreNotCommit, CountAll, false, false);
-      return;
+      return pl;
     }
-    if ((pl.early = VerifyBasic(vals, commit, height, block_id))) return;
+    if ((pl.early = VerifyBasic(vals, commit, height, block_id))) return pl;
     pl.needed = vals->TotalVotingPower() * 2 / 3;
     pl.batch = ShouldBatchVerify(*vals, *commit);
     if (mode == kFull) PlanLoop(pl, chain_id, *vals, *commit, IgnoreAbsent, CountCommit, true, true);
     else PlanLoop(pl, chain_id, *vals, *commit, IgnoreNotCommit, CountAll, false, true);
-    return;
+    return pl;
   }
 };
 
