@@ -195,6 +195,10 @@ struct MsmWork {
   uint32_t *fb_count;    // entries in fb_list
   uint32_t *loc_found;   // failing groups whose one bad entry the search named (tmv_metrics)
   uint32_t *fb_list;     // n: work indices verified one by one
+  // groups the located search could not name (two or more bad entries):
+  // their 8-entry sub-groups are checked (k_msm_subcheck) before the fallback
+  uint32_t *l2_list;     // groups
+  uint32_t *l2_count;
   // key-merged form only (null otherwise)
   uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
   uint32_t *bscal;     // groups x 8 words: B scalar of the group
@@ -211,7 +215,7 @@ struct MsmWork {
                17 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
     else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
-              G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16;
+              G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16 + 4 * G + 2 * 16;
     return b;
   }
   static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
@@ -242,6 +246,7 @@ struct MsmWork {
     w.tabR = nullptr;
     w.fail_T = nullptr;
     w.loc_count = w.fb_count = w.fb_list = w.loc_found = nullptr;
+    w.l2_list = w.l2_count = nullptr;
     if (!p.merged) {
       w.fail_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
       w.fail_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
@@ -252,6 +257,8 @@ struct MsmWork {
       w.fb_count = w.loc_count + 1;
       w.loc_found = w.loc_count + 2; o = up(o + 16);
       w.fb_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4ull * n);
+      w.l2_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
+      w.l2_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
     }
     if (p.merged) {
       w.wscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32ull * n);

@@ -189,6 +189,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       *mw.loc_count = nf << p.m_log2;  // the bucket stages' entry count: nf slots
       *mw.fb_count = 0;                // k_loc_search appends the entries left to verify
       *mw.loc_found = 0;
+      *mw.l2_count = 0;                // and the groups it could not name
     }
     if (g >= nf) return;  // block-uniform
   }
@@ -738,7 +739,7 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
 // pre-check status); otherwise every entry of the group is.
 template <bool SR>
 __global__ void __launch_bounds__(64)
-k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, int sub2) {
   __shared__ int s_cnt, s_j;
   __shared__ uint32_t s_base;
   const uint32_t f = blockIdx.x;
@@ -794,9 +795,29 @@ k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     }
     return;
   }
+  if (sub2) {  // two or more bad entries: its sub-groups are checked next
+    if (threadIdx.x == 0) mw.l2_list[atomicAdd(mw.l2_count, 1u)] = mw.fail_list[f];
+    return;
+  }
   if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < mlive; t += 64) mw.fb_list[s_base + t] = e0 + t;
+}
+
+// After k_msm_subcheck over the groups the search could not name: the
+// entries of every failing 8-entry sub-group go to the per-entry list (the
+// rest keep their pre-check status).  One lane per (listed group, sub-group).
+__global__ void __launch_bounds__(256)
+k_sub_list(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t sh = p.m_log2 - kSubGroupLog2;
+  if ((t >> sh) >= *mw.l2_count) return;
+  const uint32_t e0 = (mw.l2_list[t >> sh] << p.m_log2) + ((t & ((1u << sh) - 1)) << kSubGroupLog2);
+  const uint32_t cnt = entry_count(count_ptr, n);
+  if (e0 >= cnt || mw.sub_ok[e0 >> kSubGroupLog2]) return;
+  const uint32_t k = min(kSubGroup, cnt - e0);
+  const uint32_t at = atomicAdd(mw.fb_count, k);
+  for (uint32_t j = 0; j < k; j++) mw.fb_list[at + j] = e0 + j;
 }
 
 // Sub-group bisection (row H, before the per-entry fallback): a failing group
@@ -818,11 +839,11 @@ template <bool SR>
 __global__ void __launch_bounds__(64)
 k_msm_subcheck(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
                uint32_t n, Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q,
-               int aligned) {
+               int aligned, const uint32_t *__restrict__ list, const uint32_t *list_count) {
   constexpr int kQ = 16;                           // quads (sub-groups) per wave
   __shared__ int8_t dig[kQ][kSubGroup][2][64];     // [0]: z k mod l, [1]: z (33 digits used)
   __shared__ int8_t bdig[kQ][32];
-  const uint32_t subs = *mw.fail_count << (p.m_log2 - kSubGroupLog2);
+  const uint32_t subs = *list_count << (p.m_log2 - kSubGroupLog2);
   if (blockIdx.x * kQ >= subs) return;  // block-uniform
   const int c = (int)(threadIdx.x & 3);
   const int q = (int)(threadIdx.x >> 2);
@@ -830,7 +851,7 @@ k_msm_subcheck(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx
   const bool live = raw < subs;
   const uint32_t t = live ? raw : subs - 1;  // whole quads stay active for DPP
   const uint32_t sh = p.m_log2 - kSubGroupLog2;
-  const uint32_t g = mw.fail_list[t >> sh];
+  const uint32_t g = list[t >> sh];
   const uint32_t e0 = (g << p.m_log2) + ((t & ((1u << sh) - 1)) << kSubGroupLog2);
   const uint32_t cnt = entry_count(count_ptr, n);
 
@@ -1103,6 +1124,20 @@ static uint32_t locate_min() {
 
 uint32_t locate_min_entries() { return locate_min(); }
 
+// TMV_LOC_SUBCHECK=1: groups the located search cannot name (two or more
+// bad entries, ~2% of C2's groups of 128) get sub-group checks before the
+// per-entry fallback instead of all their entries verified one by one.  Less
+// work, a longer tail (the Straus sub-group chain, then the fallback's): C2
+// bench 126.2-126.9 with vs 127.9-128.8 M/s without (profiles/r03/
+// ab_loc_subcheck.txt), so off by default.
+static bool loc_subcheck() {
+  static const bool on = [] {
+    const char *e = getenv("TMV_LOC_SUBCHECK");
+    return e && !strcmp(e, "1");
+  }();
+  return on;
+}
+
 bool locate_enabled(uint32_t n, const MsmParams &p) {
   const uint32_t lmin = locate_min();
   return fallback_compact() && lmin && n >= lmin && !p.sub && p.WL() <= p.W;
@@ -1214,8 +1249,18 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
                        mw.loc_count, n_slots, mw, p, nullptr, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p);
+    const int sub2 = loc_subcheck() ? 1 : 0;
+    hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p, sub2);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (sub2) {  // groups the search could not name: sub-group checks, then their failing sub-groups' entries
+      const uint64_t subs = (uint64_t)p.groups << (p.m_log2 - kSubGroupLog2);
+      hipLaunchKernelGGL(k_msm_subcheck<SR>, dim3((uint32_t)((subs + 15) / 16)), dim3(64), 0, stream, sig, idx,
+                         count_ptr, n, w, mw, p, seed, btab_q, aligned, (const uint32_t *)mw.l2_list,
+                         (const uint32_t *)mw.l2_count);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_sub_list, dim3((uint32_t)((subs + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream,
                                     nullptr, nullptr, nullptr, mw.fb_list, mw.fb_count);
   }
@@ -1224,7 +1269,8 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     // grid for every group failing; blocks past the failing count exit at once
     const uint64_t subs = (uint64_t)p.groups << (p.m_log2 - kSubGroupLog2);
     hipLaunchKernelGGL(k_msm_subcheck<SR>, dim3((uint32_t)((subs + 15) / 16)), dim3(64), 0, stream, sig, idx,
-                       count_ptr, n, w, mw, p, seed, btab_q, aligned);
+                       count_ptr, n, w, mw, p, seed, btab_q, aligned, (const uint32_t *)mw.fail_list,
+                       (const uint32_t *)mw.fail_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     sub_ok = mw.sub_ok;
   }

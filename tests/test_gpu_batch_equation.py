@@ -4,6 +4,8 @@ k_msm_group) with the per-entry fallback over failing groups must give the
 same validity vector as the oracle, and honest groups must actually pass the
 equation (tmv_batch_stats), so a broken MSM cannot hide behind the fallback.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -410,3 +412,39 @@ def test_metrics_counts_calls_and_resets(bctx):
     bctx.metrics_reset()
     met = bctx.metrics()
     assert all(v == 0 for k, v in met.items() if k not in ("key_cache_hits", "key_cache_misses"))
+
+
+LOC_SUB = r"""
+import sys, numpy as np
+sys.path.insert(0, '.'); sys.path.insert(0, 'oracle'); sys.path.insert(0, 'tests')
+import oracle_c as C
+from tendermint_amd import _native as N
+from test_gpu_batch_equation import _located_case
+ctx = N.Context(1)
+b, sig, singles, pairs = _located_case(m=128)
+ctx.set_batch_options(group_log2=7, window_bits=6, seed=bytes(range(32)), stats=True)
+ctx.metrics_reset()
+ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, b.pk, sig, b.msg, b.off)
+met = ctx.metrics()
+ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
+assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
+assert met["located_groups"] == len(singles)
+subs = {i // 8 for p in pairs for i in p}  # failing 8-entry sub-groups of the two-bad groups
+assert met["fallback_signatures"] == len(singles) + sum(min(8, b.n - 8 * s) for s in subs), met
+print("ok")
+"""
+
+
+def test_located_then_subgroups_option():
+    """TMV_LOC_SUBCHECK=1 (measured slower, off by default): the groups the
+    located search cannot name are checked by 8-entry sub-groups, and only
+    the entries of their failing sub-groups are verified one by one; the
+    vector equals the oracle's."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TMV_LOC_SUBCHECK="1")
+    out = subprocess.run([sys.executable, "-c", LOC_SUB], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "ok" in out.stdout
