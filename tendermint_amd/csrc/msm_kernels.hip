@@ -449,8 +449,14 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 // wave.  The rest (a wave's edge, buckets over three or more chunks) keep
 // their runs in part_last / part_first and name the bucket in join_b at the
 // chunk of its last run, for k_msm_join.
+// Waves per SIMD k_msm_accum is compiled for (1 = the compiler's choice,
+// 145 VGPRs, 3 waves).  4 (128 VGPRs, 26 spilled) measured slower, 119.4-120.5
+// vs 123.7-124.9 M/s (profiles/r03/ab_register_budget.txt).
+#ifndef TMV_ACCUM_WAVES
+#define TMV_ACCUM_WAVES 1
+#endif
 template <int L>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, TMV_ACCUM_WAVES)
 k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   __shared__ ge_p3 first_run[256];  // a lane's first run, joined by its wave neighbour (40 KB)
   // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD a
@@ -593,9 +599,17 @@ k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   }
 }
 
+// Waves per SIMD the running-sum kernel is compiled for (register budget;
+// 1 = the compiler's choice, 178 VGPRs, 2 waves).  3 (168 VGPRs, 2 spilled)
+// measured the same, 123.8-124.9 vs 123.7-124.9 M/s
+// (profiles/r03/ab_register_budget.txt).
+#ifndef TMV_WPART_WAVES
+#define TMV_WPART_WAVES 1
+#endif
+
 // Window parts: lane (g, w, q) sums buckets [q s, (q+1) s) of window w with
 // the running-sum trick: T = sum_i (i+1) B_{qs+i}, U = sum_i B_{qs+i}.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, TMV_WPART_WAVES)
 k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t per_group = p.W * p.P;
