@@ -441,6 +441,7 @@ def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, 
                              "recoding) x 7 field multiplications x 100 int32 products (SURVEY 8(d) unit)",
          "peak_from": "measured v_mad_i64_i32 rate, 16 waves/SIMD (tools/occbench.hip, profiles/occbench_r01.json)",
          "rocprof": rp,
+         "rocprof_inflight4": dfile.get("rocprof_inflight4"),
          "under_overlap": {"avg_launch_ms": round(ov_ms / ov_cnt, 4), "launches": ov_cnt,
                            "note": f"the timed region's launches ({args.inflight} in flight share the chip, so a "
                                    "launch's span is stretched; not the kernel's own time)"},

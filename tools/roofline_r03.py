@@ -101,6 +101,22 @@ def main():
                                         "first of each launch's pair; the second is the located pass over the "
                                         "failing groups); --stats averages both",
                                 "file": "rocprof --kernel-trace (trace_alone)"}
+    # the driver's command (4 launches in flight): the same primary
+    # dispatches, against the live under-overlap figure of that traced run
+    prim4, _ = primary_trace(d, "trace", KERNEL)
+    if prim4:
+        live = None
+        log = os.path.join(d, "trace.log")
+        if os.path.exists(log):
+            for line in open(log):
+                if line.startswith("{"):
+                    live = json.loads(line).get("roofline", {}).get("under_overlap", {}).get("avg_launch_ms")
+        out["rocprof_inflight4"] = {"command": "bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extras",
+                                    "avg_ms": round(sum(prim4) / len(prim4), 4), "dispatches": len(prim4),
+                                    "live_under_overlap_ms": live,
+                                    "note": "primary k_msm_accum dispatches of the timed launches with 4 in flight "
+                                            "(stretched by sharing the chip) against the bench's own HIP-event "
+                                            "figure of the same run"}
     # FETCH_SIZE calibration: known bytes / counted bytes per kernel
     cal = {}
     known = {}
