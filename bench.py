@@ -678,19 +678,21 @@ def main():
         # end-to-end through the host C-ABI (pinned staging, H2D, kernels,
         # D2H): KE resident batches as one host-resident batch, against the
         # same KE batches in one device launch
-        KE = min(K, R)
+        # (TMV_BENCH_E2E_BATCHES, default K: the timed region's launch size)
+        KE = max(1, min(K, int(os.environ.get("TMV_BENCH_E2E_BATCHES", str(K)))))
         same = []
         for _ in range(3):
             e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             launch(0, 0, KE, e, gather=False)
             torch.cuda.synchronize(dev)
             same.append(e[0].elapsed_time(e[1]))
-        hb = Batch.concat(batches[:KE])
+        hb = Batch.concat([batches[j % R] for j in range(KE)])
         e2e = []
         for _ in range(5):
             t1 = time.perf_counter()
-            ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, hb.pk, hb.sig, hb.msg, hb.off)
+            _, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, hb.pk, hb.sig, hb.msg, hb.off)
             e2e.append(time.perf_counter() - t1)
+            assert int((st == 1).sum()) == sum(expect_valid[j % R] for j in range(KE))
         e2e_rate = hb.n / statistics.median(e2e)
         extras["end_to_end_verifies_per_s"] = round(e2e_rate, 1)
         # the same KE batches as one call: host buffers vs already resident,

@@ -288,8 +288,10 @@ int g_mixed_two = 1;               // TMV_MIXED_TWO=0: a mixed launch's two kind
 // unstreamed (two lanes of 80k chunks) 6.9 ms.  Round 3 (faster kernels,
 // the caller's pages DMA'd directly), the bench's 640k entries: parts of
 // 128k 82.7-83.8 M/s, 64k 77.3-79.1, 256k 78.9-79.8; a first part of 16k
-// or 64k changes nothing (profiles/r03/e2e_parts.txt)
-uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 21;
+// or 64k changes nothing (profiles/r03/e2e_parts.txt).  2.56 M entries per
+// call: chunks of up to 4 M (one pipeline) 106 M/s, 2 M (two pipelines of
+// 1.28 M on two lanes) 98 M/s, 1 M 87 M/s (profiles/r03/e2e_chunk.txt)
+uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 22;
 // Streamed parts DMA straight from the caller's buffers: each part pins the
 // whole pages of its pk / sig / msg spans (hipHostRegister, disjoint page
 // ranges part to part) while earlier parts run, and only the bytes outside
