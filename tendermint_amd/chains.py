@@ -67,24 +67,71 @@ def validator_set_hashes(ctx, sets: List[H.ValidatorSet]) -> List[bytes]:
     return [bytes(r) for r in out]
 
 
+def in_order(windows, run, depth: int):
+    """run(w) for each window with up to `depth` windows in flight on caller
+    threads, results yielded in window order.  The engine calls release the
+    GIL, so one window's conversion and engine call overlap another's.
+    Windows are independent (each is built from inputs only, never from an
+    earlier window's result), so a later window verified before an earlier
+    one fails only costs work: the consumer stops at the first error and
+    what ran past it is discarded -- the results equal one window at a
+    time.  A consumer that stops early cancels the windows not yet started
+    and waits for the running ones."""
+    if depth <= 1:
+        for w in windows:
+            yield run(w)
+        return
+    from collections import deque
+    from concurrent.futures import ThreadPoolExecutor
+    q = deque()
+    with ThreadPoolExecutor(depth) as ex:
+        try:
+            for w in windows:
+                q.append(ex.submit(run, w))
+                if len(q) >= depth:
+                    yield q.popleft().result()
+            while q:
+                yield q.popleft().result()
+        finally:
+            for f in q:
+                f.cancel()
+
+
 def verify_sequential(ctx, trusted: LightBlock, blocks: List[LightBlock], trusting_period_ns: int,
                       now: Tuple[int, int], max_clock_drift_ns: int = 10 * 10**9, window: int = 1000,
-                      verify_many=None) -> Tuple[int, Optional[VerificationFailed]]:
+                      verify_many=None, depth: Optional[int] = None) -> Tuple[int, Optional[VerificationFailed]]:
     """Client.verifySequential over `blocks` (heights trusted+1, ...) with a
     single primary: VerifyAdjacent(verified, interim) per height, `window`
-    headers per engine call (the light client's prefetch).  Returns (headers
-    verified, first ErrVerificationFailed or None)."""
-    run = verify_many or (lambda jobs: H.light_verify_many(ctx, jobs))
+    headers per engine call (the light client's prefetch), `depth` windows in
+    flight (default 2 on the engine, 1 with a caller's `verify_many`; see
+    in_order).  Returns (headers verified, first ErrVerificationFailed or
+    None)."""
+    if depth is None:
+        depth = 1 if verify_many else 2
+    if verify_many:
+        run, prepare = verify_many, (lambda jobs: jobs)
+    else:
+        # the C structs are built on this thread (Python, under the GIL),
+        # the engine calls on the in_order threads (GIL released)
+        fn = H._setup_light(H._setup(H._native.lib())).tmv_light_verify_many
+        run = lambda pj: H.run_light_jobs(fn, ctx.handle, pj)
+        prepare = H.PreparedLightJobs
+
+    def windows():
+        for lo in range(0, len(blocks), window):
+            p = trusted if lo == 0 else blocks[lo - 1]
+            jobs = []
+            for lb in blocks[lo:lo + window]:
+                jobs.append(LightJob(p.signed_header, None, lb.signed_header, lb.vals, trusting_period_ns, now,
+                                     max_clock_drift_ns, mode=H.LIGHT_ADJACENT))
+                p = lb
+            yield prepare(jobs)
+
     done = 0
     prev = trusted
-    for lo in range(0, len(blocks), window):
+    for lo, res in zip(range(0, len(blocks), window), in_order(windows(), run, depth)):
         chunk = blocks[lo:lo + window]
-        jobs, p = [], prev
-        for lb in chunk:
-            jobs.append(LightJob(p.signed_header, None, lb.signed_header, lb.vals, trusting_period_ns, now,
-                                 max_clock_drift_ns, mode=H.LIGHT_ADJACENT))
-            p = lb
-        for lb, (kind, text) in zip(chunk, run(jobs)):
+        for lb, (kind, text) in zip(chunk, res):
             if kind != H.LIGHT_OK:
                 return done, VerificationFailed(prev.height, lb.height, kind, text)
             prev = lb
@@ -189,8 +236,8 @@ class Block:
 
 
 def blocksync_replay(ctx, chain_id: str, vals: H.ValidatorSet, blocks: List[Block], last_block_id: H.BlockID,
-                     initial_height: int = 1, window: int = 600
-                     ) -> Tuple[int, Optional[Tuple[int, str]]]:
+                     initial_height: int = 1, window: int = 600, depth: Optional[int] = None,
+                     verify_commits=None) -> Tuple[int, Optional[Tuple[int, str]]]:
     """poolRoutine's checks for each block pair (first, second) over a static
     validator set (state.Validators == state.LastValidators):
       light: vals.VerifyCommitLight(chainID, first.BlockID, first.Height, second.LastCommit)
@@ -201,24 +248,46 @@ def blocksync_replay(ctx, chain_id: str, vals: H.ValidatorSet, blocks: List[Bloc
     previous block's BlockID after it (ApplyBlock).  `window` blocks per
     engine call (the pool buffers up to 600, internal/blocksync/pool.go:32-35);
     a commit read light at height H and full at H+1 is the same object, so its
-    signatures are verified once.  Returns (blocks applied, (height, error))."""
+    signatures are verified once; `depth` windows in flight (in_order;
+    default 2 on the engine, 1 with a caller's `verify_commits`, a function
+    jobs -> per-job error or None).  Returns (blocks applied, (height,
+    error))."""
+    if depth is None:
+        depth = 1 if verify_commits else 2
+    if verify_commits:
+        prepare = lambda jobs: jobs
+
+        def run(w):
+            return w[:3], verify_commits(w[3])
+    else:
+        prepare = H.PreparedJobs
+
+        def run(w):  # the C structs were built on the caller's thread (windows())
+            H.run_prepared_jobs(ctx, w[3])
+            return w[:3], w[3].decode()
+
+    def windows():
+        state_last = last_block_id
+        for lo in range(0, len(blocks) - 1, window):
+            chunk = blocks[lo:lo + window + 1]
+            jobs, where, early = [], [], {}
+            for i in range(len(chunk) - 1):
+                first, second = chunk[i], chunk[i + 1]
+                where.append((first.height, len(jobs)))
+                jobs.append(H.CommitJob(H.MODE_LIGHT, chain_id, vals, first.block_id, first.height,
+                                        second.last_commit))
+                if first.height == initial_height:
+                    if first.last_commit is not None and first.last_commit.signatures:
+                        early[first.height] = "initial block can't have LastCommit signatures"
+                    jobs.append(None)
+                else:
+                    jobs.append(H.CommitJob(H.MODE_FULL, chain_id, vals, state_last, first.height - 1,
+                                            first.last_commit))
+                state_last = first.block_id
+            yield jobs, where, early, prepare([j for j in jobs if j is not None])
+
     applied = 0
-    state_last = last_block_id
-    for lo in range(0, len(blocks) - 1, window):
-        chunk = blocks[lo:lo + window + 1]
-        jobs, where, early = [], [], {}
-        for i in range(len(chunk) - 1):
-            first, second = chunk[i], chunk[i + 1]
-            where.append((first.height, len(jobs)))
-            jobs.append(H.CommitJob(H.MODE_LIGHT, chain_id, vals, first.block_id, first.height, second.last_commit))
-            if first.height == initial_height:
-                if first.last_commit is not None and first.last_commit.signatures:
-                    early[first.height] = "initial block can't have LastCommit signatures"
-                jobs.append(None)
-            else:
-                jobs.append(H.CommitJob(H.MODE_FULL, chain_id, vals, state_last, first.height - 1, first.last_commit))
-            state_last = first.block_id
-        res = H.verify_commits(ctx, [j for j in jobs if j is not None])
+    for (jobs, where, early), res in in_order(windows(), run, depth):
         it = iter(res)
         flat = [next(it) if j is not None else None for j in jobs]
         for height, k in where:

@@ -48,9 +48,9 @@ def _oracle_sequential(trusted, blocks, now):
     return n, None if err is None else (err[0], err[1], err[2].kind, err[2].text)
 
 
-def _seq(fake, trusted, blocks, now, window):
+def _seq(fake, trusted, blocks, now, window, depth=1):
     n, err = chains.verify_sequential(None, trusted, blocks, PERIOD, now, DRIFT, window=window,
-                                      verify_many=fake.light_verify_many)
+                                      verify_many=fake.light_verify_many, depth=depth)
     return n, None if err is None else (err.from_height, err.to_height, err.kind, err.reason)
 
 
@@ -59,6 +59,32 @@ def test_sequential_ok(fake, window):
     trusted, blocks = make_light_chain(20, 8)
     now = _now(blocks)
     assert _seq(fake, trusted, blocks, now, window) == (20, None) == _oracle_sequential(trusted, blocks, now)
+    for depth in (2, 3):  # windows in flight on caller threads
+        assert _seq(fake, trusted, blocks, now, window, depth) == (20, None)
+
+
+def test_in_order_yields_in_window_order_and_stops():
+    """chains.in_order: results in window order whatever order the threads
+    finish in; a consumer that stops early leaves later windows unstarted
+    or discarded."""
+    import threading
+    import time
+    started = []
+    lock = threading.Lock()
+
+    def run(w):
+        with lock:
+            started.append(w)
+        time.sleep(0.002 * ((7 * w) % 5))  # windows finish out of order
+        return w * w
+
+    for depth in (1, 2, 4):
+        assert list(chains.in_order(iter(range(20)), run, depth)) == [w * w for w in range(20)]
+    started.clear()
+    for r in chains.in_order(iter(range(50)), run, 3):
+        if r == 16:  # window 4 "fails"
+            break
+    assert max(started) <= 4 + 3  # at most `depth` windows started past it
 
 
 @pytest.mark.parametrize("what", ["sig", "next_vals_hash", "vals_hash", "header_field", "chain_id", "expired",
@@ -86,7 +112,8 @@ def test_sequential_first_error_matches_oracle(fake, what):
     elif what == "time_order":
         b.header.time = blocks[10].signed_header.header.time
     for window in (1, 8, 100):
-        assert _seq(fake, trusted, blocks, now, window) == _oracle_sequential(trusted, blocks, now)
+        for depth in (1, 3):
+            assert _seq(fake, trusted, blocks, now, window, depth) == _oracle_sequential(trusted, blocks, now)
     n, err = _seq(fake, trusted, blocks, now, 100)
     assert err is not None and n < 20
 
@@ -145,10 +172,10 @@ def _fake_commits(fake):
     return lambda jobs: F.fake_verify_commits(fake, jobs)
 
 
-def _replay(fake, vals, blocks, last_bid, window, monkeypatch):
+def _replay(fake, vals, blocks, last_bid, window, monkeypatch, depth=2):
     import commit_fixtures as F
-    monkeypatch.setattr(H, "verify_commits", lambda ctx, jobs: F.fake_verify_commits(fake, jobs))
-    return chains.blocksync_replay(None, "test_chain_id", vals, blocks, last_bid, window=window)
+    return chains.blocksync_replay(None, "test_chain_id", vals, blocks, last_bid, window=window, depth=depth,
+                                   verify_commits=lambda jobs: F.fake_verify_commits(fake, jobs))
 
 
 def _oracle_replay(vals, blocks, last_bid):
@@ -181,7 +208,8 @@ def test_blocksync_replay_matches_oracle(fake, monkeypatch):
     want = _oracle_replay(vals, blocks, H.BlockID())
     assert want[1][0] == 14
     for window in (1, 5, 100):
-        assert _replay(fake, vals, blocks, H.BlockID(), window, monkeypatch) == want
+        for depth in (1, 2, 3):
+            assert _replay(fake, vals, blocks, H.BlockID(), window, monkeypatch, depth) == want
 
 
 def test_blocksync_uses_stored_last_commit(fake, monkeypatch):

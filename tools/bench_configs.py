@@ -8,6 +8,8 @@ each; the headline line is bench.py's C2).  Single GPU.
       header), window-batched through tmv_light_verify_many
   C4  blocksync replay: B blocks x 175 validators (light + full check per
       block = 292 reference verifications, 175 unique)
+  (C3 / C4 native: one window at a time, and 2 / 3 windows in flight on
+  caller threads -- chains.in_order, the drivers' default depth 2)
   C5  mixed ed25519 + sr25519 batch (kernel path, inputs resident)
 """
 import argparse, json, os, statistics, sys, time
@@ -64,6 +66,13 @@ if "3" in only:
     dn = time.perf_counter() - t
     line = {"config": f"C3 light sequential {a.headers} headers x 100 vals",
             "native_seconds": round(dn, 4), "native_headers_per_s": round(n / dn, 1)}
+    # windows pipelined on caller threads (chains.in_order, the drivers' default depth 2)
+    for depth in (2, 3):
+        t = time.perf_counter()
+        for res in chains.in_order(iter(pj), lambda p: H.run_light_jobs(L.tmv_light_verify_many, ctx.handle, p),
+                                   depth):
+            assert all(k == 0 for k, _ in res)
+        line[f"native_depth{depth}_headers_per_s"] = round(n / (time.perf_counter() - t), 1)
     if not a.native_only:
         line.update({"seconds": round(dt, 4), "headers_per_s": round(n / dt, 1),
                      "verifies_per_s_ref_count": round(67 * n / dt)})
@@ -91,6 +100,12 @@ if "4" in only:
     dn = time.perf_counter() - t
     line = {"config": f"C4 blocksync {a.blocks} blocks x 175 vals",
             "native_seconds": round(dn, 4), "native_blocks_per_s": round((len(blocks) - 2) / dn, 1)}
+    for depth in (2, 3):
+        t = time.perf_counter()
+        for rc in chains.in_order(iter(pj), lambda p: H.run_prepared_jobs(ctx, p), depth):
+            assert rc == 0
+        line[f"native_depth{depth}_blocks_per_s"] = round((len(blocks) - 2) / (time.perf_counter() - t), 1)
+    assert all(e is None for p in pj for e in p.decode())
     if not a.native_only:
         line.update({"seconds": round(dt, 4), "blocks_per_s": round(applied / dt, 1),
                      "verifies_per_s_ref_count": round(292 * applied / dt),
