@@ -20,6 +20,7 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -239,6 +240,13 @@ struct Device {
   // histograms of the key-merged form's counting sort
   std::vector<uint32_t> slots, key_count;
   std::mutex mu;
+  // lanes claimed by host-buffer calls (run_batch).  A call holds `mu` while
+  // it stages and launches a chunk, not while it waits for the device, so
+  // calls on different lanes (a caller's windows in flight) overlap; a chunk
+  // in flight is `lane[l].n != 0`, which resolve_keys waits for before a
+  // new key may evict a slot
+  bool lane_busy[kLanes] = {};
+  std::condition_variable lane_cv;
   // a device wait timed out: its work is in an unknown state, so every later
   // call on this device returns TMV_ERR_TIMEOUT (include/tmverify.h)
   std::atomic<bool> faulted{false};
@@ -1508,10 +1516,39 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   const tmh::ShardPlan plan =
       tmh::plan_shards(n, (uint32_t)ctx->devs.size(), streamable ? g_stream_chunk : g_host_chunk);
   const uint32_t shards = plan.shards;
-  std::vector<std::unique_lock<std::mutex>> locks;
-  for (uint32_t s = 0; s < shards; s++) locks.emplace_back(ctx->devs[s]->mu);
-  for (uint32_t s = 0; s < shards; s++)
-    if (ctx->devs[s]->faulted) return faulted_rc(*ctx->devs[s]);
+  // claim g_host_lanes lanes per device (devices in order, so concurrent
+  // calls cannot deadlock); released on every return
+  struct Claims {
+    tmv_ctx *ctx;
+    uint32_t nl, claimed = 0;
+    std::vector<std::array<uint32_t, kLanes>> lane;
+    ~Claims() {
+      for (uint32_t s = 0; s < claimed; s++) {
+        Device &d = *ctx->devs[s];
+        {
+          std::lock_guard<std::mutex> lk(d.mu);
+          for (uint32_t j = 0; j < nl; j++) d.lane_busy[lane[s][j]] = false;
+        }
+        d.lane_cv.notify_all();
+      }
+    }
+  } claims{ctx, std::min<uint32_t>(g_host_lanes, kLanes), 0, std::vector<std::array<uint32_t, kLanes>>(shards)};
+  for (uint32_t s = 0; s < shards; s++) {
+    Device &d = *ctx->devs[s];
+    std::unique_lock<std::mutex> lk(d.mu);
+    d.lane_cv.wait(lk, [&] {
+      uint32_t free = 0;
+      for (uint32_t l = 0; l < kLanes; l++) free += !d.lane_busy[l];
+      return free >= claims.nl || d.faulted;
+    });
+    if (d.faulted) return faulted_rc(d);
+    for (uint32_t l = 0, j = 0; l < kLanes && j < claims.nl; l++)
+      if (!d.lane_busy[l]) {
+        d.lane_busy[l] = true;
+        claims.lane[s][j++] = l;
+      }
+    claims.claimed = s + 1;
+  }
   EngineTimer tm;
   // chunk k of every shard, then chunk k + 1: the devices work side by side
   // (host/shard_run.h; the CPU test double runs the same order)
@@ -1519,30 +1556,31 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
       plan, g_host_lanes,
       [&](uint32_t s, uint32_t lane, bool ok) -> int {
         Device &d = *ctx->devs[s];
-        HostLane &ln = d.lane[lane];
-        if (ln.n == 0) return 0;
+        HostLane &ln = d.lane[claims.lane[s][lane]];
+        if (ln.n == 0) return 0;  // this call is the lane's only writer
         (void)hipSetDevice(d.id);
         int r = 0;
-        if (ok || !d.faulted) {
+        if (ok || !d.faulted) {  // the wait runs without the device lock
           const hipError_t e = wait_stream(d, ln.stream);
           if (e != hipSuccess) {
             if (e != hipErrorNotReady) set_error("hipStreamSynchronize", e);
             r = wait_rc(e);
           }
         }
-        if (ok && r == 0) {
-          std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
-          if (ctx->stats) collect_stats(ctx, d, ln.stream);
-        }
+        if (ok && r == 0) std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
         // the chunk's copies are done (its stream waited on every part's copy)
         if (r == 0 && (ok || !d.faulted)) ln.unpin();
+        std::lock_guard<std::mutex> lk(d.mu);
+        if (ok && r == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
         ln.n = 0;
         return r;
       },
       [&](uint32_t s, uint32_t lane, uint32_t c0, uint32_t c1) -> int {
         Device &d = *ctx->devs[s];
-        HostLane &ln = d.lane[lane];
+        HostLane &ln = d.lane[claims.lane[s][lane]];
         (void)hipSetDevice(d.id);
+        std::lock_guard<std::mutex> lk(d.mu);  // key cache, device scratch, workspaces
+        if (d.faulted) return faulted_rc(d);
         const int r = stage_and_launch(ctx, flags, d, ln, sch, kind, pk, sig, msg, msg_off, c0, c1, vs);
         if (r == 0) {
           ln.lo = c0;
