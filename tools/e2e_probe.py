@@ -49,8 +49,29 @@ def main():
     m = statistics.median(ts[2:])
     env = {k: v for k, v in os.environ.items() if k.startswith("TMV_")}
     h2d = pk.nbytes + sig.nbytes + msg.nbytes + off.nbytes
-    print(json.dumps({"env": env, "n": n, "median_ms": round(m * 1e3, 3), "e2e_verifies_per_s": round(n / m),
-                      "h2d_GBps": round(h2d / m / 1e9, 2), "metrics": ctx.metrics()}))
+    line = {"env": env, "n": n, "median_ms": round(m * 1e3, 3), "e2e_verifies_per_s": round(n / m),
+            "h2d_GBps": round(h2d / m / 1e9, 2)}
+    # TMV_E2E_CALLERS=C: C threads, each calling 4 times on its own copy of
+    # the batch (each call claims its own lanes)
+    callers = int(os.environ.get("TMV_E2E_CALLERS", "1"))
+    if callers > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        copies = [(pk, sig, msg, off)] + [(pk.copy(), sig.copy(), msg.copy(), off.copy()) for _ in range(callers - 1)]
+
+        def caller(b, calls=4):
+            for _ in range(calls):
+                _, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, *b)
+                assert int((st == 1).sum()) == n // 10_000 * 9950
+
+        with ThreadPoolExecutor(callers) as ex:
+            list(ex.map(lambda b: caller(b, 1), copies))
+            t = time.perf_counter()
+            list(ex.map(caller, copies))
+            dt = time.perf_counter() - t
+        line.update({"callers": callers, "callers_verifies_per_s": round(4 * callers * n / dt),
+                     "callers_h2d_GBps": round(4 * callers * h2d / dt / 1e9, 2)})
+    line["metrics"] = ctx.metrics()
+    print(json.dumps(line))
 
 
 if __name__ == "__main__":
