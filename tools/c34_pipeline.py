@@ -20,6 +20,8 @@ ap.add_argument("--blocks", type=int, default=10_000)
 ap.add_argument("--only", default="3,4")
 ap.add_argument("--modes", default="seq,thr2,seq,thr2")
 ap.add_argument("--python", action="store_true", help="also the Python drivers at depth 1 / 2")
+ap.add_argument("--c3-window", type=int, default=1000, help="headers per tmv_light_verify_many call")
+ap.add_argument("--c4-window", type=int, default=600, help="blocks per tmv_verify_commits call")
 a = ap.parse_args()
 only = set(a.only.split(","))
 ctx = N.Context(1)
@@ -58,11 +60,12 @@ if "3" in only:
     period, now = 10**15, (blocks[-1].signed_header.header.time[0] + 1, 0)
     chains.verify_sequential(ctx, trusted, blocks[:50], period, now)  # warm
     pj = []
-    for lo in range(0, len(blocks), 1000):
-        prev = [trusted] + blocks[lo:lo + 999] if lo == 0 else blocks[lo - 1:lo + 999]
+    W3 = a.c3_window
+    for lo in range(0, len(blocks), W3):
+        prev = [trusted] + blocks[lo:lo + W3 - 1] if lo == 0 else blocks[lo - 1:lo + W3 - 1]
         pj.append(H.PreparedLightJobs([H.LightJob(p.signed_header, None, lb.signed_header, lb.vals, period, now,
                                                   mode=H.LIGHT_ADJACENT)
-                                       for p, lb in zip(prev, blocks[lo:lo + 1000])]))
+                                       for p, lb in zip(prev, blocks[lo:lo + W3])]))
     if a.python:
         py_driver("C3 python driver, windows of 1000",
                   lambda d: chains.verify_sequential(ctx, trusted, blocks, period, now, window=1000, depth=d),
@@ -74,7 +77,7 @@ if "3" in only:
             continue
         dt, res = timed(run, pj, mode)
         assert all(k == 0 for r in res for k, _ in r)
-        print(json.dumps({"config": f"C3 {len(blocks)} headers x 100 vals, windows of 1000", "mode": mode,
+        print(json.dumps({"config": f"C3 {len(blocks)} headers x 100 vals, windows of {W3}", "mode": mode,
                           "seconds": round(dt, 4), "headers_per_s": round(len(blocks) / dt, 1)}), flush=True)
 
 if "4" in only:
@@ -91,7 +94,8 @@ if "4" in only:
         jobs.append(H.CommitJob(H.MODE_LIGHT, "test_chain_id", vals, f.block_id, f.height, s2.last_commit))
         jobs.append(H.CommitJob(H.MODE_FULL, "test_chain_id", vals, blocks[i - 1].block_id, f.height - 1,
                                 f.last_commit))
-    pj = [H.PreparedJobs(jobs[lo:lo + 1200]) for lo in range(0, len(jobs), 1200)]
+    W4 = 2 * a.c4_window
+    pj = [H.PreparedJobs(jobs[lo:lo + W4]) for lo in range(0, len(jobs), W4)]
     whole = H.PreparedJobs(jobs)
     for mode in a.modes.split(","):
         if mode == "whole":
@@ -101,5 +105,5 @@ if "4" in only:
             dt, res = timed(lambda p: H.run_prepared_jobs(ctx, p), pj, mode)
             wins = pj
         assert all(e is None for p in wins for e in p.decode())
-        print(json.dumps({"config": f"C4 {a.blocks} blocks x 175 vals, windows of 600 blocks", "mode": mode,
+        print(json.dumps({"config": f"C4 {a.blocks} blocks x 175 vals, windows of {a.c4_window} blocks", "mode": mode,
                           "seconds": round(dt, 4), "blocks_per_s": round((len(blocks) - 2) / dt, 1)}), flush=True)
