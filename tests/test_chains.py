@@ -87,6 +87,22 @@ def test_in_order_yields_in_window_order_and_stops():
     assert max(started) <= 4 + 3  # at most `depth` windows started past it
 
 
+def test_in_order_propagates_a_window_error_in_order():
+    """An engine error in window k surfaces when window k's result is
+    consumed (earlier windows' results first), whatever the depth."""
+    def run(w):
+        if w == 3:
+            raise RuntimeError("engine failed on window 3")
+        return w
+
+    for depth in (1, 2, 3):
+        got = []
+        with pytest.raises(RuntimeError, match="window 3"):
+            for r in chains.in_order(iter(range(8)), run, depth):
+                got.append(r)
+        assert got == [0, 1, 2]
+
+
 @pytest.mark.parametrize("what", ["sig", "next_vals_hash", "vals_hash", "header_field", "chain_id", "expired",
                                   "future", "time_order"])
 def test_sequential_first_error_matches_oracle(fake, what):
