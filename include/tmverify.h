@@ -41,7 +41,11 @@ extern "C" {
 /* A device wait exceeded $TMV_DEVICE_TIMEOUT_MS (default 60000; 0 = wait
  * forever).  The context's device work is then in an unknown state: the
  * context refuses further work (every call returns TMV_ERR_TIMEOUT); the
- * caller verifies on the CPU and may tmv_close / tmv_open a new context. */
+ * caller verifies on the CPU and may tmv_close / tmv_open a new context.
+ * Pages of the caller's input buffers that a streamed call had registered
+ * for direct DMA (TMV_REGISTER) stay page-locked after a failed call: the
+ * device may still read them, so they are never unregistered under it (and
+ * the library keeps no record that could unregister them once reused). */
 #define TMV_ERR_TIMEOUT (-5)
 
 /* Per-entry sr25519 status (tmv_sr25519_verify_batch, tmv_verify_mixed_batch):
@@ -58,11 +62,17 @@ typedef struct tmv_ctx tmv_ctx;
 
 /* Open a context on the GPUs selected by device_mask (bit i = HIP device i;
  * 0 = all visible devices).  Builds the per-device base-point tables.
- * Returns NULL on failure (tmv_last_error() says why). */
+ * Returns NULL on failure (tmv_last_error() says why).
+ * Test aid: with TMV_LOGICAL_DEVICES=k in the environment each selected GPU
+ * joins the context as k devices (own streams, lanes, workspaces, key cache),
+ * so the multi-device shard path runs on one GPU. */
 tmv_ctx *tmv_open(uint32_t device_mask);
 void tmv_close(tmv_ctx *ctx);
 int tmv_num_devices(const tmv_ctx *ctx);
 const char *tmv_last_error(void);
+/* "tmverify-mi355x <ver> (gfx950) src=<digest> git=<head>": the source digest
+   (tendermint_amd/csrc/src_digest.py over the sources this library is built
+   from) and the git HEAD compiled in by the Makefile. */
 const char *tmv_version(void);
 
 /* ed25519 batch verification with ZIP-215 semantics.
@@ -198,7 +208,9 @@ typedef struct tmv_metrics {
   uint64_t max_batch;           /* largest call, in entries */
   uint64_t batch_eq_signatures; /* entries verified through the batch equation */
   uint64_t host_signatures;     /* entries of host-buffer calls */
-  double host_seconds;          /* wall time inside host-buffer calls (end-to-end rate = host_signatures / it) */
+  double host_seconds;          /* busy wall time of host-buffer calls: the union of their intervals, so calls
+                                   in flight together count once (end-to-end rate = host_signatures / it);
+                                   a call still in flight is not yet counted */
   uint64_t h2d_bytes;           /* host-to-device bytes of host-buffer calls (zero-copy reads not counted) */
   uint64_t d2h_bytes;           /* device-to-host bytes of host-buffer calls */
   uint64_t groups;              /* batch-equation groups checked (TMV_BATCHOPT_STATS) */

@@ -165,6 +165,28 @@ def last_error() -> str:
     return lib().tmv_last_error().decode(errors="replace")
 
 
+def version() -> str:
+    """tmv_version(): the library's version with its build id (source
+    digest and git HEAD compiled in by csrc/Makefile)."""
+    return lib().tmv_version().decode(errors="replace")
+
+
+def build_info() -> dict:
+    """The loaded library's build id against the sources of this tree:
+    src_match says whether libtmgpu.so was compiled from them
+    (csrc/src_digest.py computes the same digest the Makefile compiled in)."""
+    import importlib.util
+    v = version()
+    fields = dict(kv.split("=", 1) for kv in v.split() if "=" in kv)
+    spec = importlib.util.spec_from_file_location("tmv_src_digest", os.path.join(_HERE, "csrc", "src_digest.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    tree = mod.digest()
+    return {"version": v, "src_digest_compiled": fields.get("src"), "src_digest_tree": tree,
+            "src_match": fields.get("src") == tree, "git_head_compiled": fields.get("git"),
+            "library": LIB_PATH}
+
+
 def _p(a: np.ndarray, t=ctypes.c_uint8):
     return a.ctypes.data_as(ctypes.POINTER(t))
 

@@ -74,8 +74,9 @@ class Partner {
 };
 }  // namespace
 
-int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), void *ctx) {
+int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), void *ctx, uint32_t *fail_lo) {
   const uint32_t target = host_slice_jobs();
+  if (fail_lo) *fail_lo = 0;
   if (!target || n_jobs < 2 * target) return run_slice(ctx, 0, n_jobs);
   // one partner per process: concurrent sliced calls queue for it (the
   // second caller runs its slices alone)
@@ -87,6 +88,11 @@ int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), vo
   const uint32_t ns = (n_jobs + target - 1) / target, per = (n_jobs + ns - 1) / ns;
   std::atomic<uint32_t> next{0};
   std::atomic<int> bad{0}, err{0};
+  // the first failing slice's message and first job (its thread's last
+  // error is thread-local: the caller reads its own after the join)
+  std::mutex emu;
+  std::string emsg;
+  uint32_t elo = 0;
   auto work = [&] {
     for (uint32_t k; (k = next.fetch_add(1)) < ns;) {
       const uint32_t lo = k * per, hi = std::min(n_jobs, lo + per);
@@ -94,7 +100,11 @@ int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), vo
       const int r = run_slice(ctx, lo, hi);
       if (r < 0) {
         int z = 0;
-        err.compare_exchange_strong(z, r);
+        if (err.compare_exchange_strong(z, r)) {
+          std::lock_guard<std::mutex> lk(emu);
+          emsg = tmv_last_error();
+          elo = lo;
+        }
       } else {
         bad.fetch_add(r);
       }
@@ -103,7 +113,13 @@ int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), vo
   if (own.owns_lock()) partner->post(work);
   work();
   if (own.owns_lock()) partner->wait();
-  return err.load() ? err.load() : bad.load();
+  if (err.load()) {
+    std::lock_guard<std::mutex> lk(emu);
+    tmv_internal_set_error(emsg.c_str());
+    if (fail_lo) *fail_lo = elo;
+    return err.load();
+  }
+  return bad.load();
 }
 
 void put_err(char *err, size_t cap, const std::string &s) {
@@ -684,13 +700,14 @@ int tmv_verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs
     char *errs;
     size_t stride;
   } c{ctx, jobs, results, errs, err_stride};
+  uint32_t fail_lo = 0;
   const int rc = run_sliced(n_jobs, [](void *p, uint32_t lo, uint32_t hi) {
     const Call &c = *static_cast<const Call *>(p);
-    const int r = verify_commits(c.ctx, c.jobs + lo, hi - lo, c.results ? c.results + lo : nullptr,
-                                 c.errs && c.stride ? c.errs + (size_t)lo * c.stride : nullptr, c.stride, nullptr);
-    if (r < 0 && lo && c.errs && c.stride) std::memcpy(c.errs, c.errs + (size_t)lo * c.stride, c.stride);
-    return r;
-  }, &c);
+    return verify_commits(c.ctx, c.jobs + lo, hi - lo, c.results ? c.results + lo : nullptr,
+                          c.errs && c.stride ? c.errs + (size_t)lo * c.stride : nullptr, c.stride, nullptr);
+  }, &c, &fail_lo);
+  // an infrastructure error's text goes to errs[0] (after every slice ended)
+  if (rc < 0 && fail_lo && errs && err_stride) std::memcpy(errs, errs + (size_t)fail_lo * err_stride, err_stride);
   return rc;
 }
 

@@ -15,6 +15,11 @@
 #include "pool.h"
 #include "tm_types.h"
 
+// Sets the calling thread's tmv_last_error() text (defined by the runtime,
+// and by the CPU test double); the host layer moves a worker thread's error
+// to the caller's thread with it.
+extern "C" void tmv_internal_set_error(const char *msg);
+
 namespace tmh_internal {
 
 // Phase timing of a host-layer call, printed to stderr when the environment
@@ -78,6 +83,12 @@ uint32_t host_slice_jobs();
 // k verifies.  Every job's result is its own (sharing only saves work), so
 // slicing changes no result.  Returns the sum of the slices' returns, or the
 // first negative one.
-int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), void *ctx);
+// Returns the first infrastructure error (< 0) of any slice, else the sum of
+// the slices' results.  On an error its slice's message (tmv_last_error on
+// the thread that ran it) becomes the caller thread's last error, and
+// *fail_lo (if given) is that slice's first job, read after every slice
+// has finished.
+int run_sliced(uint32_t n_jobs, int (*run_slice)(void *, uint32_t, uint32_t), void *ctx,
+               uint32_t *fail_lo = nullptr);
 
 }  // namespace tmh_internal

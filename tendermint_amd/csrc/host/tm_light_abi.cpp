@@ -173,13 +173,15 @@ int tmv_light_verify_many(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jo
     char *errs;
     size_t stride;
   } c{ctx, jobs, results, errs, err_stride};
-  return run_sliced(n_jobs, [](void *p, uint32_t lo, uint32_t hi) {
+  uint32_t fail_lo = 0;
+  const int rc = run_sliced(n_jobs, [](void *p, uint32_t lo, uint32_t hi) {
     const Call &c = *static_cast<const Call *>(p);
-    const int r = light_verify_slice(c.ctx, c.jobs + lo, hi - lo, c.results ? c.results + lo : nullptr,
-                                     c.errs && c.stride ? c.errs + (size_t)lo * c.stride : nullptr, c.stride);
-    if (r < 0 && lo && c.errs && c.stride) std::memcpy(c.errs, c.errs + (size_t)lo * c.stride, c.stride);
-    return r;
-  }, &c);
+    return light_verify_slice(c.ctx, c.jobs + lo, hi - lo, c.results ? c.results + lo : nullptr,
+                              c.errs && c.stride ? c.errs + (size_t)lo * c.stride : nullptr, c.stride);
+  }, &c, &fail_lo);
+  // an infrastructure error's text goes to errs[0] (after every slice ended)
+  if (rc < 0 && fail_lo && errs && err_stride) std::memcpy(errs, errs + (size_t)fail_lo * err_stride, err_stride);
+  return rc;
 }
 
 }  // extern "C"

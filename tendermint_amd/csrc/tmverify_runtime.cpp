@@ -212,8 +212,11 @@ constexpr int kLanes = 4;  // streams per device; TMV_HOST_LANES of them carry c
 
 struct Device {
   int id = -1;
+  // device-pointer entry points called with stream = NULL run here; the host
+  // lanes have streams of their own, so such a call never shares a lane's
+  // stream (or its workspace) with a host-buffer call in flight
   hipStream_t stream = nullptr;
-  HostLane lane[kLanes];  // lane[0].stream == stream
+  HostLane lane[kLanes];
   tmv::ge_precomp *d_btable = nullptr;   // 32x8 comb (single-lane kernel)
   tmv::fe *d_btab_q = nullptr;           // 8 x CachedQ multiples of B (quad kernel)
   tmv::strobe_t *d_prefix = nullptr;     // sr25519 transcript prefix (empty context)
@@ -483,6 +486,24 @@ struct tmv_ctx {
       m_located{0}, m_fallback{0};
   uint64_t khits_base = 0, kmiss_base = 0;
   std::mutex opt_mu;
+  // m_host_ns is busy wall time: the union of the host-buffer calls'
+  // intervals (calls overlap -- lane claims, windows in flight -- so summing
+  // each call's duration would count shared time more than once)
+  std::mutex host_mu;
+  uint32_t host_inflight = 0;
+  std::chrono::steady_clock::time_point host_t0;
+
+  void host_enter() {
+    std::lock_guard<std::mutex> lk(host_mu);
+    if (host_inflight++ == 0) host_t0 = std::chrono::steady_clock::now();
+  }
+  void host_leave(uint64_t n) {
+    std::lock_guard<std::mutex> lk(host_mu);
+    m_host_sigs += n;
+    if (--host_inflight == 0)
+      m_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                       std::chrono::steady_clock::now() - host_t0).count();
+  }
 
   void count_call(uint64_t n) {
     m_calls++;
@@ -598,8 +619,7 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
   if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
-  d.lane[0].stream = d.stream;
-  for (int l = 1; l < kLanes; l++) {
+  for (int l = 0; l < kLanes; l++) {
     e = hipStreamCreateWithFlags(&d.lane[l].stream, hipStreamNonBlocking);
     if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
   }
@@ -1084,7 +1104,7 @@ int tmv_kernel_timing_read(tmv_ctx *ctx, const char *kernel, double *total_ms, u
 }
 
 const char *tmv_last_error(void) { return g_last_error.c_str(); }
-const char *tmv_version(void) { return "tmverify-mi355x 0.1 (gfx950)"; }
+void tmv_internal_set_error(const char *msg) { g_last_error = msg ? msg : ""; }
 
 tmv_ctx *tmv_open(uint32_t device_mask) {
   int count = 0;
@@ -1094,13 +1114,25 @@ tmv_ctx *tmv_open(uint32_t device_mask) {
                               : std::string("no HIP device visible"));
     return nullptr;
   }
+  // TMV_LOGICAL_DEVICES=k (test aid, read on every open): each selected GPU
+  // joins the context as k devices -- own streams, lanes, workspaces and key
+  // cache -- so the multi-device shard / launch / harvest path of run_batch
+  // runs on real streams on a one-GPU box.  Device-pointer entry points name
+  // a GPU by its HIP id and reach its first logical device.
+  int logical = 1;
+  if (const char *lg = getenv("TMV_LOGICAL_DEVICES")) logical = std::max(1, std::min(8, atoi(lg)));
   auto ctx = std::make_unique<tmv_ctx>();
   for (int i = 0; i < count && i < 32; i++) {
     if (device_mask != 0 && !(device_mask & (1u << i))) continue;
-    auto d = std::make_unique<Device>();
-    d->id = i;
-    if (init_device(*d) != 0) return nullptr;
-    ctx->devs.push_back(std::move(d));
+    for (int k = 0; k < logical; k++) {
+      auto d = std::make_unique<Device>();
+      d->id = i;
+      if (init_device(*d) != 0) {
+        tmv_close(ctx.release());
+        return nullptr;
+      }
+      ctx->devs.push_back(std::move(d));
+    }
   }
   if (ctx->devs.empty()) {
     set_error("device_mask selects no visible device");
@@ -1114,6 +1146,7 @@ void tmv_close(tmv_ctx *ctx) {
   for (auto &d : ctx->devs) {
     (void)hipSetDevice(d->id);
     if (d->faulted) continue;  // work still running on its buffers: leak them rather than free them under it
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (HostLane &l : d->lane) {
       if (l.stream) (void)hipStreamSynchronize(l.stream);
       if (l.copy) (void)hipStreamSynchronize(l.copy);
@@ -1158,7 +1191,7 @@ void tmv_close(tmv_ctx *ctx) {
     if (d->work_done) (void)hipEventDestroy(d->work_done);
     if (d->kbuild_copied) (void)hipEventDestroy(d->kbuild_copied);
     if (d->d_btable) (void)hipFree(d->d_btable);
-    for (int l = 1; l < kLanes; l++)
+    for (int l = 0; l < kLanes; l++)
       if (d->lane[l].stream) (void)hipStreamDestroy(d->lane[l].stream);
     if (d->stream) (void)hipStreamDestroy(d->stream);
   }
@@ -1337,6 +1370,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       const bool drained = wait_stream(d, ln.copy) == hipSuccess;
       if (ln.helper) (void)wait_stream(d, ln.helper);
       if (wait_stream(d, ln.stream) == hipSuccess && drained) ln.unpin();
+      else ln.pinned.clear();  // copies may be in flight: leave the pages registered (see run_batch)
       return rc;
     }
     if (tm.on) fprintf(stderr, "[tmv_engine] pinning %9.3f ms (%zu ranges)\n", pin_ms, ln.pinned.size());
@@ -1496,17 +1530,12 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   }
   read_env();
   ctx->count_call(n);
-  const auto t_call = std::chrono::steady_clock::now();
-  struct HostTime {  // wall time of the call into tmv_metrics, on every return
+  ctx->host_enter();
+  struct HostTime {  // busy wall time of host-buffer calls into tmv_metrics, on every return
     tmv_ctx *c;
     uint32_t n;
-    std::chrono::steady_clock::time_point t;
-    ~HostTime() {
-      c->m_host_sigs += n;
-      c->m_host_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                          std::chrono::steady_clock::now() - t).count();
-    }
-  } host_time{ctx, n, t_call};
+    ~HostTime() { c->host_leave(n); }
+  } host_time{ctx, n};
   // streamed batch-equation chunks are large (one pipeline, one tail each);
   // other paths alternate smaller chunks over the lanes
   const uint32_t per_dev = n / (uint32_t)ctx->devs.size();
@@ -1568,8 +1597,13 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
           }
         }
         if (ok && r == 0) std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
-        // the chunk's copies are done (its stream waited on every part's copy)
+        // the chunk's copies are done (its stream waited on every part's copy);
+        // if they may not be (a failed or skipped wait), the caller's pages
+        // stay registered and only the records are dropped: unregistering
+        // under a DMA in flight, or later, after the caller freed the
+        // memory, would be worse (include/tmverify.h, TMV_ERR_TIMEOUT)
         if (r == 0 && (ok || !d.faulted)) ln.unpin();
+        else ln.pinned.clear();
         std::lock_guard<std::mutex> lk(d.mu);
         if (ok && r == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
         ln.n = 0;

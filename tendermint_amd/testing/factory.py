@@ -145,9 +145,10 @@ def random_block_id(rng: random.Random) -> BlockID:
                    PartSetHeader(rng.randrange(1, 1 << 16), bytes(rng.randrange(256) for _ in range(32))))
 
 
-def make_c2_batch(n: int = 10_000, seed: int = 0xED25519, chain_id: str = "test_chain_id",
-                  edge_scale: float = 1.0) -> Batch:
-    """Config 2: n ed25519 signatures over commit-vote sign-bytes, 1% edge cases."""
+C2_VALID_KINDS = ("honest", "small_order", "noncanonical_y", "neg_zero")  # valid under ZIP-215
+
+
+def _c2_plan(n: int, seed: int, edge_scale: float):
     rng = random.Random(seed)
     counts = {"bitflip": 20, "s_plus_l": 15, "undecodable": 15, "small_order": 20,
               "noncanonical_y": 15, "neg_zero": 15}
@@ -157,6 +158,21 @@ def make_c2_batch(n: int = 10_000, seed: int = 0xED25519, chain_id: str = "test_
         kinds += [k] * c
     kinds += ["honest"] * (n - len(kinds))
     rng.shuffle(kinds)
+    return rng, counts, kinds
+
+
+def c2_kinds(n: int = 10_000, seed: int = 0xED25519, edge_scale: float = 1.0) -> List[str]:
+    """The per-entry kinds make_c2_batch(n, seed) assigns, without signing
+    anything: its exact validity vector is [k in C2_VALID_KINDS for k in
+    c2_kinds(...)] (bench.py's strong-scaling leg checks a gathered 1M
+    vector on every rank against it)."""
+    return _c2_plan(n, seed, edge_scale)[2]
+
+
+def make_c2_batch(n: int = 10_000, seed: int = 0xED25519, chain_id: str = "test_chain_id",
+                  edge_scale: float = 1.0) -> Batch:
+    """Config 2: n ed25519 signatures over commit-vote sign-bytes, 1% edge cases."""
+    rng, counts, kinds = _c2_plan(n, seed, edge_scale)
     block_id = random_block_id(rng)
     base_secs = 1577836800  # 2020-01-01T00:00:00Z
     undec = undecodable_encodings(counts.get("undecodable", 0) or 1, rng)

@@ -10,7 +10,10 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <atomic>
+#include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tmhost.h"
@@ -76,9 +79,12 @@ extern "C" {
 int commitcheck_backend_calls = 0;
 int commitcheck_entries_verified = 0;
 int g_skip_hash = 0;  // timing of the host layer alone (tools only)
-int g_fail_next = 0;  // the next device call returns this infrastructure error (e.g. TMV_ERR_TIMEOUT)
+// the next device call returns this infrastructure error (e.g.
+// TMV_ERR_TIMEOUT), on whichever thread makes it, and leaves a message
+// naming that thread as its last error
+std::atomic<int> g_fail_next{0};
 
-void commitcheck_fail_next(int rc) { g_fail_next = rc; }
+void commitcheck_fail_next(int rc) { g_fail_next.store(rc); }
 
 // tmh::poll_until (host/wait.h, the runtime's bounded device waits) against a
 // query that completes after `ready_after` polls (< 0: never) or fails.
@@ -94,7 +100,19 @@ int commitcheck_poll(int ready_after, int fail, int64_t timeout_ms, double *elap
   return (int)r;
 }
 
-const char *tmv_last_error(void) { return "fake device error"; }
+static thread_local std::string g_fake_error;
+const char *tmv_last_error(void) { return g_fake_error.empty() ? "fake device error" : g_fake_error.c_str(); }
+void tmv_internal_set_error(const char *msg) { g_fake_error = msg ? msg : ""; }
+static int take_failure() {
+  const int rc = g_fail_next.exchange(0);
+  if (rc) {
+    char buf[96];
+    snprintf(buf, sizeof(buf), "fake infrastructure error on thread %zx",
+             std::hash<std::thread::id>()(std::this_thread::get_id()));
+    g_fake_error = buf;
+  }
+  return rc;
+}
 
 // Simulated devices: a context of g_devices devices runs every batch through
 // the runtime's shard plan and launch / harvest order (host/shard_plan.h,
@@ -154,7 +172,7 @@ extern "C" {
 
 int tmv_verify_batch_ex(tmv_ctx *, uint8_t key_kind, uint32_t, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *msg, const uint32_t *msg_off, uint32_t n, int8_t *status_out) {
-  if (g_fail_next) { const int rc = g_fail_next; g_fail_next = 0; return rc; }
+  if (const int rc = take_failure()) return rc;
   commitcheck_backend_calls++;
   commitcheck_entries_verified += (int)n;
   run_devices(n, status_out, [&](uint32_t i) -> int8_t {
@@ -194,7 +212,7 @@ static Bytes vote_message(const tmv_vote_template &t, const tmv_vote &v) {
 
 int tmv_verify_votes(tmv_ctx *, uint8_t key_kind, uint32_t, const tmv_vote_template *tmpl, uint32_t n_tmpl,
                      const tmv_vote *votes, const uint8_t *pk, const uint8_t *sig, uint32_t n, int8_t *status_out) {
-  if (g_fail_next) { const int rc = g_fail_next; g_fail_next = 0; return rc; }
+  if (const int rc = take_failure()) return rc;
   commitcheck_backend_calls++;
   commitcheck_entries_verified += (int)n;
   for (uint32_t i = 0; i < n; i++)

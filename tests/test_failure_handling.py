@@ -75,3 +75,37 @@ def test_timeout_surfaces_from_light_verify(fake):
             fake.light_verify_many([job])
     finally:
         fake.real_signatures(False)
+
+
+def test_sliced_call_error_reaches_caller_thread(fake, monkeypatch):
+    """a sliced call (TMV_HOST_SLICE) whose failing slice ran on
+    the partner thread still returns that slice's infrastructure error, with
+    its message as the caller thread's last error and in errs[0] (copied
+    after every slice has finished, so no slice's own error text races it)."""
+    import numpy as np
+    monkeypatch.setenv("TMV_HOST_SLICE", "4")
+    fake.L.tmv_last_error.restype = ctypes.c_char_p
+    L = fake.L
+    L.commitcheck_verify_commits.argtypes = [ctypes.POINTER(H.CCommitJob), ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p, ctypes.c_size_t]
+    L.commitcheck_verify_commits.restype = ctypes.c_int
+    jobs = F.random_jobs("fake", 32, seed=11)
+    pj = H.PreparedJobs(jobs)
+    seen = set()
+    for _ in range(12):  # the failing call lands on either thread; both must report it
+        fake.L.commitcheck_fail_next(TMV_ERR_TIMEOUT)
+        rc = L.commitcheck_verify_commits(pj.arr, pj.n, pj.results, pj.errs, pj.stride)
+        assert rc == TMV_ERR_TIMEOUT
+        msg = fake.L.tmv_last_error().decode()
+        assert msg.startswith("fake infrastructure error on thread"), msg
+        raw = ctypes.string_at(pj.errs, pj.stride)
+        assert raw.split(b"\0")[0].decode() == msg
+        seen.add(msg)
+    # a clean call after the failures: results equal a one-slice run's
+    ok = L.commitcheck_verify_commits(pj.arr, pj.n, pj.results, pj.errs, pj.stride)
+    sliced = pj.decode()
+    monkeypatch.setenv("TMV_HOST_SLICE", "0")
+    pj1 = H.PreparedJobs(jobs)
+    assert L.commitcheck_verify_commits(pj1.arr, pj1.n, pj1.results, pj1.errs, pj1.stride) == ok >= 0
+    assert pj1.decode() == sliced
+    assert len(seen) >= 1 and np.all(np.asarray([len(s) for s in seen]) > 0)

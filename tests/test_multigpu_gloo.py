@@ -129,7 +129,7 @@ def test_bench_control_flow_world2():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"), "--gpus", "2",
            "--steps", "7", "--warmup", "2", "--batch", "500", "--resident", "3", "--inflight", "2",
-           "--batches-per-step", "3", "--cpu-stub"]
+           "--batches-per-step", "3", "--cpu-stub", "--strong-n", "4003"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=repo)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -140,3 +140,11 @@ def test_bench_control_flow_world2():
     # value = every rank's signatures: 2 ranks x 7 steps x 3 batches x 500
     assert abs(r["value"] * r["ms_per_step"] * 7e-3 / (2 * 7 * 3 * 500) - 1) < 1e-3
     assert "STUB" in r["data"]
+    # the strong-scaling legs: one 4,003-signature batch (ed25519) and one
+    # mixed batch split over both ranks, gathered and checked on every rank
+    for leg in ("strong_1m", "strong_1m_mixed"):
+        s = r[leg]
+        assert s["signatures"] == 4003 and s["ranks"] == 2 and s["shard_per_rank"] == [2001, 2002]
+        assert s["exact_vector_on_every_rank"] is True
+        assert s["kernel_only"]["verifies_per_s"] > 0 and s["end_to_end"]["verifies_per_s"] > 0
+    assert r["end_to_end_verifies_per_s"] > 0 and "end_to_end_vs_headline" in r
