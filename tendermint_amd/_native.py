@@ -13,7 +13,9 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libtmgpu.so")
+# TMV_LIB_PATH: an A/B build of the same library (tools/build_ab.sh) for
+# measurement runs; the default is the in-tree build
+LIB_PATH = os.environ.get("TMV_LIB_PATH") or os.path.join(_HERE, "_build", "libtmgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tmverify.h")
 HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(_HERE), "include", "tmhost.h")]
 

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -235,19 +236,28 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
   std::vector<const tmh::ValidatorSet *> vq(vsets.size(), nullptr);
   for (size_t i = 0; i < vsets.size(); i++)
     if (need_v[i]) vq[i] = vsets[i].get();
+  // The hashes run beside the signature checks: Header.Hash and
+  // ValidatorSet.Hash only decide two comparisons in PlanLight (the commit's
+  // BlockID hash, the header's ValidatorsHash), so every job is first planned
+  // as if both matched -- the hashes the header claims -- and its commit
+  // checks are verified while a helper thread hashes; a job whose real hashes
+  // differ ends in PlanLight's early error (ahead of any commit check in the
+  // reference's order) and its speculative commit results are dropped.  A job
+  // whose hashes match has exactly the speculative plan.
   std::vector<tmh::Bytes> hh, vh;
-  int rc = header_hashes(ctx, hq, hh);
-  tm.mark("hdr hash");
-  if (rc >= 0) rc = valset_hashes(ctx, vq, V.src, vh);
-  tm.mark("vs hash");
-  if (rc < 0) {
-    if (errs && err_stride) put_err(errs, err_stride, tmv_last_error());
-    return rc;
-  }
-  // non-signature checks, in the reference's order
+  int hrc = 0;
+  std::string hash_error;
+  std::thread hasher([&] {
+    hrc = header_hashes(ctx, hq, hh);
+    if (hrc >= 0) hrc = valset_hashes(ctx, vq, V.src, vh);
+    if (hrc < 0) hash_error = tmv_last_error();
+  });
+  struct Join {
+    std::thread &t;
+    ~Join() { if (t.joinable()) t.join(); }
+  } join_hasher{hasher};
   static const tmh::Bytes kNone;
-  std::vector<tmh::LightPlan> plans(n_jobs);
-  parallel_for(n_jobs, 16, [&](size_t j) {
+  auto light_job = [&](uint32_t j) {
     const tmv_light_job &jb = jobs[j];
     const Ref &r = refs[j];
     tmh::LightJob lj;
@@ -263,7 +273,18 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
     lj.max_clock_drift_ns = jb.max_clock_drift_ns;
     lj.trust_num = jb.trust_num;
     lj.trust_den = jb.trust_den;
-    plans[j] = tmh::PlanLight(lj, r.uh == UINT32_MAX ? kNone : hh[r.uh], r.uv == UINT32_MAX ? kNone : vh[r.uv]);
+    return lj;
+  };
+  // speculative plans: the hashes the untrusted header and commit claim
+  std::vector<tmh::LightPlan> plans(n_jobs);
+  parallel_for(n_jobs, 16, [&](size_t j) {
+    const tmh::LightJob lj = light_job((uint32_t)j);
+    tmh::Bytes claim_h, claim_v;
+    if (lj.untrusted.commit) claim_h.assign(lj.untrusted.commit->block_id.hash.begin(),
+                                            lj.untrusted.commit->block_id.hash.end());
+    if (lj.untrusted.header) claim_v.assign(lj.untrusted.header->validators_hash.begin(),
+                                            lj.untrusted.header->validators_hash.end());
+    plans[j] = tmh::PlanLight(lj, claim_h, claim_v);
   });
   tm.mark("plan");
   // the commit checks of every job, one signature batch
@@ -294,13 +315,29 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
     conv.commits.reserve(commits.size());
     for (size_t i = 0; i < commits.size(); i++)
       if (commits[i]) conv.commits.emplace(C.src[i], commits[i].get());
-    rc = verify_commits(ctx, cj.data(), (uint32_t)cj.size(), cres.data(), cerr.data(), kStride, cne.data(), &conv);
+    const int rc = verify_commits(ctx, cj.data(), (uint32_t)cj.size(), cres.data(), cerr.data(), kStride, cne.data(),
+                                  &conv);
     if (rc < 0) {
       if (errs && err_stride) put_err(errs, err_stride, std::string(cerr.data()));
       return rc;
     }
   }
   tm.mark("commits");
+  hasher.join();
+  tm.mark("hashes joined");
+  if (hrc < 0) {
+    tmv_internal_set_error(hash_error.c_str());
+    if (errs && err_stride) put_err(errs, err_stride, hash_error);
+    return hrc;
+  }
+  // the real plans; a job whose hashes differ from the claimed ones now
+  // carries its early error (and none of the speculative checks)
+  parallel_for(n_jobs, 16, [&](size_t j) {
+    const Ref &r = refs[j];
+    const tmh::LightPlan real = tmh::PlanLight(light_job((uint32_t)j), r.uh == UINT32_MAX ? kNone : hh[r.uh],
+                                               r.uv == UINT32_MAX ? kNone : vh[r.uv]);
+    if (real.early) plans[j].early = real.early;
+  });
   int bad = 0;
   for (uint32_t j = 0; j < n_jobs; j++) {
     const size_t k = plans[j].checks.size();

@@ -607,6 +607,27 @@ k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 #define TMV_WPART_WAVES 1
 #endif
 
+// A window sum as k_msm_horner reads it: the top window (Horner's start) as a
+// P3Q point (X, Y, Z, T), every other window already in CachedQ order
+// (Y-X, Y+X, 2dT, Z, carried), so Horner's chain adds it without a
+// to_cached multiply of its own (one field multiplication per window here,
+// on the running-sum lane, instead of one per window on Horner's chain).
+__device__ __forceinline__ void store_window_sum(ge_p3 *dst, const ge_p3 &S, bool top) {
+  if (top) {
+    *dst = S;
+    return;
+  }
+  ge_p3 q;
+  fe t;
+  fe_sub(t, S.Y, S.X);
+  fe_carry(q.X, t);
+  fe_add(t, S.Y, S.X);
+  fe_carry(q.Y, t);
+  fe_mul(q.Z, S.T, consts::d2());
+  q.T = S.Z;
+  *dst = q;
+}
+
 // Window parts: lane (g, w, q) sums buckets [q s, (q+1) s) of window w with
 // the running-sum trick: T = sum_i (i+1) B_{qs+i}, U = sum_i B_{qs+i}.
 __global__ void __launch_bounds__(256, TMV_WPART_WAVES)
@@ -649,8 +670,12 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   }
   if (!u_set) ge_p3_identity(U);
   if (!t_set) ge_p3_identity(T);
-  mw.wpart[2ull * t] = T;
-  if (p.P > 1) mw.wpart[2ull * t + 1] = U;  // P = 1: k_msm_horner reads T only
+  if (p.P > 1) {
+    mw.wpart[2ull * t] = T;
+    mw.wpart[2ull * t + 1] = U;
+  } else {  // T is the window sum: k_msm_horner reads it
+    store_window_sum(&mw.wpart[2ull * t], T, wdx == p.W - 1);
+  }
 }
 
 // Window sums: S_w = sum_q T_q + s * sum_q q U_q (s = H / P).
@@ -673,7 +698,7 @@ k_msm_wsum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   } else {
     acc = wp[0];
   }
-  mw.wsum[t] = acc;
+  store_window_sum(&mw.wsum[t], acc, t - g * p.W == p.W - 1);
 }
 
 // Group verdicts: one quad per group (lane c holds coordinate c), 16 groups
@@ -699,12 +724,11 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
   fe acc = reinterpret_cast<const fe *>(&S[st * (p.W - 1)])[c];
   fe r, q, qc;
   for (int wI = (int)p.W - 2; wI >= 0; wI--) {
+    qc = reinterpret_cast<const fe *>(&S[st * wI])[c];  // CachedQ (store_window_sum), loaded ahead
     for (uint32_t d = 0; d < p.c; d++) {
       quad::dbl(r, acc);
       quad::p1p1_to_p3(acc, r);
     }
-    q = reinterpret_cast<const fe *>(&S[st * wI])[c];
-    quad::to_cached(qc, q);
     quad::add(r, acc, qc);
     quad::p1p1_to_p3(acc, r);
   }

@@ -34,7 +34,38 @@ TMV_DEV void fe_signed(fe &h, const fe &f, int s) {
 }
 
 // h = f^2 << sh (sh in {0, 1}, per lane), carried to level 1
+#ifndef TMV_SQ_BIAS
+#define TMV_SQ_BIAS 1
+#endif
 TMV_DEV void fe_sq_shift(fe &h, const fe &f, int sh) {
+#if TMV_SQ_BIAS
+  // 2^sh f^2 with the left operands taken from f << sh, each column started
+  // at its carry bias by its first product (mad_bias, as fe_sq): no 64-bit
+  // shift of the columns and no bias adds before the carry
+  int32_t g[10], g2[10], f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g[i] = (int32_t)((uint32_t)f.v[i] << sh);
+    g2[i] = 2 * g[i];
+    f19[i] = mul19(f.v[i]);
+  }
+  int64_t c[10];
+  bool started[10] = {false, false, false, false, false, false, false, false, false, false};
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      const int oddodd = (i & 1) && (j & 1);
+      int32_t a = (i == j) ? g[i] : g2[i];
+      if (oddodd) a = 2 * a;
+      const int k = i + j < 10 ? i + j : i + j - 10;
+      const int32_t b = i + j < 10 ? f.v[j] : f19[j];
+      if (!started[k]) { c[k] = mad_bias(a, b, k); started[k] = true; }
+      else c[k] = mad_acc(a, b, c[k]);
+    }
+  }
+  fe_carry_biased(h, c);
+#else
   int32_t f2[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = mul19(f.v[i]); }
@@ -55,6 +86,7 @@ TMV_DEV void fe_sq_shift(fe &h, const fe &f, int sh) {
 #pragma unroll
   for (int k = 0; k < 10; k++) c[k] = c[k] << sh;
   fe_carry_wide(h, c);
+#endif
 }
 
 TMV_DEV int lane4() { return (int)(threadIdx.x & 3); }
@@ -78,7 +110,99 @@ TMV_DEV void p1p1_to_p3(fe &p, const fe &r) {
   fe_mul(p, o1, o2);
 }
 
+// Linear glue with fused DPP operands (TMV_QUAD_GLUE, default): every
+// cross-lane read feeds a VOP2 op directly (v_and / v_xor / v_add _dpp), and a
+// per-lane sign is an XOR with -1 completed by one +1 per negated term in the
+// limb's final add, so a limb of the doubling's glue is 7 instructions and of
+// the addition's 8 (the selects / negations of the older form below took
+// about 20 and 14; the values are identical).
+#ifndef TMV_QUAD_GLUE
+#define TMV_QUAD_GLUE 1
+#endif
+template <int CTRL>
+TMV_DEV int32_t dpp(int32_t x) { return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true); }
+// A lane mask (0 / -1) the compiler cannot see through: an AND with a mask it
+// knows came from a compare becomes a v_cndmask (VOP3, no DPP operand), so
+// the DPP read would stay a separate v_mov_b32_dpp
+TMV_DEV int32_t lane_mask(bool b) {
+  int32_t m = b ? -1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(m));
+#endif
+  return m;
+}
+
+#if TMV_QUAD_GLUE
 // P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
+// E = S3 - S1 - S0, H = S1 + S0, G = S1 - S0, F = S2 - S1 + S0 (all negated
+// relative to dbl-2008-hwcd, same projective point).
+TMV_DEV void dbl(fe &r, const fe &p) {
+  const int c = lane4();
+  const int32_t k3 = lane_mask(c == 3);
+  fe s;
+#pragma unroll
+  for (int i = 0; i < 10; i++)  // X, Y, Z, X + Y (level 2)
+    s.v[i] = dpp<qp(0, 1, 2, 0)>(p.v[i]) + (dpp<qp(1, 1, 1, 1)>(p.v[i]) & k3);
+  fe S;
+  fe_sq_shift(S, s, c == 2 ? 1 : 0);
+  // lane: 0: S3 - S1 - S0, 1: S1 + S0, 2: S2 + S1 - S0, 3: S2 - S1 + S0
+  const int32_t kb = lane_mask(c == 0 || c == 3);  // base S3 (lane 0) / S2 (lane 3)
+  const int32_t m1 = (c == 0 || c == 3) ? -1 : 0;  // -S1
+  const int32_t m0 = (c == 0 || c == 2) ? -1 : 0;  // -S0
+  const int32_t corr = -(m1 + m0);
+#pragma unroll
+  for (int i = 0; i < 10; i++)
+    r.v[i] = (dpp<qp(3, 3, 2, 2)>(S.v[i]) & kb) + (dpp<qp(1, 1, 1, 1)>(S.v[i]) ^ m1) +
+             (dpp<qp(0, 0, 0, 0)>(S.v[i]) ^ m0) + corr;  // level 3
+}
+
+// (Y-X, Y+X, T, Z) of a P3Q point (level 2): the first half of add / to_cached
+TMV_DEV void ymx_ypx(fe &t, const fe &p) {
+  const int c = lane4();
+  const int32_t k = lane_mask(c <= 1), m = c == 0 ? -1 : 0, corr = c == 0 ? 1 : 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) t.v[i] = dpp<qp(1, 1, 3, 2)>(p.v[i]) + (((dpp<qp(0, 0, 0, 0)>(p.v[i]) & k) ^ m) + corr);
+}
+
+// P3Q + CachedQ -> P1P1Q
+TMV_DEV void add(fe &r, const fe &p, const fe &q) {
+  const int c = lane4();
+  fe op1, M;
+  ymx_ypx(op1, p);                          // Y-X, Y+X, T, Z
+  fe_mul(M, op1, q);                        // A, B, C, D
+  const int32_t k2 = lane_mask(c >= 2);     // 2D on lanes 2, 3
+  const int32_t mv = (c == 0 || c == 3) ? -1 : 0, corr = -mv;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int32_t u = dpp<qp(1, 1, 3, 3)>(M.v[i]) + (dpp<qp(1, 1, 3, 3)>(M.v[i]) & k2);  // B, B, 2D, 2D
+    r.v[i] = u + (dpp<qp(0, 0, 2, 2)>(M.v[i]) ^ mv) + corr;  // B-A, B+A, 2D+C, 2D-C (level 3)
+  }
+}
+
+// q -> -q in CachedQ when neg (quad-uniform flag): swap lanes 0/1, negate lane 2
+TMV_DEV void cached_cneg(fe &q, bool neg) {
+  const int c = lane4();
+  const int32_t m = c == 2 ? -1 : 0, corr = -m;
+  fe t;
+#pragma unroll
+  for (int i = 0; i < 10; i++) t.v[i] = (dpp<qp(1, 0, 2, 3)>(q.v[i]) ^ m) + corr;
+  fe_cmov(q, t, neg);
+}
+
+// P3Q -> CachedQ: (Y-X, Y+X, 2dT, Z)
+TMV_DEV void to_cached(fe &q, const fe &p) {
+  const int c = lane4();
+  fe t, k;
+  ymx_ypx(t, p);
+  if (c == 2) {
+    k = consts::d2();
+  } else {
+    fe_one(k);
+  }
+  fe_mul(q, t, k);                          // lane 2 scales by 2d; others re-carry
+}
+#else
+// (older glue) P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
 // E = S3 - S1 - S0, H = S1 + S0, G = S1 - S0, F = S2 - S1 + S0 (all negated
 // relative to dbl-2008-hwcd, same projective point).
 TMV_DEV void dbl(fe &r, const fe &p) {
@@ -142,6 +266,8 @@ TMV_DEV void to_cached(fe &q, const fe &p) {
   }
   fe_mul(q, t, k);                          // lane 2 scales by 2d; others re-carry
 }
+
+#endif
 
 // [8]P == O on a P3Q point: X == 0 and Y == Z.  Returns the quad verdict on
 // every lane of the quad.

@@ -294,6 +294,7 @@ int g_stream = 1;
 bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
 int g_stream_two = 1;              // TMV_STREAM_TWO=0: every part on the lane's stream
 int g_mixed_two = 1;               // TMV_MIXED_TWO=0: a mixed launch's two kind pipelines on one stream
+uint32_t g_sr_group_log2 = 0;      // TMV_SR_GROUP_LOG2: group size of uncached sr25519 launches (A/B; 0 = default)
 // Round 2, 320k C2 entries end to end (parts on two streams): 5.7 ms with
 // parts of 32k / 64k, 5.85-6.0 with 32k / 128k; one stream 6.05-6.3;
 // unstreamed (two lanes of 80k chunks) 6.9 ms.  Round 3 (faster kernels,
@@ -337,6 +338,8 @@ void read_env() {
     if (to) g_timeout_ms = strtoll(to, nullptr, 10);
     const char *st = getenv("TMV_STREAM");
     if (st) g_stream = atoi(st);
+    const char *sg = getenv("TMV_SR_GROUP_LOG2");
+    if (sg) g_sr_group_log2 = (uint32_t)strtoul(sg, nullptr, 10);
     const char *m2 = getenv("TMV_MIXED_TWO");
     if (m2) g_mixed_two = atoi(m2);
     const char *s2 = getenv("TMV_STREAM_TWO");
@@ -528,7 +531,8 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
   bool fixed;
   {
     std::lock_guard<std::mutex> lk(ctx->opt_mu);  // tmv_set_batch_options writes these
-    o.p = msm_params(n, ctx->msm_m_log2, ctx->msm_c, merged, ed_only, ctx->msm_sub);
+    o.p = msm_params(n, ctx->msm_m_log2 ? ctx->msm_m_log2 : (!merged && !ed_only ? g_sr_group_log2 : 0), ctx->msm_c,
+                     merged, ed_only, ctx->msm_sub);
     // mixed launches: each kind's half its own group size -- ed25519 takes
     // the located-fallback groups of 128 at the size ed25519-only launches
     // do, sr25519 keeps 64 (msm_params); both stay the caller's when set

@@ -13,7 +13,9 @@
 #   tracebench[:ARGS]   rocprofv3 --kernel-trace --stats of bench.py ARGS     -> tracebench_K/
 #   configs[:ARGS]      tools/bench_configs.py ARGS       -> configs_K.log
 #   py[:ARGS]           python -u ARGS                    -> py_K.log
-# Optional per-step limit: STEP@SECONDS (default 600).
+# Optional per-step limit: STEP@SECONDS (default 600).  Optional per-step
+# environment: [K=V,K2=V2]STEP (e.g. [TMV_MSM_PARTS=2]alone:--n 125000, or
+# [TMV_LIB_PATH=tendermint_amd/_build/ab_x.so]alone:... for an A/B build).
 set -o pipefail
 name=$1; shift
 out=gpurun_out/$name
@@ -25,10 +27,15 @@ for step in "$@"; do
   k=$((k + 1))
   lim=600
   if [[ "$step" == *@* ]]; then lim=${step##*@}; step=${step%@*}; fi
+  envs=""
+  if [[ "$step" == \[* ]]; then envs=${step%%]*}; envs=${envs#[}; step=${step#*]}; fi
   kind=${step%%:*}
   args=""
   [[ "$step" == *:* ]] && args=${step#*:}
-  echo "[gpu_call] step $k: $kind $args (limit ${lim}s)"
+  echo "[gpu_call] step $k: ${envs:+[$envs] }$kind $args (limit ${lim}s)"
+  saved_env=()
+  IFS=',' read -ra kvs <<< "$envs"
+  for kv in "${kvs[@]}"; do [ -n "$kv" ] && { saved_env+=("${kv%%=*}"); export "$kv"; }; done
   case $kind in
     tests)
       timeout -k 10 "$lim" python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu ${args:-tests} \
@@ -58,6 +65,7 @@ for step in "$@"; do
     *)
       echo "unknown step $kind"; exit 2;;
   esac
+  for v in "${saved_env[@]}"; do unset "$v"; done
   if [ $rc -ne 0 ]; then echo "[gpu_call] step $k ($kind) failed rc=$rc"; exit $rc; fi
 done
 echo "[gpu_call] all $k steps ok"
