@@ -112,4 +112,48 @@ void pool_for(size_t n, size_t max_threads, void (*fn)(void *, size_t), void *ct
   pool().run(n, std::min(nt - 1, pool().workers()), fn, ctx);
 }
 
+
+namespace {
+constexpr size_t kReapBacklog = 3;
+
+class Reaper {
+ public:
+  Reaper() { std::thread([this] { loop(); }).detach(); }
+  bool post(std::unique_ptr<Garbage> &g) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (q_.size() >= kReapBacklog) return false;
+    q_.push_back(std::move(g));
+    cv_.notify_one();
+    return true;
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return !q_.empty(); });
+      std::unique_ptr<Garbage> g = std::move(q_.front());
+      q_.erase(q_.begin());
+      lk.unlock();
+      g.reset();
+      lk.lock();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<std::unique_ptr<Garbage>> q_;
+};
+}  // namespace
+
+bool reap(std::unique_ptr<Garbage> &g) {
+  static const bool on = [] {
+    const char *e = std::getenv("TMV_DEFERRED_RELEASE");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return false;
+  // never destroyed: its detached thread waits on the condition variable
+  static Reaper *r = new Reaper;
+  return r->post(g);
+}
+
 }  // namespace tmh

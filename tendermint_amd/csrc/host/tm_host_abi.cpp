@@ -27,14 +27,17 @@
 
 namespace tmh_internal {
 
-// Default 2,048 jobs: slicing only calls of >= 4,096 jobs keeps every
-// slice's engine call large (a C4 window of 1,200 jobs cut into three ran
-// its GPU work at half the rate: 35k-signature key-merged launches are
-// latency-bound, and the engine serialises calls per device).  Read on every
-// call (tests change it).
+// Default 600 jobs: a call of >= 1,200 jobs (a C4 window: 600 blocks, a
+// light and a full check each) runs as two slices on two threads, one
+// slice's host phases beside the other's engine call.  Round 4, one box:
+// C4 one window at a time 122-126k -> 130-139k blocks/s; three slices (500)
+// 88-100k (35k-signature key-merged launches are latency-bound).  Round 3
+// measured slicing slower, before calls on one device could overlap (lane
+// claims) and before the deferred release.  Read on every call (tests
+// change it).
 uint32_t host_slice_jobs() {
   const char *e = std::getenv("TMV_HOST_SLICE");
-  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 2048u;
+  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 600u;
 }
 
 namespace {
@@ -676,13 +679,21 @@ int verify_commits(tmv_ctx *ctx, const tmv_commit_job *jobs, uint32_t n_jobs, in
     if (e) bad.fetch_add(1, std::memory_order_relaxed);
   });
   tm.mark("finish");
-  // the converted sets, commits and plans are ~10^5 small heap objects per
-  // window; freed on one thread they took ~7 ms of a C3 window
-  parallel_for(std::max(own_v.size(), std::max(own_c.size(), (size_t)n_jobs)), 16, [&](size_t i) {
-    if (i < own_v.size()) own_v[i].reset();
-    if (i < own_c.size()) own_c[i].reset();
-    if (i < n_jobs) plans[i] = tmh::CommitPlan();
-  });
+  // the converted sets, commits and plans are ~10^4 small heap objects per
+  // window: handed to the reaper thread (pool.h), or freed here in parallel
+  // when it is backlogged (freed on one thread they took ~7 ms of a C3 window)
+  {
+    std::unique_ptr<tmh::Garbage> g(new tmh::GarbageOf<decltype(own_v), decltype(own_c), decltype(plans)>(
+        std::move(own_v), std::move(own_c), std::move(plans)));
+    if (!tmh::reap(g)) {
+      auto &[gv, gc, gp] = static_cast<tmh::GarbageOf<decltype(own_v), decltype(own_c), decltype(plans)> &>(*g).items;
+      parallel_for(std::max(gv.size(), std::max(gc.size(), gp.size())), 16, [&](size_t i) {
+        if (i < gv.size()) gv[i].reset();
+        if (i < gc.size()) gc[i].reset();
+        if (i < gp.size()) gp[i] = tmh::CommitPlan();
+      });
+    }
+  }
   return bad.load();
 }
 

@@ -354,14 +354,21 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
     bad += lr.kind != tmh::kLightOk;
   }
   tm.mark("finish");
-  // many small heap objects (validators, signatures, plans): freed in parallel
-  const size_t nrel = std::max({headers.size(), commits.size(), vsets.size(), (size_t)n_jobs});
-  parallel_for(nrel, 16, [&](size_t i) {
-    if (i < headers.size()) headers[i].reset();
-    if (i < commits.size()) commits[i].reset();
-    if (i < vsets.size()) vsets[i].reset();
-    if (i < n_jobs) plans[i] = tmh::LightPlan();
-  });
+  // many small heap objects (validators, signatures, plans): to the reaper
+  // thread (pool.h), or freed here in parallel when it is backlogged
+  using Bundle = tmh::GarbageOf<decltype(headers), decltype(commits), decltype(vsets), decltype(plans)>;
+  std::unique_ptr<tmh::Garbage> g(new Bundle(std::move(headers), std::move(commits), std::move(vsets),
+                                             std::move(plans)));
+  if (!tmh::reap(g)) {
+    auto &[gh, gc, gv, gp] = static_cast<Bundle &>(*g).items;
+    const size_t nrel = std::max({gh.size(), gc.size(), gv.size(), gp.size()});
+    parallel_for(nrel, 16, [&](size_t i) {
+      if (i < gh.size()) gh[i].reset();
+      if (i < gc.size()) gc[i].reset();
+      if (i < gv.size()) gv[i].reset();
+      if (i < gp.size()) gp[i] = tmh::LightPlan();
+    });
+  }
   return bad;
 }
 
