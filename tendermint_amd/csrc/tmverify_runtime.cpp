@@ -215,7 +215,8 @@ struct Device {
   // device-pointer entry points called with stream = NULL run here; the host
   // lanes have streams of their own, so such a call never shares a lane's
   // stream (or its workspace) with a host-buffer call in flight
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // created on first use (context_stream)
+  std::once_flag stream_once;
   HostLane lane[kLanes];
   tmv::ge_precomp *d_btable = nullptr;   // 32x8 comb (single-lane kernel)
   tmv::fe *d_btab_q = nullptr;           // 8 x CachedQ multiples of B (quad kernel)
@@ -355,6 +356,16 @@ void read_env() {
     const char *sc = getenv("TMV_STREAM_CHUNK");
     if (sc) g_stream_chunk = std::max<uint32_t>(2048, (uint32_t)strtoul(sc, nullptr, 10));
   });
+}
+
+// The context's own stream (device-pointer calls with stream = NULL, the
+// hashing entry points), created on first use; NULL if creation failed.
+hipStream_t context_stream(Device &d) {
+  std::call_once(d.stream_once, [&] {
+    (void)hipSetDevice(d.id);
+    if (hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) d.stream = nullptr;
+  });
+  return d.stream;
 }
 
 // Bounded waits (host/wait.h).  hipErrorNotReady = timed out (the device is
@@ -621,8 +632,12 @@ static void collect_stats(tmv_ctx *ctx, Device &d, hipStream_t s) {
 static int init_device(Device &d) {
   hipError_t e = hipSetDevice(d.id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
-  e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
-  if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
+  // The lanes' streams are created first and the context's own stream only
+  // when a call first needs it (context_stream): HIP spreads streams over
+  // its hardware queues (GPU_MAX_HW_QUEUES = 4) in creation order, and with
+  // the context stream created ahead of the lanes a streamed host call's
+  // copy stream shared a queue with its lane's kernels -- end to end 105 ->
+  // 82 M/s on 2.56 M-entry calls (profiles/r04/e2e_lane0.txt).
   for (int l = 0; l < kLanes; l++) {
     e = hipStreamCreateWithFlags(&d.lane[l].stream, hipStreamNonBlocking);
     if (e != hipSuccess) { set_error("hipStreamCreate", e); return TMV_ERR_NO_DEVICE; }
@@ -1755,18 +1770,20 @@ int64_t tmv_vote_sign_bytes_device(tmv_ctx *ctx, const tmv_vote_template *tmpl, 
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   const size_t v_at = 0, t_at = align16(sizeof(tmv_vote) * n), o_at = t_at + align16(tab.size()),
                m_at = o_at + align16(4ull * (n + 1)), bytes = m_at + std::max<size_t>(total, 1);
+  hipStream_t s = context_stream(d);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   uint8_t *dev = nullptr;
   if ((e = hipMalloc(&dev, bytes)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
   int rc = 0;
-  if ((e = hipMemcpyAsync(dev + v_at, votes, sizeof(tmv_vote) * n, hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
-      (e = hipMemcpyAsync(dev + t_at, tab.data(), tab.size(), hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
-      (e = hipMemcpyAsync(dev + o_at, off.data(), 4ull * (n + 1), hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(dev + v_at, votes, sizeof(tmv_vote) * n, hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(dev + t_at, tab.data(), tab.size(), hipMemcpyHostToDevice, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(dev + o_at, off.data(), 4ull * (n + 1), hipMemcpyHostToDevice, s)) != hipSuccess ||
       (e = tmv::launch_vote_signbytes(reinterpret_cast<const tmv_vote *>(dev + v_at),
                                       reinterpret_cast<const tmv::VoteTab *>(dev + t_at), dev + t_at + blob_at,
-                                      reinterpret_cast<const uint32_t *>(dev + o_at), n, dev + m_at, d.stream)) !=
+                                      reinterpret_cast<const uint32_t *>(dev + o_at), n, dev + m_at, s)) !=
           hipSuccess ||
-      (e = hipMemcpyAsync(msg_out, dev + m_at, total, hipMemcpyDeviceToHost, d.stream)) != hipSuccess ||
-      (e = wait_stream(d, d.stream)) != hipSuccess) {
+      (e = hipMemcpyAsync(msg_out, dev + m_at, total, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = wait_stream(d, s)) != hipSuccess) {
     if (e != hipErrorNotReady) set_error("tmv_vote_sign_bytes_device", e);
     rc = wait_rc(e);
   }
@@ -1872,7 +1889,7 @@ int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kin
   if (n == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   const LaunchOpts o = make_opts(ctx, 0, n);
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
@@ -1891,7 +1908,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
   if (key_kind > TMV_KIND_MIXED) { set_error("unsupported key kind"); return TMV_ERR_ARG; }
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
@@ -1946,7 +1963,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   if (N == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   const uint32_t n = (uint32_t)N;
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
   ctx->count_call(n);
@@ -2007,7 +2024,7 @@ int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key
   const size_t o_kind = o_pk + align16(32ull * n), in_bytes = o_kind + align16(n);
   const size_t o_na = in_bytes, o_nb = o_na + 32ull * n, o_out = o_nb + 32ull * n;
   const size_t dev_bytes = o_out + 32ull * n_sets;
-  hipStream_t s = d.stream;
+  hipStream_t s = context_stream(d);
   if ((e = wait_stream(d, s)) != hipSuccess) return wait_rc(e);  // staging may still feed an earlier call
   if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
@@ -2065,7 +2082,7 @@ int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off
   const size_t in_bytes = o_data + align16(bytes);
   const size_t o_na = in_bytes, o_nb = o_na + 32ull * n_leaves, o_out = o_nb + 32ull * n_leaves;
   const size_t dev_bytes = o_out + 32ull * n_trees;
-  hipStream_t s = d.stream;
+  hipStream_t s = context_stream(d);
   if ((e = wait_stream(d, s)) != hipSuccess) return wait_rc(e);  // staging shared with tmv_validator_set_hashes
   if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
@@ -2115,7 +2132,7 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   if (n == 0) return TMV_NOT_ALL;
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
-  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : dev->stream;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   const LaunchOpts o = make_opts(ctx, 0, n, false, true);
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
