@@ -192,3 +192,28 @@ def test_streamed_c2_host_batch_sharded(contexts):
         _, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, hb.pk, hb.sig, hb.msg, hb.off)
         bad = np.flatnonzero(np.asarray(st, np.int8) != want)
         assert not len(bad), f"{k} devices: entries {bad[:8]} differ from the oracle"
+
+
+def test_c5_mixed_host_batch_sharded(contexts):
+    """A C5-shaped mixed ed25519 + sr25519 host batch (a 20k mixed base
+    tiled to 200k, ~1% of each kind corrupted) through the batch equation on
+    1, 2 and 3 devices: identical status vectors (sr25519 Add errors
+    included), equal to the C oracle's statuses of the base, tiled."""
+    from tendermint_amd.testing.factory import make_mixed_batch
+    kind, base = make_mixed_batch(20_000)
+    ed = np.flatnonzero(kind == 0)
+    sr = np.flatnonzero(kind == 1)
+    want1 = np.zeros(base.n, np.int8)
+    be, bs = base.take(ed), base.take(sr)
+    want1[ed] = oracle_c.ed25519_verify_packed(be.pk, be.sig, be.msg, be.off, threads=16)[1]
+    want1[sr] = oracle_c.sr25519_status_packed(bs.pk, bs.sig, bs.msg, bs.off, threads=16)
+    n = 200_000
+    idx = np.arange(n) % base.n
+    hb = base.take(idx)
+    kinds = np.ascontiguousarray(kind[idx])
+    want = want1[idx]
+    assert (want < 0).any() and (want == 0).any()
+    for k, ctx in contexts.items():
+        _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
+        bad = np.flatnonzero(np.asarray(st, np.int8) != want)
+        assert not len(bad), f"{k} devices: entries {bad[:8]}: {np.asarray(st)[bad[:8]]} vs {want[bad[:8]]}"

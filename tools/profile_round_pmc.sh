@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 profile (under gpurun; tag = first argument).  Outputs under
+# Round profile (round 3 on; round 4 reran it unchanged) (under gpurun; tag = first argument).  Outputs under
 # gpurun_out/prof_<tag>/; stops at the first timeout / crash.
 #   trace_alone  kernel trace + stats of bench.py --inflight 1 (one launch at
 #                a time: every dispatch's duration is the kernel's own, the
@@ -9,7 +9,7 @@
 #                launch size (256 C2 batches = 2.56M signatures per launch)
 #   fetchcal     FETCH_SIZE of tools/fetchbench (known byte counts: the
 #                gfx950 correction per access pattern)
-R=${1:-r03}
+R=${1:-r04}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT

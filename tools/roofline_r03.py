@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Dominant-kernel roofline inputs from a round-3 profile directory
-(tools/profile_r03.sh) -> profiles/r03/dominant_kernel.json, read by
+(tools/profile_round_pmc.sh, round 3: profile_r03.sh) -> profiles/r03/dominant_kernel.json, read by
 bench.py's roofline object:
 
   rocprof_alone   rocprofv3 --kernel-trace --stats of bench.py --inflight 1:
