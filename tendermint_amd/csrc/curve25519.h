@@ -123,6 +123,38 @@ TMV_HD void fe_carry_biased(fe &h, int64_t c[10]) {
   for (int i = 0; i < 10; i++) h.v[i] = (int32_t)(c[i] - carry_bias(i));
 }
 
+// The same carry in two parallel rounds (latency form): every column's
+// quotient at once, added to the next column; then once more for the small
+// second-round quotients.  Two dependent steps instead of the twelve-step
+// chain, ~20 more instructions; the limbs are level 1 plus at most 19 * 2^12
+// (a different representation of the same element: results encode the same).
+// Used by the quad formulas (one wave's dependent chain: Horner, the
+// per-entry checks), not by the throughput kernels (TMV_QUAD_PCARRY).
+TMV_HD void fe_carry_biased_par(fe &h, int64_t c[10]) {
+  int64_t k[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int sh = (i & 1) ? 25 : 26;
+    k[i] = c[i] >> sh;
+    c[i] -= k[i] * ((int64_t)1 << sh);  // [0, 2^sh): the bias is still in it
+  }
+#pragma unroll
+  for (int i = 9; i >= 1; i--) c[i] += k[i - 1];
+  c[0] += k[9] * 19;
+  int32_t k2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int sh = (i & 1) ? 25 : 26;
+    k2[i] = (int32_t)(c[i] >> sh);
+    c[i] -= (int64_t)k2[i] * ((int64_t)1 << sh);
+  }
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int32_t in = i ? k2[i - 1] : k2[9] * 19;
+    h.v[i] = (int32_t)(c[i] - carry_bias(i)) + in;
+  }
+}
+
 // The same for columns without the bias.
 TMV_HD void fe_carry_wide(fe &h, int64_t c[10]) {
 #pragma unroll
@@ -175,6 +207,30 @@ TMV_HD void fe_mul(fe &h, const fe &f, const fe &g) {
     }
   }
   fe_carry_biased(h, c);
+}
+
+// fe_mul with the two-round carry (quad formulas, latency-bound chains)
+TMV_HD void fe_mul_par(fe &h, const fe &f, const fe &g) {
+  TMV_ASSERT_LEVEL(f, 3);
+  TMV_ASSERT_LEVEL(g, 3);
+  int32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    g19[i] = mul19(g.v[i]);
+    f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
+  }
+  int64_t c[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      if (i == 0) c[j] = mad_bias(a, g.v[j], j);
+      else if (i + j < 10) c[i + j] = mad_acc(a, g.v[j], c[i + j]);
+      else                 c[i + j - 10] = mad_acc(a, g19[j], c[i + j - 10]);
+    }
+  }
+  fe_carry_biased_par(h, c);
 }
 
 // h = f^2 (55 products via symmetry)

@@ -33,6 +33,26 @@ TMV_DEV void fe_signed(fe &h, const fe &f, int s) {
   for (int i = 0; i < 10; i++) h.v[i] = ((f.v[i] ^ m) - m) & keep;
 }
 
+// Carry of the quad formulas' products: the two-round parallel form
+// (TMV_QUAD_PCARRY=1) or the twelve-step chain (0).
+#ifndef TMV_QUAD_PCARRY
+#define TMV_QUAD_PCARRY 0
+#endif
+TMV_DEV void qcarry(fe &h, int64_t c[10]) {
+#if TMV_QUAD_PCARRY
+  fe_carry_biased_par(h, c);
+#else
+  fe_carry_biased(h, c);
+#endif
+}
+TMV_DEV void qmul(fe &h, const fe &f, const fe &g) {
+#if TMV_QUAD_PCARRY
+  fe_mul_par(h, f, g);
+#else
+  fe_mul(h, f, g);
+#endif
+}
+
 // h = f^2 << sh (sh in {0, 1}, per lane), carried to level 1
 #ifndef TMV_SQ_BIAS
 #define TMV_SQ_BIAS 1
@@ -64,7 +84,7 @@ TMV_DEV void fe_sq_shift(fe &h, const fe &f, int sh) {
       else c[k] = mad_acc(a, b, c[k]);
     }
   }
-  fe_carry_biased(h, c);
+  qcarry(h, c);
 #else
   int32_t f2[10], f19[10];
 #pragma unroll
@@ -107,7 +127,7 @@ TMV_DEV void p1p1_to_p3(fe &p, const fe &r) {
   fe o1, o2;
   fe_dpp<qp(0, 1, 2, 0)>(o1, r);
   fe_dpp<qp(3, 2, 3, 1)>(o2, r);
-  fe_mul(p, o1, o2);
+  qmul(p, o1, o2);
 }
 
 // Linear glue with fused DPP operands (TMV_QUAD_GLUE, default): every
@@ -169,7 +189,7 @@ TMV_DEV void add(fe &r, const fe &p, const fe &q) {
   const int c = lane4();
   fe op1, M;
   ymx_ypx(op1, p);                          // Y-X, Y+X, T, Z
-  fe_mul(M, op1, q);                        // A, B, C, D
+  qmul(M, op1, q);                        // A, B, C, D
   const int32_t k2 = lane_mask(c >= 2);     // 2D on lanes 2, 3
   const int32_t mv = (c == 0 || c == 3) ? -1 : 0, corr = -mv;
 #pragma unroll
@@ -199,7 +219,7 @@ TMV_DEV void to_cached(fe &q, const fe &p) {
   } else {
     fe_one(k);
   }
-  fe_mul(q, t, k);                          // lane 2 scales by 2d; others re-carry
+  qmul(q, t, k);                          // lane 2 scales by 2d; others re-carry
 }
 #else
 // (older glue) P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
@@ -233,7 +253,7 @@ TMV_DEV void add(fe &r, const fe &p, const fe &q) {
   fe_dpp<qp(0, 0, 0, 0)>(b, p);             // X
   fe_signed(b, b, c == 0 ? -1 : (c == 1 ? 1 : 0));
   fe_add(op1, a, b);                        // Y-X, Y+X, T, Z (level 2)
-  fe_mul(M, op1, q);                        // A, B, C, D
+  qmul(M, op1, q);                        // A, B, C, D
   fe u, v;
   fe_dpp<qp(1, 1, 3, 3)>(u, M);             // B, B, D, D
   fe_dpp<qp(0, 0, 2, 2)>(v, M);             // A, A, C, C
@@ -264,7 +284,7 @@ TMV_DEV void to_cached(fe &q, const fe &p) {
   } else {
     fe_one(k);
   }
-  fe_mul(q, t, k);                          // lane 2 scales by 2d; others re-carry
+  qmul(q, t, k);                          // lane 2 scales by 2d; others re-carry
 }
 
 #endif
@@ -302,7 +322,7 @@ TMV_DEV bool p3_equal(const fe &a, const fe &b) {
   fe_cmov(o1, tb, c >= 2);                  // X1, Y1, X2, Y2
   o2 = zb;
   fe_cmov(o2, za, c >= 2);                  // Z2, Z2, Z1, Z1
-  fe_mul(p, o1, o2);
+  qmul(p, o1, o2);
   fe_dpp<qp(2, 3, 0, 1)>(d, p);
   fe_sub(d, p, d);                          // lane 0: X1 Z2 - X2 Z1, lane 1: Y1 Z2 - Y2 Z1
   const int zero = fe_is_zero(d) ? 1 : 0;
@@ -317,7 +337,7 @@ TMV_DEV bool ristretto_equal(const fe &a, const fe &b) {
   fe o1, o2, p, d;
   fe_dpp<qp(0, 1, 1, 0)>(o1, a);            // X1, Y1, Y1, X1
   fe_dpp<qp(1, 0, 1, 0)>(o2, b);            // Y2, X2, Y2, X2
-  fe_mul(p, o1, o2);
+  qmul(p, o1, o2);
   fe_dpp<qp(1, 1, 3, 3)>(d, p);
   fe_sub(d, p, d);                          // lane 0: X1Y2 - Y1X2, lane 2: Y1Y2 - X1X2
   const int zero = fe_is_zero(d) ? 1 : 0;

@@ -45,6 +45,33 @@ extern "C" void hostcheck_sc_reduce512(const uint8_t in[64], uint8_t out[32]) {
     for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(r[i] >> (8 * j));
 }
 
+// fe_mul_par (two-round carry, the quad formulas' TMV_QUAD_PCARRY form)
+// against fe_mul on limbs given directly (level <= 3 extremes included):
+// `rounds` chained products of each; returns 1 when every pair encodes the
+// same element (the limb bounds are asserted under TMV_BOUNDS_CHECK).
+extern "C" int hostcheck_fe_mul_par(const int32_t fl[10], const int32_t gl[10], int rounds) {
+  fe x, y, a, b;
+  for (int i = 0; i < 10; i++) { x.v[i] = fl[i]; y.v[i] = gl[i]; }
+  fe_mul(a, x, y);
+  fe_mul_par(b, x, y);
+  for (int r = 0; r <= rounds; r++) {
+    uint32_t wa[8], wb[8];
+    fe_to_words(wa, a);
+    fe_to_words(wb, b);
+    for (int i = 0; i < 8; i++)
+      if (wa[i] != wb[i]) return 0;
+    fe t;
+    fe_add(t, b, b);  // level 2 (from the slightly wider par output)
+    fe_add(t, t, b);  // ~level 3
+    fe sa;
+    fe_add(sa, a, a);
+    fe_add(sa, sa, a);
+    fe_mul(a, sa, a);
+    fe_mul_par(b, t, b);
+  }
+  return 1;
+}
+
 extern "C" void hostcheck_fe_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
   fe x, y, z;
   fe_from_bytes(x, a);

@@ -39,6 +39,25 @@ def test_fe_mul(H):
         assert int.from_bytes(out.tobytes(), "little") == a * b % E.P
 
 
+def test_fe_mul_two_round_carry(H):
+    """The quad formulas' two-round parallel carry (fe_mul_par,
+    TMV_QUAD_PCARRY) encodes the same product as the twelve-step carry, over
+    chains of 40 products whose inputs are pushed to level 3, from random
+    limbs and from the level-3 extremes (limb bounds asserted in this build)."""
+    import ctypes
+    H.hostcheck_fe_mul_par.restype = ctypes.c_int
+    rng = np.random.default_rng(9)
+    i32 = ctypes.POINTER(ctypes.c_int32)
+    cases = []
+    for _ in range(300):
+        lim = np.array([3 << (25 if i % 2 == 0 else 24) for i in range(10)], np.int64)
+        cases.append((rng.integers(-lim, lim + 1).astype(np.int32), rng.integers(-lim, lim + 1).astype(np.int32)))
+    ext = np.array([3 << (25 if i % 2 == 0 else 24) for i in range(10)], np.int32)
+    cases += [(ext, ext), (-ext, ext), (-ext, -ext), (ext, np.zeros(10, np.int32))]
+    for f, g in cases:
+        assert H.hostcheck_fe_mul_par(f.ctypes.data_as(i32), g.ctypes.data_as(i32), 40) == 1
+
+
 def test_sc_reduce512(H):
     rng = np.random.default_rng(6)
     cases = [rng.bytes(64) for _ in range(1000)] + [b"\xff" * 64, bytes(64), E.L.to_bytes(64, "little"),
