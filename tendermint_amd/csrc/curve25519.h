@@ -268,9 +268,70 @@ TMV_HD void fe_sq2(fe &h, const fe &f) {
   fe_carry(h, t);   // callers treat the result as level 1
 }
 
+// h = f^2 with floor carries: limbs in [0, 2^26) / [0, 2^25) (limb 1 up to
+// 2^25 + 2^13), not centred.  Such limbs are below the level-3 bound
+// (3 * 2^25), so they may be squared again, but not added to anything: only
+// the inner squarings of fe_sqn produce them.  Saves the ten bias
+// subtractions of the centred carry (the columns start at 0).
+TMV_HD void fe_sq_floor(fe &h, const fe &f) {
+  TMV_ASSERT_LEVEL(f, 3);
+  int32_t f2[10], f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) { f2[i] = 2 * f.v[i]; f19[i] = mul19(f.v[i]); }
+  int64_t zero = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(zero));  // an opaque zero addend: each column one v_mad_i64_i32 chain
+#endif
+  int64_t c[10];
+  bool started[10] = {false, false, false, false, false, false, false, false, false, false};
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      const int oddodd = (i & 1) && (j & 1);
+      int32_t a = (i == j) ? f.v[i] : f2[i];
+      if (oddodd) a = 2 * a;
+      const int k = i + j < 10 ? i + j : i + j - 10;
+      const int32_t b = i + j < 10 ? f.v[j] : f19[j];
+      c[k] = mad_acc(a, b, started[k] ? c[k] : zero);
+      started[k] = true;
+    }
+  }
+  int64_t k;
+  k = c[0] >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
+  k = c[4] >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
+  k = c[1] >> 25; c[2] += k; c[1] -= k * ((int64_t)1 << 25);
+  k = c[5] >> 25; c[6] += k; c[5] -= k * ((int64_t)1 << 25);
+  k = c[2] >> 26; c[3] += k; c[2] -= k * ((int64_t)1 << 26);
+  k = c[6] >> 26; c[7] += k; c[6] -= k * ((int64_t)1 << 26);
+  k = c[3] >> 25; c[4] += k; c[3] -= k * ((int64_t)1 << 25);
+  k = c[7] >> 25; c[8] += k; c[7] -= k * ((int64_t)1 << 25);
+  k = c[4] >> 26; c[5] += k; c[4] -= k * ((int64_t)1 << 26);
+  k = c[8] >> 26; c[9] += k; c[8] -= k * ((int64_t)1 << 26);
+  k = c[9] >> 25; c[0] += k * 19; c[9] -= k * ((int64_t)1 << 25);
+  k = c[0] >> 26; c[1] += k; c[0] -= k * ((int64_t)1 << 26);
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = (int32_t)c[i];
+}
+
+// h = f^(2^n): the inner squarings with floor carries, the last centred
+// (level 1).  TMV_SQN_FLOOR=0: every squaring centred.
+#ifndef TMV_SQN_FLOOR
+#define TMV_SQN_FLOOR 1
+#endif
 TMV_HD void fe_sqn(fe &h, const fe &f, int n) {
+#if TMV_SQN_FLOOR
+  if (n == 1) {
+    fe_sq(h, f);
+    return;
+  }
+  fe_sq_floor(h, f);
+  for (int i = 2; i < n; i++) fe_sq_floor(h, h);
+  fe_sq(h, h);
+#else
   fe_sq(h, f);
   for (int i = 1; i < n; i++) fe_sq(h, h);
+#endif
 }
 
 // Bit positions of the ten limbs.

@@ -701,6 +701,61 @@ k_msm_wsum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   store_window_sum(&mw.wsum[t], acc, t - g * p.W == p.W - 1);
 }
 
+// Quad form of k_msm_wpart (P = 1, buckets joined): one quad per (group,
+// window), lane c holding coordinate c (quad.h), 64 windows per workgroup.
+// U = sum_{j >= i} B_j is only ever an addend, so it is kept in CachedQ form
+// and the bucket sum B_i is the P3Q operand of its addition: a step costs
+// each lane five multiplications (U's addition, its P3 and cached forms, T's
+// addition and P3 form) where the one-lane form costs one lane 18, so a
+// window's 2 H-addition chain is ~3.5x shorter; empty buckets add the
+// identity (the formulas are complete), so every quad runs the same steps.
+// The next bucket's count and sum are loaded one step ahead.
+__global__ void __launch_bounds__(256)
+k_msm_wpart_quad(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;  // (group, window) row
+  const uint32_t g = t / p.W;
+  if (g >= p.groups || (g << p.m_log2) >= entry_count(count_ptr, n)) return;  // quad-uniform
+  const uint32_t wdx = t - g * p.W;
+  const int c = quad::lane4();
+  const uint32_t b0 = g * p.W * p.H + p.bucket(wdx, 0);
+  fe T, Uc, U, B, Bn, r;
+  quad::p3_identity(T);
+  quad::cached_identity(Uc);
+  uint32_t cnt = mw.bk_cnt[b0 + p.H - 1];
+  if (cnt) Bn = reinterpret_cast<const fe *>(&mw.bk_sum[b0 + p.H - 1])[c];
+  else quad::p3_identity(Bn);
+  for (int i = (int)p.H - 1; i >= 0; i--) {
+    B = Bn;
+    if (i > 0) {
+      cnt = mw.bk_cnt[b0 + i - 1];
+      if (cnt) Bn = reinterpret_cast<const fe *>(&mw.bk_sum[b0 + i - 1])[c];
+      else quad::p3_identity(Bn);
+    }
+    quad::add(r, B, Uc);  // U += B_i
+    quad::p1p1_to_p3(U, r);
+    quad::to_cached(Uc, U);
+    quad::add(r, T, Uc);  // T += U
+    quad::p1p1_to_p3(T, r);
+  }
+  fe *dst = reinterpret_cast<fe *>(&mw.wpart[2ull * t]);
+  if (wdx == p.W - 1) {  // Horner's start: P3Q
+    dst[c] = T;
+  } else {  // CachedQ, as store_window_sum
+    quad::to_cached(U, T);
+    dst[c] = U;
+  }
+}
+
+// Rows of (group, window) up to which the running sums run in quad form
+// (TMV_WPART_QUAD_ROWS; 0 = never).
+static uint32_t wpart_quad_rows() {
+  static const uint32_t v = [] {
+    const char *e = getenv("TMV_WPART_QUAD_ROWS");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0xffffffffu;
+  }();
+  return v;
+}
+
 // Group verdicts: one quad per group (lane c holds coordinate c), 16 groups
 // per wave; T_g = sum_w 2^(c w) S_w by Horner, then
 //   ed25519: [8] T_g == O;  sr25519: T_g is the Ristretto identity.
@@ -1096,7 +1151,11 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
   }
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
   tk = timed ? ktimer::begin(ktimer::kWpart, stream) : nullptr;
-  hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  if (kMsmJoin && p.P == 1 && parts <= wpart_quad_rows())
+    hipLaunchKernelGGL(k_msm_wpart_quad, dim3((uint32_t)((4 * parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n,
+                       mw, p);
+  else
+    hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
   if (p.P == 1) return hipSuccess;  // the parts are the window sums

@@ -72,6 +72,22 @@ extern "C" int hostcheck_fe_mul_par(const int32_t fl[10], const int32_t gl[10], 
   return 1;
 }
 
+// fe_pow22523 (the square-root exponent (p - 5) / 8; fe_sqn's floor-carry
+// squarings inside) and fe_invert of a 32-byte input.
+extern "C" void hostcheck_fe_pow(const uint8_t a[32], uint8_t pow_out[32], uint8_t inv_out[32]) {
+  uint32_t w[8];
+  memcpy(w, a, 32);
+  fe x, y;
+  fe_from_words(x, w);
+  fe_pow22523(y, x);
+  fe_to_words(w, y);
+  memcpy(pow_out, w, 32);
+  fe_from_words(x, reinterpret_cast<const uint32_t *>(a));
+  fe_invert(y, x);
+  fe_to_words(w, y);
+  memcpy(inv_out, w, 32);
+}
+
 extern "C" void hostcheck_fe_mul(const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
   fe x, y, z;
   fe_from_bytes(x, a);

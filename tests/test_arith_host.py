@@ -39,6 +39,22 @@ def test_fe_mul(H):
         assert int.from_bytes(out.tobytes(), "little") == a * b % E.P
 
 
+def test_fe_pow_chains(H):
+    """fe_pow22523 = x^((p-5)/8) and fe_invert = x^(p-2), whose fe_sqn runs
+    the floor-carry squarings, against Python integers (limb bounds asserted
+    in this build), on random values, 0, 1, p-1 and values >= p."""
+    rng = np.random.default_rng(11)
+    vals = [0, 1, 2, E.P - 1, E.P, E.P + 1, (1 << 255) - 1] + [int.from_bytes(rng.bytes(32), "little") & ((1 << 255) - 1)
+                                                             for _ in range(300)]
+    for v in vals:
+        po = ctypes.create_string_buffer(32)
+        io = ctypes.create_string_buffer(32)
+        H.hostcheck_fe_pow(v.to_bytes(32, "little"), po, io)
+        x = v % E.P
+        assert int.from_bytes(po.raw, "little") == pow(x, (E.P - 5) // 8, E.P)
+        assert int.from_bytes(io.raw, "little") == pow(x, E.P - 2, E.P)
+
+
 def test_fe_mul_two_round_carry(H):
     """The quad formulas' two-round parallel carry (fe_mul_par,
     TMV_QUAD_PCARRY) encodes the same product as the twelve-step carry, over
