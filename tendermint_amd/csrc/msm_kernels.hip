@@ -455,6 +455,9 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 #ifndef TMV_ACCUM_WAVES
 #define TMV_ACCUM_WAVES 1
 #endif
+#ifndef TMV_ACCUM_REGIDX
+#define TMV_ACCUM_REGIDX 0
+#endif
 template <int L>
 __global__ void __launch_bounds__(256, TMV_ACCUM_WAVES)
 k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
@@ -473,6 +476,10 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   if (g >= live_groups) return;
   const uint32_t base = t * L;
   const uint32_t lane = threadIdx.x & 63;
+#if TMV_ACCUM_REGIDX
+  // the chunk's words in registers: the loop below is not unrolled (L copies
+  // of a 1,400-instruction body), so bk[q] / pt[q] become 16-way compare /
+  // select chains (~90 VALU instructions per entry)
   uint32_t bk[L], pt[L];
   {
     const uint4 *b4 = reinterpret_cast<const uint4 *>(mw.ent_bk + base);
@@ -484,7 +491,16 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       pt[4 * q] = y.x; pt[4 * q + 1] = y.y; pt[4 * q + 2] = y.z; pt[4 * q + 3] = y.w;
     }
   }
-  if (bk[0] == kMsmEmpty) {  // padding: nothing to join (k_msm_join reads every live chunk's word)
+#define TMV_BK(q) bk[q]
+#define TMV_PT(q) pt[q]
+#else
+  // the chunk's words read entry by entry (L1 / L2 hits after the first):
+  // no register array indexed by the rolled loop's counter
+  const uint32_t *bkp = mw.ent_bk + base, *ptp = mw.ent_pt + base;
+#define TMV_BK(q) bkp[q]
+#define TMV_PT(q) ptp[q]
+#endif
+  if (TMV_BK(0) == kMsmEmpty) {  // padding: nothing to join (k_msm_join reads every live chunk's word)
     if (kMsmJoin) mw.join_b[t] = kMsmEmpty;
     return;
   }
@@ -505,36 +521,43 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   // every lane's first run starts at entry 0: take that point as the
   // accumulator (one multiply) instead of adding it to the identity (seven)
   ge_p3 acc;
+  const uint32_t pt0 = TMV_PT(0);
   if (kNielsPer == 2) {  // the signed point's own slot
-    const niels_pt P = mw.pts[pt[0]];
+    const niels_pt P = mw.pts[pt0];
     niels_to_p3(acc, P.ypx, P.ymx);
   } else {
-    const niels_pt P = mw.pts[pt[0] >> 1];
-    const bool neg = pt[0] & 1;
+    const niels_pt P = mw.pts[pt0 >> 1];
+    const bool neg = pt0 & 1;
     niels_to_p3(acc, neg ? P.ymx : P.ypx, neg ? P.ypx : P.ymx);
   }
-  uint32_t cur = bk[0], rs = base;
+  uint32_t cur = TMV_BK(0), rs = base;
   uint32_t j = 1;
   bool more = true;
+  uint32_t bn = TMV_BK(1), pn = TMV_PT(1);  // loaded one entry ahead
 #pragma unroll
   for (int q = 1; q < L; q++) {
-    more = more && bk[q] != kMsmEmpty;  // padding only follows the last bucket
+    const uint32_t bq = bn, pq = pn;
+    if (q + 1 < L) {
+      bn = TMV_BK(q + 1);
+      pn = TMV_PT(q + 1);
+    }
+    more = more && bq != kMsmEmpty;  // padding only follows the last bucket
     if (!more) continue;
-    if (bk[q] != cur) {
+    if (bq != cur) {
       flush(cur, rs, base + q, acc);
       ge_p3_identity(acc);
-      cur = bk[q];
+      cur = bq;
       rs = base + q;
     }
     ge_precomp np;
     if (kNielsPer == 2) {
-      const niels_pt P = mw.pts[pt[q]];
+      const niels_pt P = mw.pts[pq];
       np.ypx = P.ypx;
       np.ymx = P.ymx;
       np.xy2d = P.xy2d;
     } else {
-      const niels_pt P = mw.pts[pt[q] >> 1];
-      const bool neg = pt[q] & 1;
+      const niels_pt P = mw.pts[pq >> 1];
+      const bool neg = pq & 1;
       np.ypx = neg ? P.ymx : P.ypx;
       np.ymx = neg ? P.ypx : P.ymx;
       fe_neg(np.xy2d, P.xy2d);
@@ -563,6 +586,8 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   }
   if (kMsmJoin) mw.join_b[t] = join;
 }
+#undef TMV_BK
+#undef TMV_PT
 
 // The buckets accumulation could not join inside a wave (about 1% of the
 // chunks name one): bucket value from its chunk partials (part_last of every
