@@ -7,9 +7,14 @@
 
 namespace tmv {
 
-struct sha512_k {
-  static TMV_HD uint64_t k(int i) {
-    const uint64_t K[80] = {
+// Round constants: device constant memory, read with scalar loads (the
+// round index is wave-uniform).  A function-local table indexed by the round
+// counter was materialised in VGPRs and read through s_set_gpr_idx (~30
+// moves per round).
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__
+#endif
+static const uint64_t kSha512K[80] = {
         0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
         0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
         0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
@@ -30,33 +35,49 @@ struct sha512_k {
         0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
         0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
         0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
-    return K[i];
-  }
-};
 
-TMV_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate: two v_alignbit_b32 on the device (the shift pair the
+// compiler emits otherwise costs three instructions)
+TMV_HD uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t a = n < 32 ? hi : lo, b = n < 32 ? lo : hi;  // n is a compile-time constant
+  const int k = n & 31;
+  if (k == 0) return ((uint64_t)a << 32) | b;
+  return ((uint64_t)__builtin_amdgcn_alignbit(b, a, k) << 32) | __builtin_amdgcn_alignbit(a, b, k);
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 
-// One compression of a 16-word (big-endian-decoded) block into h[8].
+// One compression of a 16-word (big-endian-decoded) block into h[8]: 16
+// rounds on the block's words, then four passes of 16 with the message
+// schedule, each unrolled, so every schedule index is a compile-time
+// register (t & 15 == i), no branch sits inside a pass (a per-round
+// "first pass?" test made the register allocator copy w[] at every round),
+// and only the round constant is read by pass index.
 TMV_HD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
   uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll 16
-  for (int t = 0; t < 80; t++) {
-    uint64_t wt;
-    if (t < 16) {
-      wt = w[t];
-    } else {
-      const uint64_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-      wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
-      w[t & 15] = wt;
-    }
+  auto round = [&](uint64_t wt, uint64_t kt) {
     const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
     const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = hh + S1 + ch + sha512_k::k(t) + wt;
+    const uint64_t t1 = hh + S1 + ch + kt + wt;
     const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint64_t x = a ^ b;
+    const uint64_t mj = (x & c) | (~x & a);  // majority: c where a != b, else a (one bit-field insert)
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  };
+#pragma unroll
+  for (int i = 0; i < 16; i++) round(w[i], kSha512K[i]);
+  for (int r = 1; r < 5; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+      w[i] += s0 + w[(i + 9) & 15] + s1;
+      round(w[i], kSha512K[16 * r + i]);
+    }
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
@@ -82,45 +103,47 @@ TMV_HD void sha512_pq_msg(uint32_t out[16], const uint32_t P[8], const uint32_t 
   sha512_init(h);
   const uint64_t total = 64ull + mlen;
   const uint32_t nblocks = (uint32_t)((total + 17 + 127) / 128);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // message bytes from aligned dword loads: dword indices clamped to the one
+  // holding the last message byte (so every load stays inside that byte's
+  // page, and none is made for an empty message), funnel-shifted by the
+  // message's misalignment, bytes past the end masked off -- no branch per
+  // word on the lane's message length
+  const uint32_t sh = (uint32_t)((uintptr_t)m & 3);
+  const uint32_t *mw = reinterpret_cast<const uint32_t *>((uintptr_t)m - sh);
+  const uint32_t last = mlen ? (sh + mlen - 1) >> 2 : 0;
+#endif
   for (uint32_t blk = 0; blk < nblocks; blk++) {
     uint64_t w[16];
 #pragma unroll
     for (int t = 0; t < 16; t++) {
       const uint64_t base = (uint64_t)blk * 128 + 8 * t;
       uint64_t word;
-      if (base + 8 <= 64) {
+      if (blk == 0 && t < 8) {
         // bytes of P||Q: word t covers u32 words 2t, 2t+1 (little-endian bytes)
-        const uint32_t i = (uint32_t)(base >> 2);
-        const uint32_t lo = i < 8 ? P[i] : Q[i - 8];
-        const uint32_t hi = (i + 1) < 8 ? P[i + 1] : Q[i + 1 - 8];
+        const uint32_t lo = t < 4 ? P[2 * t] : Q[2 * t - 8];
+        const uint32_t hi = t < 4 ? P[2 * t + 1] : Q[2 * t + 1 - 8];
         word = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
       } else {
 #if defined(__HIP_DEVICE_COMPILE__)
-        // message bytes [off, off + 8) (off is a multiple of 8: P||Q is 64
-        // bytes) from aligned dword loads -- no dword past the one holding
-        // the last message byte is read, so the loads stay inside that
-        // byte's page -- then the 0x80 pad byte and zeros
-        const uint32_t off = (uint32_t)(base - 64);
-        const uint32_t sh = (uint32_t)((uintptr_t)m & 3);
-        const uint32_t *a = reinterpret_cast<const uint32_t *>((uintptr_t)m - sh);
+        const uint32_t off = (uint32_t)(base - 64);  // message offset of the word's first byte
         const uint32_t d0i = (sh + off) >> 2;
-        const uint32_t last = mlen ? (sh + mlen - 1) >> 2 : 0;
-        const bool any = mlen > off;
-        const uint32_t d0 = any ? a[d0i] : 0u;
-        const uint32_t d1 = (any && d0i + 1 <= last) ? a[d0i + 1] : 0u;
-        const uint32_t d2 = (any && sh && d0i + 2 <= last) ? a[d0i + 2] : 0u;
-        const uint64_t lo64 = ((uint64_t)d1 << 32) | d0, hi64 = ((uint64_t)d2 << 32) | d1;
-        uint32_t b_lo = (uint32_t)(lo64 >> (8 * sh));  // message bytes off .. off+3, little-endian
-        uint32_t b_hi = (uint32_t)(hi64 >> (8 * sh));  // bytes off+4 .. off+7
-        const int v = mlen > off ? (mlen - off >= 8 ? 8 : (int)(mlen - off)) : 0;  // valid bytes here
-        if (v < 8) {
-          const uint64_t keep = v ? ((uint64_t)1 << (8 * v)) - 1 : 0;
-          uint64_t x = (((uint64_t)b_hi << 32) | b_lo) & keep;
-          if (off + v == total - 64) x |= (uint64_t)0x80 << (8 * v);  // pad byte right after the message
-          b_lo = (uint32_t)x;
-          b_hi = (uint32_t)(x >> 32);
+        uint32_t d0 = 0, d1 = 0, d2 = 0;
+        if (mlen) {
+          d0 = mw[d0i < last ? d0i : last];
+          d1 = mw[d0i + 1 < last ? d0i + 1 : last];
+          d2 = mw[d0i + 2 < last ? d0i + 2 : last];
         }
-        word = ((uint64_t)bswap32(b_lo) << 32) | bswap32(b_hi);
+        const uint32_t b_lo = __builtin_amdgcn_alignbit(d1, d0, 8 * sh);  // bytes off .. off+3
+        const uint32_t b_hi = __builtin_amdgcn_alignbit(d2, d1, 8 * sh);  // bytes off+4 .. off+7
+        uint64_t x = ((uint64_t)b_hi << 32) | b_lo;
+        const int32_t rem = (int32_t)mlen - (int32_t)off;  // message bytes from off on
+        if (rem < 8) {
+          const uint32_t v = rem > 0 ? (uint32_t)rem : 0u;
+          x &= ((uint64_t)1 << (8 * v)) - 1;
+          if (rem >= 0) x |= (uint64_t)0x80 << (8 * v);  // pad byte right after the message
+        }
+        word = ((uint64_t)__builtin_bswap32((uint32_t)x) << 32) | __builtin_bswap32((uint32_t)(x >> 32));
 #else
         word = 0;
         for (int b = 0; b < 8; b++) {
