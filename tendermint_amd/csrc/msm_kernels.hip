@@ -772,11 +772,15 @@ k_msm_wpart_quad(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p)
 }
 
 // Rows of (group, window) up to which the running sums run in quad form
-// (TMV_WPART_QUAD_ROWS; 0 = never).
+// (TMV_WPART_QUAD_ROWS; default 0 = never).  Measured and not kept: 125k
+// launch 222 -> 255 us for the running sums (rocprof), the C2 bench 129.9
+// -> 125.3 M/s (profiles/r04/ab_kernels_r04k.txt) -- the quad form does ~10%
+// more lane work per step, and at these sizes the one-lane kernel is no
+// longer chain-bound.
 static uint32_t wpart_quad_rows() {
   static const uint32_t v = [] {
     const char *e = getenv("TMV_WPART_QUAD_ROWS");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0xffffffffu;
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
   }();
   return v;
 }
