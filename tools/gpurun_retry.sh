@@ -3,8 +3,10 @@
 # the box failed while being prepared (exit 3 / "transient": nothing ran,
 # nothing charged).  Any other outcome -- including a failing command -- ends
 # here.  Usage: tools/gpurun_retry.sh TIMEOUT 'command'
+# (TMV_RETRY_ATTEMPTS, default 20, attempts 150 s apart)
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
+N=${TMV_RETRY_ATTEMPTS:-20}
+for attempt in $(seq 1 "$N"); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
   rc=$?
   echo "$out" | tail -40
