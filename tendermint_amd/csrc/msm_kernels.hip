@@ -455,8 +455,21 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 #ifndef TMV_ACCUM_WAVES
 #define TMV_ACCUM_WAVES 1
 #endif
+// How the lane reads its chunk's bucket / point words (A/B, profiles/r04/
+// ab_accum_r04m.txt, per-launch k_msm_accum at the bench's size relative to
+// the unchanged k_msm_wpart of the same run): TMV_ACCUM_REGIDX=1 (default)
+// loads them as four uint4 into register arrays, which the rolled loop
+// indexes with compare / select chains (~90 VALU instructions per entry, yet
+// the fastest: 2.44x the running sums' time); 0 reads each entry's words
+// from memory one entry ahead (no selects, 2.47x); TMV_ACCUM_PREFETCH=1 also
+// loads the next entry's Niels point during this entry's addition (163
+// VGPRs, still 3 waves / SIMD, 2.60x).  The accumulation is not purely
+// issue-bound: the gathers' latency, not the selects, is what the loop waits on.
 #ifndef TMV_ACCUM_REGIDX
-#define TMV_ACCUM_REGIDX 0
+#define TMV_ACCUM_REGIDX 1
+#endif
+#ifndef TMV_ACCUM_PREFETCH
+#define TMV_ACCUM_PREFETCH 0
 #endif
 template <int L>
 __global__ void __launch_bounds__(256, TMV_ACCUM_WAVES)
@@ -533,6 +546,29 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   uint32_t cur = TMV_BK(0), rs = base;
   uint32_t j = 1;
   bool more = true;
+#if TMV_ACCUM_PREFETCH
+  // software pipeline: the next entry's Niels point is loaded while this
+  // entry's addition runs, its bucket / point words two entries ahead (the
+  // point's address needs them); padding entries load nothing
+  auto slot_of = [](uint32_t ptw) { return kNielsPer == 2 ? ptw : ptw >> 1; };
+  uint32_t b1 = TMV_BK(1), p1 = TMV_PT(1);
+  niels_pt P1;
+  if (b1 != kMsmEmpty) P1 = mw.pts[slot_of(p1)];
+  uint32_t b2 = L > 2 ? TMV_BK(2) : kMsmEmpty, p2 = L > 2 ? TMV_PT(2) : 0u;
+#pragma unroll
+  for (int q = 1; q < L; q++) {
+    const uint32_t bq = b1, pq = p1;
+    const niels_pt P = P1;
+    if (q + 1 < L) {
+      b1 = b2;
+      p1 = p2;
+      if (b1 != kMsmEmpty) P1 = mw.pts[slot_of(p1)];
+      if (q + 2 < L) {
+        b2 = TMV_BK(q + 2);
+        p2 = TMV_PT(q + 2);
+      }
+    }
+#else
   uint32_t bn = TMV_BK(1), pn = TMV_PT(1);  // loaded one entry ahead
 #pragma unroll
   for (int q = 1; q < L; q++) {
@@ -541,6 +577,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       bn = TMV_BK(q + 1);
       pn = TMV_PT(q + 1);
     }
+#endif
     more = more && bq != kMsmEmpty;  // padding only follows the last bucket
     if (!more) continue;
     if (bq != cur) {
@@ -550,13 +587,14 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       rs = base + q;
     }
     ge_precomp np;
+#if !TMV_ACCUM_PREFETCH
+    const niels_pt P = mw.pts[kNielsPer == 2 ? pq : pq >> 1];
+#endif
     if (kNielsPer == 2) {
-      const niels_pt P = mw.pts[pq];
       np.ypx = P.ypx;
       np.ymx = P.ymx;
       np.xy2d = P.xy2d;
     } else {
-      const niels_pt P = mw.pts[pq >> 1];
       const bool neg = pq & 1;
       np.ypx = neg ? P.ymx : P.ypx;
       np.ymx = neg ? P.ypx : P.ymx;
