@@ -7,7 +7,8 @@
 //
 // Lane layouts (c = lane & 3):
 //   P3Q      (X, Y, Z, T)                 extended point
-//   P1P1Q    (E, H, G, F)                 completed point (x = E/G, y = H/F)
+//   P1P1R    (E, G, F, H)                 completed point (x = E/G, y = H/F);
+//            the older glue (TMV_QUAD_GLUE=0) uses P1P1Q (E, H, G, F)
 //   CachedQ  (Y-X, Y+X, 2dT, Z)           addend; B-table entries have Z = 1
 // Every branch below is quad-uniform or lane-select only: DPP requires all
 // four lanes of a quad to be active.
@@ -122,14 +123,6 @@ TMV_DEV void cached_identity(fe &q) {
   q.v[0] = (c == 2) ? 0 : 1;
 }
 
-// P1P1Q -> P3Q: (E F, H G, G F, E H)
-TMV_DEV void p1p1_to_p3(fe &p, const fe &r) {
-  fe o1, o2;
-  fe_dpp<qp(0, 1, 2, 0)>(o1, r);
-  fe_dpp<qp(3, 2, 3, 1)>(o2, r);
-  qmul(p, o1, o2);
-}
-
 // Linear glue with fused DPP operands (TMV_QUAD_GLUE, default): every
 // cross-lane read feeds a VOP2 op directly (v_and / v_xor / v_add _dpp), and a
 // per-lane sign is an XOR with -1 completed by one +1 per negated term in the
@@ -153,8 +146,21 @@ TMV_DEV int32_t lane_mask(bool b) {
 }
 
 #if TMV_QUAD_GLUE
-// P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
-// E = S3 - S1 - S0, H = S1 + S0, G = S1 - S0, F = S2 - S1 + S0 (all negated
+// Completed points in the rotated layout P1P1R (E, G, F, H): each lane owns
+// one factor of its P3Q product (X = E F, Y = G H, Z = F G, T = H E -- the
+// products walk the cycle E-F-G-H), so p1p1_to_p3 reads one operand across
+// lanes instead of two (10 DPP moves per conversion instead of 20; the
+// multiply-add takes no DPP operand).
+
+// P1P1R -> P3Q: lane c multiplies its own value by lane (2, 3, 1, 0)[c]'s
+TMV_DEV void p1p1_to_p3(fe &p, const fe &r) {
+  fe o2;
+  fe_dpp<qp(2, 3, 1, 0)>(o2, r);
+  qmul(p, r, o2);
+}
+
+// P3Q -> P1P1R doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
+// E = S3 - S1 - S0, G = S1 - S0, F = S2 - S1 + S0, H = S1 + S0 (all negated
 // relative to dbl-2008-hwcd, same projective point).
 TMV_DEV void dbl(fe &r, const fe &p) {
   const int c = lane4();
@@ -165,10 +171,10 @@ TMV_DEV void dbl(fe &r, const fe &p) {
     s.v[i] = dpp<qp(0, 1, 2, 0)>(p.v[i]) + (dpp<qp(1, 1, 1, 1)>(p.v[i]) & k3);
   fe S;
   fe_sq_shift(S, s, c == 2 ? 1 : 0);
-  // lane: 0: S3 - S1 - S0, 1: S1 + S0, 2: S2 + S1 - S0, 3: S2 - S1 + S0
-  const int32_t kb = lane_mask(c == 0 || c == 3);  // base S3 (lane 0) / S2 (lane 3)
-  const int32_t m1 = (c == 0 || c == 3) ? -1 : 0;  // -S1
-  const int32_t m0 = (c == 0 || c == 2) ? -1 : 0;  // -S0
+  // lane: 0: S3 - S1 - S0, 1: S1 - S0, 2: S2 - S1 + S0, 3: S1 + S0
+  const int32_t kb = lane_mask(c == 0 || c == 2);  // base S3 (lane 0) / S2 (lane 2)
+  const int32_t m1 = (c == 0 || c == 2) ? -1 : 0;  // -S1
+  const int32_t m0 = (c == 0 || c == 1) ? -1 : 0;  // -S0
   const int32_t corr = -(m1 + m0);
 #pragma unroll
   for (int i = 0; i < 10; i++)
@@ -184,18 +190,18 @@ TMV_DEV void ymx_ypx(fe &t, const fe &p) {
   for (int i = 0; i < 10; i++) t.v[i] = dpp<qp(1, 1, 3, 2)>(p.v[i]) + (((dpp<qp(0, 0, 0, 0)>(p.v[i]) & k) ^ m) + corr);
 }
 
-// P3Q + CachedQ -> P1P1Q
+// P3Q + CachedQ -> P1P1R
 TMV_DEV void add(fe &r, const fe &p, const fe &q) {
   const int c = lane4();
   fe op1, M;
   ymx_ypx(op1, p);                          // Y-X, Y+X, T, Z
   qmul(M, op1, q);                        // A, B, C, D
-  const int32_t k2 = lane_mask(c >= 2);     // 2D on lanes 2, 3
-  const int32_t mv = (c == 0 || c == 3) ? -1 : 0, corr = -mv;
+  const int32_t k2 = lane_mask(c == 1 || c == 2);  // 2D on lanes 1, 2
+  const int32_t mv = (c == 0 || c == 2) ? -1 : 0, corr = -mv;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    const int32_t u = dpp<qp(1, 1, 3, 3)>(M.v[i]) + (dpp<qp(1, 1, 3, 3)>(M.v[i]) & k2);  // B, B, 2D, 2D
-    r.v[i] = u + (dpp<qp(0, 0, 2, 2)>(M.v[i]) ^ mv) + corr;  // B-A, B+A, 2D+C, 2D-C (level 3)
+    const int32_t u = dpp<qp(1, 3, 3, 1)>(M.v[i]) + (dpp<qp(1, 3, 3, 1)>(M.v[i]) & k2);  // B, 2D, 2D, B
+    r.v[i] = u + (dpp<qp(0, 2, 2, 0)>(M.v[i]) ^ mv) + corr;  // B-A, 2D+C, 2D-C, B+A (level 3)
   }
 }
 
@@ -222,7 +228,16 @@ TMV_DEV void to_cached(fe &q, const fe &p) {
   qmul(q, t, k);                          // lane 2 scales by 2d; others re-carry
 }
 #else
-// (older glue) P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
+// (older glue, P1P1Q layout (E, H, G, F))
+// P1P1Q -> P3Q: (E F, H G, G F, E H)
+TMV_DEV void p1p1_to_p3(fe &p, const fe &r) {
+  fe o1, o2;
+  fe_dpp<qp(0, 1, 2, 0)>(o1, r);
+  fe_dpp<qp(3, 2, 3, 1)>(o2, r);
+  qmul(p, o1, o2);
+}
+
+// P3Q -> P1P1Q doubling: squares of (X, Y, Z, X+Y) with 2Z^2 on lane 2, then
 // E = S3 - S1 - S0, H = S1 + S0, G = S1 - S0, F = S2 - S1 + S0 (all negated
 // relative to dbl-2008-hwcd, same projective point).
 TMV_DEV void dbl(fe &r, const fe &p) {
