@@ -79,7 +79,7 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-PMC_DIRS = ("r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
+PMC_DIRS = ("r04", "r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
 
 
 def _load_pmc(method: str, batches_per_step: int = 32):
@@ -399,7 +399,7 @@ def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method):
     return out
 
 
-DOMINANT_FILE = os.path.join("profiles", "r03", "dominant_kernel.json")
+DOMINANT_FILE = os.path.join("profiles", "r04", "dominant_kernel.json")
 
 
 def _dominant_file():
@@ -435,7 +435,7 @@ def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, 
     shares the chip -- against the measured v_mad_i64_i32 peak.  The
     committed rocprofv3 --kernel-trace --stats of bench.py --inflight 1 (one
     launch at a time) gives the same kernel's average dispatch
-    (profiles/r03/dominant_kernel.json); traffic = its HBM bytes per launch
+    (profiles/r04/dominant_kernel.json); traffic = its HBM bytes per launch
     from PMC passes at this launch size (256 x 10k)."""
     m_grp, c_win = msm_shape(K * n, args.group_log2, args.window)
     per_launch = K * n * accum_entries_per_sig(m=m_grp, c=c_win) * ACCUM_PRODUCTS_PER_ENTRY
