@@ -761,6 +761,179 @@ k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict_
   if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
 }
 
+// Four-wave latency form (TMV_FUSED_WAVES=4, default): the 96 comb additions
+// were one quad chain on wave 0 after the hash (the kernel's critical path,
+// ~40% longer than the R decode).  Now a workgroup of four waves covers 16
+// signatures: wave 1 decodes the R's as before; wave 2 runs the 32 base-comb
+// additions (s is known at once); waves 0 and 3 each hash (the same SHA-512 /
+// transcript, computed twice so neither waits for the other) and run half of
+// the 64 key-comb additions; wave 0 then adds the other partial sums (LDS)
+// and makes the final check.  Critical path: max(R decode, hash + 32
+// additions) + 2 additions + the check.  One __syncthreads per wave.
+template <bool SR>
+__global__ void __launch_bounds__(4 * kQuadBlock)
+k_verify_cached_fused4(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
+                       const uint8_t *__restrict__ msg, const uint32_t *__restrict__ msg_off,
+                       const uint32_t *__restrict__ key_slot, uint32_t n, KeyTable kt, const fe *__restrict__ bcomb,
+                       const strobe_t *__restrict__ prefix, uint8_t *__restrict__ out, int aligned) {
+  __shared__ int8_t dig_k[2][kQuadSigs][64];  // waves 0 / 3: their own recoding of k
+  __shared__ int8_t dig_s[kQuadSigs][32];     // wave 2: s in radix 256
+  __shared__ fe part[2][kQuadSigs][4];        // P3Q partial sums of waves 2 and 3
+  __shared__ fe Rs[kQuadSigs][4];
+  __shared__ uint8_t rok[kQuadSigs];
+  const uint32_t base = blockIdx.x * kQuadSigs;
+  if (base >= n) return;  // block-uniform
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave == 1) {
+    if (lane < kQuadSigs) {
+      const uint32_t i = min(base + lane, n - 1);
+      uint32_t r_w[8];
+      if (aligned) load_words_aligned(r_w, sig + 64ull * i);
+      else load_words_unaligned(r_w, sig + 64ull * i);
+      ge_p3 P;
+      const bool ok = SR ? ristretto_decode(P, r_w) : ge_decode_zip215(P, r_w);
+      if (!ok) ge_p3_identity(P);
+      rok[lane] = ok ? 1 : 0;
+      if (SR) {
+        Rs[lane][0] = P.X; Rs[lane][1] = P.Y;
+        fe t; fe_one(t); Rs[lane][2] = t;
+        Rs[lane][3] = P.T;
+      } else {  // CachedQ of R, negated by the final check
+        ge_cached cc;
+        ge_p3_to_cached(cc, P);
+        fe t;
+        fe_carry(t, cc.YmX); Rs[lane][0] = t;
+        fe_carry(t, cc.YpX); Rs[lane][1] = t;
+        Rs[lane][2] = cc.T2d;
+        Rs[lane][3] = cc.Z;
+      }
+    }
+    __syncthreads();
+    return;
+  }
+  const int c = lane & 3;
+  const int q = lane >> 2;
+  const uint32_t raw = base + q;
+  const bool live = raw < n;
+  const uint32_t i = live ? raw : n - 1;
+  fe acc, r, idq;
+  quad::p3_identity(acc);
+  quad::cached_identity(idq);
+  if (wave == 2) {  // base comb: Σ d_t(s) (256^t B), 32 additions
+    uint32_t s_raw[8], s_w[8];
+    if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+    else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+    bool s_ok;
+    if (SR) {
+      s_ok = sr25519_decode_s(s_w, s_raw);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
+      s_ok = sc_is_canonical(s_w);
+    }
+    if (!s_ok) s_w[7] &= 0x0fffffffu;  // keep the recoding in range; the entry is rejected anyway
+    if (c == 1) recode256_store(&dig_s[q][0], s_w);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    auto entry_at = [&](int t, int &dsg) -> const fe * {
+      dsg = dig_s[q][t];
+      const int a = dsg < 0 ? -dsg : dsg;
+      return bcomb + ((t * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
+    };
+    comb_accumulate<32>(acc, idq, entry_at);
+    part[0][q][c] = acc;
+    __syncthreads();
+    return;
+  }
+  // waves 0 and 3: the challenge k, then key-comb rows [32 h, 32 h + 32)
+  const int h = wave == 3 ? 1 : 0;
+  if (c == 0) {
+    uint32_t k_w[8];
+    uint32_t a_w[8], r_w[8];
+    if (aligned) {
+      load_words_aligned(a_w, pk + 32ull * i);
+      load_words_aligned(r_w, sig + 64ull * i);
+    } else {
+      load_words_unaligned(a_w, pk + 32ull * i);
+      load_words_unaligned(r_w, sig + 64ull * i);
+    }
+    const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
+    if constexpr (SR) {  // transcript state in LDS, one slot per quad and wave
+      __shared__ uint64_t strobe_lanes[2][25][kQuadSigs];
+      sr25519_challenge_lds<kQuadSigs>(k_w, *prefix, &strobe_lanes[h][0][q], a_w, r_w, msg + o0, o1 - o0);
+    } else {
+      uint32_t hh[16];
+      sha512_pq_msg(hh, r_w, a_w, msg + o0, o1 - o0);
+      sc_reduce512(k_w, hh);
+    }
+    recode16_store(&dig_k[h][q][0], k_w, true);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const uint32_t slot = key_slot[i];
+  const fe *krow = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
+  auto entry_at = [&](int t, int &dsg) -> const fe * {
+    const int tt = t + 32 * h;
+    dsg = dig_k[h][q][tt];
+    const int a = dsg < 0 ? -dsg : dsg;
+    return krow + ((tt * 8) + (a ? a - 1 : 0)) * 4 + c;
+  };
+  comb_accumulate<32>(acc, idq, entry_at);
+  if (wave == 3) {
+    part[1][q][c] = acc;
+    __syncthreads();
+    return;
+  }
+  // wave 0: the S check, the other partial sums, the final check
+  uint32_t s_raw[8], s_w[8];
+  if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
+  else load_words_unaligned(s_raw, sig + 64ull * i + 32);
+  bool s_ok;
+  if (SR) {
+    s_ok = sr25519_decode_s(s_w, s_raw);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
+    s_ok = sc_is_canonical(s_w);
+  }
+  const bool a_ok = kt.ok[slot] != 0;
+  __syncthreads();  // partial sums and R's written
+#pragma unroll
+  for (int pi = 0; pi < 2; pi++) {
+    fe pc;
+    quad::to_cached(pc, part[pi][q][c]);
+    quad::add(r, acc, pc);
+    quad::p1p1_to_p3(acc, r);
+  }
+  const bool r_ok = rok[q] != 0;
+  int status;
+  if (SR) {
+    const fe Rq = Rs[q][c];
+    const bool eq = quad::ristretto_equal(acc, Rq);
+    status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
+  } else {
+    fe Rq = Rs[q][c];
+    quad::cached_cneg(Rq, true);
+    quad::add(r, acc, Rq);
+    quad::p1p1_to_p3(acc, r);
+    status = (quad::is_identity_times8(acc) && s_ok && a_ok && r_ok) ? 1 : 0;
+  }
+  if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
+}
+
+// Waves per fused latency workgroup (TMV_FUSED_WAVES: 4 = k_verify_cached_fused4,
+// 2 = k_verify_cached_fused).
+static int fused_waves() {
+  static const int v = [] {
+    const char *e = getenv("TMV_FUSED_WAVES");
+    return (e && atoi(e) == 2) ? 2 : 4;
+  }();
+  return v;
+}
+
 hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
                             fe *bases, hipStream_t stream) {
   if (m == 0) return hipSuccess;
@@ -782,10 +955,17 @@ hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, 
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
   if (n <= fused_max) {  // latency-bound: one fused kernel
     const uint32_t blocks = (n + kQuadSigs - 1) / kQuadSigs;
-    if (sr) hipLaunchKernelGGL(k_verify_cached_fused<true>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig, msg,
-                               msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
-    else hipLaunchKernelGGL(k_verify_cached_fused<false>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig, msg,
-                            msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+    if (fused_waves() == 4) {
+      if (sr) hipLaunchKernelGGL(k_verify_cached_fused4<true>, dim3(blocks), dim3(4 * kQuadBlock), 0, stream, pk, sig,
+                                 msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+      else hipLaunchKernelGGL(k_verify_cached_fused4<false>, dim3(blocks), dim3(4 * kQuadBlock), 0, stream, pk, sig,
+                              msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+    } else {
+      if (sr) hipLaunchKernelGGL(k_verify_cached_fused<true>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig,
+                                 msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+      else hipLaunchKernelGGL(k_verify_cached_fused<false>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig,
+                              msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+    }
     return hipGetLastError();
   }
   w.niels = nullptr;

@@ -11,6 +11,7 @@
 #   alone[:ARGS]        tools/launch_alone.py ARGS        -> alone_K.jsonl
 #   trace[:ARGS]        rocprofv3 --kernel-trace --stats of tools/launch_alone.py ARGS -> trace_K/
 #   tracebench[:ARGS]   rocprofv3 --kernel-trace --stats of bench.py ARGS     -> tracebench_K/
+#   tracepy:SCRIPT ARGS rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS -> tracepy_K/
 #   configs[:ARGS]      tools/bench_configs.py ARGS       -> configs_K.log
 #   py[:ARGS]           python -u ARGS                    -> py_K.log
 # Optional per-step limit: STEP@SECONDS (default 600).  Optional per-step
@@ -57,6 +58,10 @@ for step in "$@"; do
       timeout -k 10 "$lim" rocprofv3 --kernel-trace --stats --output-format csv -d "$out/tracebench_$k" -o run -- \
         python3 -u bench.py $args > "$out/tracebench_$k.log" 2>&1; rc=$?
       grep '^{' "$out/tracebench_$k.log" | tail -c 400;;
+    tracepy)
+      timeout -k 10 "$lim" rocprofv3 --kernel-trace --stats --output-format csv -d "$out/tracepy_$k" -o run -- \
+        python3 -u $args > "$out/tracepy_$k.log" 2>&1; rc=$?
+      grep '^{' "$out/tracepy_$k.log" | tail -c 600;;
     configs)
       timeout -k 10 "$lim" python -u tools/bench_configs.py $args > "$out/configs_$k.log" 2>&1; rc=$?
       cat "$out/configs_$k.log" | grep '^{';;
