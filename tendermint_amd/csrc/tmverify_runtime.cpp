@@ -747,25 +747,39 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
   const uint32_t parts = n >= 16384 ? kParts : 1;
   d.kseen.assign((size_t)parts * d.kcap, 0);
   uint32_t misses[kParts] = {0};
+  // missing entries by (entry part p, key part q): list p * parts + q, in
+  // entry order; q = a key's hash bits, so every distinct key lives in one q
+  std::vector<std::vector<uint32_t>> mb((size_t)parts * parts);
+  auto key_part = [&](const uint8_t *k33) -> uint32_t {
+    return parts == 1 ? 0u : (uint32_t)(KeyIndex::hash(k33) >> 58) & (kParts - 1);
+  };
   auto lookup = [&](uint32_t part) {
     const uint32_t lo = (uint32_t)((uint64_t)n * part / parts), hi = (uint32_t)((uint64_t)n * (part + 1) / parts);
     uint8_t *seen = d.kseen.data() + (size_t)part * d.kcap;
     uint8_t key[33];
     key[0] = sr ? 1 : 0;
     const uint8_t *last_pk = nullptr;
-    uint32_t last_slot = UINT32_MAX, miss = 0;
+    uint32_t last_slot = UINT32_MAX, miss = 0, last_q = 0;
     for (uint32_t i = lo; i < hi; i++) {
       const uint8_t *p = pk + 32ull * i;
       if (last_pk && std::memcmp(p, last_pk, 32) == 0) {
         slots_out[i] = last_slot;
-        miss += last_slot == UINT32_MAX;
+        if (last_slot == UINT32_MAX) {
+          miss++;
+          mb[(size_t)part * parts + last_q].push_back(i);
+        }
         continue;
       }
       std::memcpy(key + 1, p, 32);
       last_slot = slots_out[i] = d.kindex.find(key);
       last_pk = p;
-      if (last_slot == UINT32_MAX) miss++;
-      else seen[last_slot] = 1;
+      if (last_slot == UINT32_MAX) {
+        miss++;
+        last_q = key_part(key);
+        mb[(size_t)part * parts + last_q].push_back(i);
+      } else {
+        seen[last_slot] = 1;
+      }
     }
     misses[part] = miss;
   };
@@ -794,33 +808,48 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
       const hipError_t we = wait_stream(d, l.stream);
       if (we != hipSuccess) return wait_rc(we);
     }
-  // 3) misses.  First decide, before touching the index, whether the batch
-  //    fits: bailing out after inserting keys whose tables were never built
-  //    would leave stale entries behind.
+  // 3) misses.  Distinct missing keys per key part q, in parallel (each
+  //    part reads its lists in entry order, so the result is deterministic);
+  //    then decide, before touching the index, whether the batch fits:
+  //    bailing out after inserting keys whose tables were never built would
+  //    leave stale entries behind.  (Serially over every missing entry this
+  //    cost ~1.5 ms per C3 window, where ~60k of 67k entries name one of the
+  //    window's 1,000 new keys.)
+  struct MissPart {
+    KeyIndex ix;                  // distinct new key -> ordinal in first / slot
+    std::vector<uint32_t> first;  // entry of its first occurrence
+    std::vector<uint32_t> slot;   // its cache slot
+  };
+  std::vector<MissPart> mp(parts);
+  auto dedupe = [&](uint32_t q) {
+    MissPart &m = mp[q];
+    m.ix.init(16);
+    uint8_t k[33];
+    k[0] = sr ? 1 : 0;
+    for (uint32_t p = 0; p < parts; p++)
+      for (uint32_t i : mb[(size_t)p * parts + q]) {
+        std::memcpy(k + 1, pk + 32ull * i, 32);
+        if (m.ix.find(k) == UINT32_MAX) {
+          m.ix.insert(k, (uint32_t)m.first.size());
+          m.first.push_back(i);
+        }
+      }
+  };
+  if (parts > 1) tmh::parallel_for_n(parts, kParts, dedupe);
+  else dedupe(0);
+  for (uint32_t q = 0; q < parts; q++) distinct += (uint32_t)mp[q].first.size();
+  if (distinct > d.kcap) return 1;
   uint8_t key[33];
   key[0] = sr ? 1 : 0;
-  {
-    KeyIndex fresh;
-    bool any = false;
-    for (uint32_t i = 0; i < n && distinct <= d.kcap; i++) {
-      if (slots_out[i] != UINT32_MAX) continue;
-      if (!any) { fresh.init(std::min<size_t>(n, d.kcap + 1)); any = true; }
-      std::memcpy(key + 1, pk + 32ull * i, 32);
-      if (fresh.find(key) == UINT32_MAX) {
-        fresh.insert(key, 0);
-        distinct++;
-      }
-    }
-    if (distinct > d.kcap) return 1;
-  }
-  //    then give each missing key a slot (LRU victims are never keys of this
+  //    then give each new key a slot (LRU victims are never keys of this
   //    batch: every key found above is pinned to this epoch)
-  for (uint32_t i = 0; i < n; i++) {
-    if (slots_out[i] != UINT32_MAX) continue;
-    const uint8_t *p = pk + 32ull * i;
-    std::memcpy(key + 1, p, 32);
-    uint32_t slot = d.kindex.find(key);  // inserted by an earlier miss of this batch
-    if (slot == UINT32_MAX) {
+  for (uint32_t q = 0; q < parts; q++) {
+    MissPart &m = mp[q];
+    m.slot.resize(m.first.size());
+    for (size_t t = 0; t < m.first.size(); t++) {
+      const uint32_t i = m.first[t];
+      std::memcpy(key + 1, pk + 32ull * i, 32);
+      uint32_t slot;
       if (d.kindex.size() < d.kcap && d.klru.size() < d.kcap) {
         slot = (uint32_t)d.klru.size();
         d.klru.push_front(slot);
@@ -833,12 +862,25 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
       std::memcpy(d.kslot_key[slot].data(), key, 33);
       d.kslot_epoch[slot] = epoch;
       d.kindex.insert(key, slot);
+      m.slot[t] = slot;
       miss_idx.push_back(i);
       miss_slot.push_back(slot);
       d.kmisses++;
     }
-    slots_out[i] = slot;
   }
+  //    and every missing entry its key's slot
+  auto fill = [&](uint32_t q) {
+    const MissPart &m = mp[q];
+    uint8_t k[33];
+    k[0] = sr ? 1 : 0;
+    for (uint32_t p = 0; p < parts; p++)
+      for (uint32_t i : mb[(size_t)p * parts + q]) {
+        std::memcpy(k + 1, pk + 32ull * i, 32);
+        slots_out[i] = m.slot[m.ix.find(k)];
+      }
+  };
+  if (parts > 1) tmh::parallel_for_n(parts, kParts, fill);
+  else fill(0);
   const uint32_t m = (uint32_t)miss_idx.size();
   if (m) {
     // keys, slots, then the row-base scratch of the two-launch build
