@@ -356,6 +356,7 @@ struct GpuBackend {
     std::unordered_map<const tmh::Commit *, std::vector<std::pair<const std::string *, uint32_t>>> by_commit;
     std::vector<uint32_t> ent_tmpl(es.size());
     std::vector<std::pair<size_t, uint32_t>> runs;  // (first entry, template) of each run of one plan
+    std::vector<const tmh::CommitPlan *> tmpl_src;  // a plan of each template's (commit, chain_id)
     for (size_t i = 0; i < es.size(); i++) {
       const tmh::CommitPlan *pl = es[i].pl;
       if (i && pl == es[i - 1].pl) continue;
@@ -365,11 +366,9 @@ struct GpuBackend {
         uint32_t t = UINT32_MAX;
         for (auto &c : chains)
           if (*c.first == pl->chain_id) t = c.second;
-        if (t == UINT32_MAX) {
-          t = (uint32_t)tmpls.size();
-          const tmh::Commit &cm = *pl->commit;
-          tmpls.push_back(tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round,
-                                                  &cm.block_id));
+        if (t == UINT32_MAX) {  // encoded below, in parallel
+          t = (uint32_t)tmpl_src.size();
+          tmpl_src.push_back(pl);
           chains.emplace_back(&pl->chain_id, t);
         }
         it->second = t;
@@ -377,6 +376,12 @@ struct GpuBackend {
       runs.emplace_back(i, it->second);
     }
     runs.emplace_back(es.size(), 0u);
+    tmpls.resize(tmpl_src.size());
+    parallel_for(tmpl_src.size(), 16, [&](size_t t) {
+      const tmh::CommitPlan *pl = tmpl_src[t];
+      const tmh::Commit &cm = *pl->commit;
+      tmpls[t] = tmh::EncodeVoteTemplate(pl->chain_id, tmh::kPrecommitType, cm.height, cm.round, &cm.block_id);
+    });
     parallel_for(runs.size() - 1, 32, [&](size_t r) {
       std::fill(ent_tmpl.begin() + runs[r].first, ent_tmpl.begin() + runs[r + 1].first, runs[r].second);
     });

@@ -821,6 +821,7 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     std::vector<uint32_t> slot;   // its cache slot
   };
   std::vector<MissPart> mp(parts);
+  std::vector<uint32_t> ord(n);  // missing entry -> its key's ordinal in its part
   auto dedupe = [&](uint32_t q) {
     MissPart &m = mp[q];
     m.ix.init(16);
@@ -828,11 +829,18 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     k[0] = sr ? 1 : 0;
     for (uint32_t p = 0; p < parts; p++)
       for (uint32_t i : mb[(size_t)p * parts + q]) {
+        if (i > 0 && slots_out[i - 1] == UINT32_MAX && std::memcmp(pk + 32ull * i, pk + 32ull * (i - 1), 32) == 0) {
+          ord[i] = ord[i - 1];  // a run of one key (same list: same key part, entry order)
+          continue;
+        }
         std::memcpy(k + 1, pk + 32ull * i, 32);
-        if (m.ix.find(k) == UINT32_MAX) {
-          m.ix.insert(k, (uint32_t)m.first.size());
+        uint32_t o = m.ix.find(k);
+        if (o == UINT32_MAX) {
+          o = (uint32_t)m.first.size();
+          m.ix.insert(k, o);
           m.first.push_back(i);
         }
+        ord[i] = o;
       }
   };
   if (parts > 1) tmh::parallel_for_n(parts, kParts, dedupe);
@@ -869,18 +877,11 @@ static int resolve_keys(Device &d, bool sr, const uint8_t *pk, uint32_t n, uint3
     }
   }
   //    and every missing entry its key's slot
-  auto fill = [&](uint32_t q) {
+  for (uint32_t q = 0; q < parts; q++) {
     const MissPart &m = mp[q];
-    uint8_t k[33];
-    k[0] = sr ? 1 : 0;
     for (uint32_t p = 0; p < parts; p++)
-      for (uint32_t i : mb[(size_t)p * parts + q]) {
-        std::memcpy(k + 1, pk + 32ull * i, 32);
-        slots_out[i] = m.slot[m.ix.find(k)];
-      }
-  };
-  if (parts > 1) tmh::parallel_for_n(parts, kParts, fill);
-  else fill(0);
+      for (uint32_t i : mb[(size_t)p * parts + q]) slots_out[i] = m.slot[ord[i]];
+  }
   const uint32_t m = (uint32_t)miss_idx.size();
   if (m) {
     // keys, slots, then the row-base scratch of the two-launch build
