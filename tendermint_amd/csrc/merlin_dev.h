@@ -25,7 +25,21 @@ struct keccak_rc {
   }
 };
 
-TMV_HD uint64_t rotl64(uint64_t x, int n) { return n ? ((x << n) | (x >> (64 - n))) : x; }
+// 64-bit rotate left: on the device two v_alignbit_b32 for a compile-time n
+// (the shift pair the compiler emits otherwise costs three or four)
+TMV_HD uint64_t rotl64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (n == 0) return x;
+  const int r = 64 - n;  // rotate right by r
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t a = r < 32 ? hi : lo, b = r < 32 ? lo : hi;
+  const int k = r & 31;
+  if (k == 0) return ((uint64_t)a << 32) | b;
+  return ((uint64_t)__builtin_amdgcn_alignbit(b, a, k) << 32) | __builtin_amdgcn_alignbit(a, b, k);
+#else
+  return n ? ((x << n) | (x >> (64 - n))) : x;
+#endif
+}
 
 // Keccak-f[1600] on 25 lanes (lane x + 5y), fully unrolled theta/rho/pi/chi.
 TMV_HD void keccak_f1600_lanes(uint64_t a[25]) {
