@@ -121,14 +121,66 @@ __device__ __forceinline__ int window_digit(const uint32_t *s, uint32_t w, uint3
   return d;
 }
 
+// The same digits read window after window: a 64-bit buffer of the next
+// bits, refilled from the scalar's next word (a uniform index, once every
+// ~32 / c windows) instead of two run-time word selects per window (the
+// select chains were over half of k_msm_sort's VALU instructions).  Equal
+// to window_digit for w = 0, 1, 2, ...  Measured neutral and off by default
+// (TMV_SORT_DIGIT_READER=1): the sort's scalars live in scratch either way
+// (its per-entry loop is not unrolled), and at the bench's size the primary
+// sort took 738 vs 709 us, the located pass's 171 vs 232 us, bench 132.0 /
+// 131.4 vs 132.0 / 131.2 M/s (profiles/r04/ab_sort_reader.txt).
+#ifndef TMV_SORT_DIGIT_READER
+#define TMV_SORT_DIGIT_READER 0
+#endif
+template <int NW>
+struct DigitReader {  // the scalar's words stay in the caller's registers (no pointer kept)
+  uint64_t buf;    // bits [pos, pos + avail) of the scalar, zeros above
+  uint32_t avail;  // 32 < avail <= 64 between calls
+  uint32_t nxt;    // next word to load
+  int carry;
+  __device__ __forceinline__ void init(const uint32_t *s) {
+    buf = (uint64_t)s[0] | ((uint64_t)(NW > 1 ? s[1] : 0u) << 32);
+    avail = 64;
+    nxt = 2;
+    carry = 0;
+  }
+  __device__ __forceinline__ int next(const uint32_t *s, uint32_t c, bool top) {
+    int d = (int)(buf & ((1u << c) - 1)) + carry;
+    buf >>= c;
+    avail -= c;
+    if (avail <= 32) {
+      if (nxt < (uint32_t)NW) buf |= (uint64_t)word_at<NW>(s, nxt) << avail;
+      nxt++;
+      avail += 32;
+    }
+    if (!top && d >= (1 << (c - 1))) {
+      d -= 1 << c;
+      carry = 1;
+    } else {
+      carry = 0;
+    }
+    return d;
+  }
+};
+
 // For every nonzero digit of a scalar: f(bucket within group, negative).
 template <int NW, typename F>
 __device__ __forceinline__ void for_each_digit(const uint32_t *s, uint32_t windows, const MsmParams &p, F f) {
+#if TMV_SORT_DIGIT_READER
+  DigitReader<NW> rd;
+  rd.init(s);
+  for (uint32_t w = 0; w < windows; w++) {
+    const int d = rd.next(s, p.c, w + 1 == windows);
+    if (d != 0) f(p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1)), d < 0);
+  }
+#else
   int carry = 0;
   for (uint32_t w = 0; w < windows; w++) {
     const int d = window_digit<NW>(s, w, p.c, w + 1 == windows, carry);
     if (d != 0) f(p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1)), d < 0);
   }
+#endif
 }
 
 __device__ __forceinline__ void p3_add(ge_p3 &a, const ge_p3 &b) {
@@ -389,9 +441,20 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   uint32_t *ent_bk = mw.ent_bk + gbase;
   const uint32_t wcap = 2 * p.m() + 1;  // entries one window can hold: m R + m A digits + B
   uint32_t *st_pt = scan + BS + 1, *st_bk = st_pt + wcap;
+#if TMV_SORT_DIGIT_READER
+  DigitReader<ZW> rz[R];
+  DigitReader<8> rw[R], rb;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    rz[r].init(z[r]);
+    rw[r].init(wv[r]);
+  }
+  rb.init(bsc);
+#else
   int cz[R], cw[R], cb = 0;  // per-scalar digit carries, window to window
 #pragma unroll
   for (int r = 0; r < R; r++) cz[r] = cw[r] = 0;
+#endif
   const uint32_t total = scan[BS];
   for (uint32_t w = 0; w < p.W; w++) {
     const uint32_t wbeg = hist[p.bucket(w, 0)];
@@ -402,7 +465,11 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       if (!live[r]) continue;
       const uint32_t e = e0 + tid + r * BS;
       if (w < WRz) {
+#if TMV_SORT_DIGIT_READER
+        const int d = rz[r].next(z[r], p.c, w + 1 == WRz);
+#else
         const int d = window_digit<ZW>(z[r], w, p.c, w + 1 == WRz, cz[r]);
+#endif
         if (d != 0) {
           const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
           const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;  // < cap: checked above
@@ -411,7 +478,11 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
         }
       }
       if (!KM) {
+#if TMV_SORT_DIGIT_READER
+        const int d = rw[r].next(wv[r], p.c, w + 1 == p.W);
+#else
         const int d = window_digit<8>(wv[r], w, p.c, w + 1 == p.W, cw[r]);
+#endif
         if (d != 0) {
           const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
           const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;
@@ -421,7 +492,11 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       }
     }
     if (!KM && tid == 0) {
+#if TMV_SORT_DIGIT_READER
+      const int d = rb.next(bsc, p.c, w + 1 == p.W);
+#else
       const int d = window_digit<8>(bsc, w, p.c, w + 1 == p.W, cb);
+#endif
       if (d != 0) {
         const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
         const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;
