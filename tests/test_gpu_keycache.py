@@ -112,3 +112,74 @@ print("ok")
                          timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ok" in out.stdout
+
+
+def test_parallel_key_resolution_scattered_keys():
+    """Batches of >= 16,384 entries resolve their keys in 16 parts: missing
+    keys are deduplicated per key-hash part in parallel and every entry gets
+    its key's slot from that part's ordinal.  Keys here recur across all
+    parts (3,000 distinct keys over 20,000 entries, most entries signed by
+    another key), over three calls whose key sets overlap (hits, misses and
+    LRU evictions at capacity 4,096), then over a capacity of 2,048, where
+    the batch has more distinct keys than the cache and takes the uncached
+    path; every vector equals the oracle's."""
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, '.'); sys.path.insert(0, 'oracle')
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import make_c2_batch, Batch
+ctx = N.Context(1)
+base = make_c2_batch(20000, seed=37, edge_scale=2.0)
+ents = [base.entry(i) for i in range(base.n)]
+def keyed(n_keys, first):
+    # entry i keeps its own key when i % 50 == 0, else takes key first + (7 i) % n_keys of the pool
+    out = [(ents[first + (7 * i) % n_keys][0], m, s) if i % 50 else (pk, m, s) for i, (pk, m, s) in enumerate(ents)]
+    return Batch.from_entries(out)
+for n_keys, first in ((3000, 0), (3000, 1500), (2500, 3000)):
+    b = keyed(n_keys, first)
+    _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st.astype(np.uint8), ref), (n_keys, first)
+s = ctx.key_cache_stats()
+if sys.argv[1] == "4096":  # ~3,400 distinct keys per call fit: hits, misses and evictions
+    assert s["hits"] > 0 and s["misses"] > 0, s
+print("ok", s)
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for cap in ("4096", "2048"):
+        env = dict(os.environ, TMV_KEY_CACHE_CAPACITY=cap)
+        out = subprocess.run([sys.executable, "-c", code, cap], env=env, cwd=root, capture_output=True, text=True,
+                             timeout=300)
+        assert out.returncode == 0, (cap, out.stderr[-2000:])
+        assert "ok" in out.stdout
+
+
+def test_fused_two_wave_form_matches_oracle():
+    """TMV_FUSED_WAVES=2 keeps the round-3 two-wave fused latency kernel
+    (hash + 96 comb additions on one wave beside the R decode); it must give
+    the oracle's vectors as the four-wave default does."""
+    code = r"""
+import sys, numpy as np
+sys.path.insert(0, '.'); sys.path.insert(0, 'oracle')
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import make_c2_batch, make_sr25519_batch
+ctx = N.Context(1)
+b = make_c2_batch(700, seed=38, edge_scale=6.0)
+_, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=4)
+for _ in range(2):
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st.astype(np.uint8), ref)
+s = make_sr25519_batch(300, seed=39, bad_frac=0.05)
+ref = C.sr25519_status_packed(s.pk, s.sig, s.msg, s.off, threads=4)
+ok, st = ctx.verify_batch_ex(N.TMV_KIND_SR25519, N.TMV_FLAG_KEY_CACHE, s.pk, s.sig, s.msg, s.off)
+assert np.array_equal(st, ref)
+print("ok")
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TMV_FUSED_WAVES="2")
+    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ok" in out.stdout
