@@ -744,6 +744,14 @@ k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 #ifndef TMV_WPART_WAVES
 #define TMV_WPART_WAVES 1
 #endif
+// Running sums with the next bucket's sum loaded one step ahead (219
+// VGPRs, still 2 waves): measured no faster -- running sums / accumulation
+// time 0.419 vs 0.413 without, bench 127.7 / 129.1 vs 129.4 / 129.4 M/s
+// (profiles/r04/ab_wpart_prefetch.txt); the kernel waits on its addition
+// chains, not on the bucket loads.  Off by default.
+#ifndef TMV_WPART_PREFETCH
+#define TMV_WPART_PREFETCH 0
+#endif
 
 // A window sum as k_msm_horner reads it: the top window (Horner's start) as a
 // P3Q point (X, Y, Z, T), every other window already in CachedQ order
@@ -778,9 +786,37 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t s = p.H / p.P;
   ge_p3 U, T;
   bool u_set = false, t_set = false;
+  const uint32_t gb = g * p.W * p.H, i0 = part * s;
+#if TMV_WPART_PREFETCH
+  if (kMsmJoin) {
+    // whole buckets only: the next bucket's sum is loaded during this
+    // step's two additions, its count one step earlier still
+    uint32_t c_cur = mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 1)];
+    ge_p3 Bn;
+    if (c_cur) Bn = mw.bk_sum[gb + p.bucket(wdx, i0 + s - 1)];
+    uint32_t c_next = s > 1 ? mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 2)] : 0u;
+    for (int i = (int)s - 1; i >= 0; i--) {
+      const ge_p3 B = Bn;
+      const bool nz = c_cur != 0;
+      if (i > 0) {
+        c_cur = c_next;
+        if (c_cur) Bn = mw.bk_sum[gb + p.bucket(wdx, i0 + (uint32_t)i - 1)];
+        if (i > 1) c_next = mw.bk_cnt[gb + p.bucket(wdx, i0 + (uint32_t)i - 2)];
+      }
+      if (nz) {
+        if (u_set) p3_add(U, B);
+        else { U = B; u_set = true; }
+      }
+      if (u_set) {
+        if (t_set) p3_add(T, U);
+        else { T = U; t_set = true; }
+      }
+    }
+  } else
+#endif
+  {
   // the next bucket's count and start are loaded one iteration ahead, so
   // only its point load is exposed
-  const uint32_t gb = g * p.W * p.H, i0 = part * s;
   uint32_t cnt = mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 1)], bst = mw.bk_start[gb + p.bucket(wdx, i0 + s - 1)];
   for (int i = (int)s - 1; i >= 0; i--) {
     ge_p3 B;
@@ -805,6 +841,7 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       if (t_set) p3_add(T, U);
       else { T = U; t_set = true; }
     }
+  }
   }
   if (!u_set) ge_p3_identity(U);
   if (!t_set) ge_p3_identity(T);
