@@ -279,6 +279,12 @@ int g_zero_copy = 1;
 // pipelined in chunks (of half to one of these) over two lanes
 // (TMV_HOST_CHUNK).
 uint32_t g_host_chunk = 262144;
+// Mixed ed25519 + sr25519 host batches on the batch equation are not
+// streamed (one-kind batches only): each chunk is a whole pipeline with its
+// two kinds' latency tails, so they are cut into fewer, larger chunks than
+// other host batches -- 1M entries in two 500k chunks, the second's copy
+// beside the first's kernels (TMV_MIXED_CHUNK).
+uint32_t g_mixed_chunk = 786432;
 // Lanes the chunks rotate over (TMV_HOST_LANES, 1..kLanes).
 uint32_t g_host_lanes = 2;
 // Bound on every wait for device work (TMV_DEVICE_TIMEOUT_MS, 0 = none).
@@ -329,6 +335,8 @@ void read_env() {
     if (zc) g_zero_copy = atoi(zc);
     const char *hc = getenv("TMV_HOST_CHUNK");
     if (hc) g_host_chunk = (uint32_t)strtoul(hc, nullptr, 10);
+    const char *mxc = getenv("TMV_MIXED_CHUNK");
+    if (mxc) g_mixed_chunk = (uint32_t)strtoul(mxc, nullptr, 10);
     const char *hl = getenv("TMV_HOST_LANES");
     if (hl) g_host_lanes = std::min<uint32_t>(kLanes, std::max<uint32_t>(1, (uint32_t)strtoul(hl, nullptr, 10)));
     const char *mp = getenv("TMV_MSM_PARTS");
@@ -1604,8 +1612,10 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   const bool streamable = g_stream && !vs && (sch == Scheme::Ed25519 || sch == Scheme::Sr25519) &&
                           !(flags & TMV_FLAG_PER_ENTRY) &&
                           ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
-  const tmh::ShardPlan plan =
-      tmh::plan_shards(n, (uint32_t)ctx->devs.size(), streamable ? g_stream_chunk : g_host_chunk);
+  const bool mixed_batch_eq = sch == Scheme::Mixed && !vs && !(flags & TMV_FLAG_PER_ENTRY) &&
+                              ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
+  const tmh::ShardPlan plan = tmh::plan_shards(
+      n, (uint32_t)ctx->devs.size(), streamable ? g_stream_chunk : (mixed_batch_eq ? g_mixed_chunk : g_host_chunk));
   const uint32_t shards = plan.shards;
   // claim g_host_lanes lanes per device (devices in order, so concurrent
   // calls cannot deadlock); released on every return
