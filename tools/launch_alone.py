@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=16, help="distinct C2 batches, tiled")
     ap.add_argument("--method", default="batch", choices=["batch", "per-entry", "auto"])
-    ap.add_argument("--kind", default="ed25519", choices=["ed25519", "mixed"])
+    ap.add_argument("--kind", default="ed25519", choices=["ed25519", "mixed", "mixed-ed", "mixed-sr"],
+                    help="mixed-ed / mixed-sr: one kind's entries of the C5 base alone (pure-kind launch)")
     a = ap.parse_args()
     sizes = [int(x) for x in a.n.split(",")]
     with ProcessPoolExecutor(8) as ex:
@@ -42,6 +43,10 @@ def main():
         from tendermint_amd.testing.factory import make_mixed_batch
         kind_arr, mb = make_mixed_batch(20_000)
         base = [mb]
+    elif a.kind in ("mixed-ed", "mixed-sr"):
+        from tendermint_amd.testing.factory import make_mixed_batch
+        karr, mb = make_mixed_batch(20_000)
+        base = [mb.take(np.flatnonzero(karr == (1 if a.kind == "mixed-sr" else 0)))]
     import torch
     from tendermint_amd import _native as N
     dev = torch.device("cuda", 0)
@@ -55,7 +60,8 @@ def main():
         d = [t(hb.pk), t(hb.sig), t(hb.msg), t(hb.off.view(np.int32))]
         dk = t(np.tile(kind_arr, -(-n // len(kind_arr)))[:n]) if kind_arr is not None else None
         out = torch.zeros(n, dtype=torch.int8, device=dev)
-        kk = N.TMV_KIND_MIXED if dk is not None else N.TMV_KIND_ED25519
+        kk = (N.TMV_KIND_MIXED if dk is not None
+              else N.TMV_KIND_SR25519 if a.kind == "mixed-sr" else N.TMV_KIND_ED25519)
         lat = []
         for r in range(a.warmup + a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,7 +75,7 @@ def main():
                 lat.append(e0.elapsed_time(e1))
         line = {"n": n, "method": a.method, "kind": a.kind, "ms_median": round(statistics.median(lat), 4),
                 "ms_min": round(min(lat), 4), "verifies_per_s": round(n / statistics.median(lat) * 1e3, 1)}
-        if dk is None:
+        if a.kind == "ed25519":
             want = np.array([k in C2_VALID_KINDS for k in hb.kinds], np.int8)
             line["exact"] = bool(np.array_equal(out.cpu().numpy(), want))
         print(json.dumps(line), flush=True)
