@@ -158,3 +158,26 @@ extern "C" void hostcheck_chacha20_block(const uint8_t key[32], uint32_t counter
   for (int i = 0; i < 16; i++)
     for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(o[i] >> (8 * j));
 }
+
+// sr25519 challenge k for (pk, R, M) through the generic STROBE path (fast =
+// 0) or the register-state transcript for vote-sized messages (fast = 1;
+// returns 0 when the message length is outside its range).
+extern "C" int hostcheck_sr25519_challenge(const uint8_t pk[32], const uint8_t r[32], const uint8_t *m, uint32_t mlen,
+                                           int fast, uint8_t out[32]) {
+  strobe_t prefix;
+  sr25519_context_prefix(prefix);
+  uint32_t a[8], rw[8], k[8];
+  load_words(a, pk);
+  load_words(rw, r);
+  if (fast) {
+    if (!sr25519_fast_eligible(prefix, mlen)) return 0;
+    uint64_t slot[25];
+    for (int i = 0; i < 25; i++) slot[i] = 0x0123456789abcdefULL * (i + 1);  // stale LDS contents
+    sr25519_challenge_fast<1>(k, prefix, slot, a, rw, m, mlen);
+  } else {
+    sr25519_challenge(k, prefix, a, rw, m, mlen);
+  }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(k[i] >> (8 * j));
+  return 1;
+}

@@ -173,3 +173,27 @@ def test_chacha20_known_answer(H):
     # weights for consecutive entries (counter = entry index) are distinct and nonzero
     z = {dev(key, e, nonce)[:16] for e in range(4096)}
     assert len(z) == 4096 and bytes(16) not in z
+
+
+def test_sr25519_transcript_fast_path(H):
+    """The register-state transcript (merlin_dev.h sr25519_challenge_fast,
+    messages of 98..127 bytes) gives the generic STROBE path's challenge for
+    every eligible length; other lengths are refused (they take the generic
+    path on the device)."""
+    H.hostcheck_sr25519_challenge.restype = ctypes.c_int
+    rng = np.random.default_rng(98127)
+    eligible = 0
+    for mlen in range(0, 141):
+        for _ in range(3):
+            pk = rng.integers(0, 256, 32, dtype=np.uint8)
+            r = rng.integers(0, 256, 32, dtype=np.uint8)
+            m = rng.integers(0, 256, mlen + 1, dtype=np.uint8)
+            gen = np.zeros(32, np.uint8)
+            fast = np.zeros(32, np.uint8)
+            assert H.hostcheck_sr25519_challenge(p(pk), p(r), p(m), mlen, 0, p(gen)) == 1
+            ok = H.hostcheck_sr25519_challenge(p(pk), p(r), p(m), mlen, 1, p(fast))
+            assert ok == (98 <= mlen <= 127), mlen
+            if ok:
+                eligible += 1
+                assert np.array_equal(gen, fast), mlen
+    assert eligible == 30 * 3

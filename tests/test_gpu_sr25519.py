@@ -54,3 +54,37 @@ def test_mixed_unknown_kind_is_invalid(ctx):
     kind[5] = 7
     _, st = ctx.verify_mixed_batch(kind, b.pk, b.sig, b.msg, b.off)
     assert st[5] == 0
+
+
+@pytest.mark.parametrize("n", [150, 4000])
+@pytest.mark.parametrize("flag", ["per_entry", "batch", "key_cache"])
+def test_sr25519_transcript_lengths(ctx, n, flag):
+    """Every message length around the register-state transcript's range
+    (98..127 bytes, merlin_dev.h sr25519_challenge_fast) and outside it
+    (generic STROBE path), mixed in the same waves, at any alignment, with a
+    fraction of message bit flips -- vs the oracle, on the per-entry,
+    batch-equation and key-cached kernels (small n: the latency kernels)."""
+    import random
+    from tendermint_amd import _native as N
+    from tendermint_amd.testing.factory import Batch
+    from tendermint_amd.testing.sr25519_factory import Sr25519Signer, mini_from_secret
+    rng = random.Random(9127 + n)
+    signers = [Sr25519Signer(mini_from_secret(b"len: %x" % k)) for k in range(16)]
+    ents = []
+    for i in range(n):
+        mlen = 90 + i % 46 if i % 5 else rng.randrange(200)
+        msg = bytes(rng.randrange(256) for _ in range(mlen))
+        s = signers[i % len(signers)]
+        sig = s.sign(msg, b"%d" % i)
+        if i % 13 == 0 and msg:
+            b = bytearray(msg)
+            b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+            msg = bytes(b)
+        ents.append((s.public_key, msg, sig))
+    b = Batch.from_entries(ents)
+    ref = C.sr25519_status_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+    assert (ref == 1).sum() > n // 2 and (ref == 0).sum() > 0
+    flags = {"per_entry": N.TMV_FLAG_PER_ENTRY, "batch": N.TMV_FLAG_BATCH_EQUATION,
+             "key_cache": N.TMV_FLAG_KEY_CACHE}[flag]
+    _, st = ctx.verify_batch_ex(N.TMV_KIND_SR25519, flags, b.pk, b.sig, b.msg, b.off)
+    assert np.array_equal(st, ref)
