@@ -514,6 +514,18 @@ TMV_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
   fe_mul(r.T, p.X, p.Y);
 }
 TMV_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
+// completed -> cached without the extended form in between (five
+// multiplications, as p1p1_to_p3 + p3_to_cached, when T itself is not needed)
+TMV_HD void ge_p1p1_to_cached(ge_cached &r, const ge_p1p1 &p) {
+  fe x, y, t;
+  fe_mul(x, p.X, p.T);
+  fe_mul(y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(t, p.X, p.Y);
+  fe_mul(r.T2d, t, consts::d2());
+  fe_add(r.YpX, y, x);                // level 2
+  fe_sub(r.YmX, y, x);                // level 2
+}
 
 TMV_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
   fe_add(r.YpX, p.Y, p.X);            // level 2

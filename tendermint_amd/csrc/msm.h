@@ -337,6 +337,9 @@ TMV_HD void sc_mul_mod(uint32_t r[8], const uint32_t *a, int na, const uint32_t 
   uint32_t x[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) x[i] = 0;
+  // unrolled (na is a constant at every call site): with a rolled loop x[i + j]
+  // was a run-time register index (s_set_gpr_idx) and x[] partly in scratch
+#pragma unroll
   for (int i = 0; i < na; i++) {
     uint64_t carry = 0;
 #pragma unroll

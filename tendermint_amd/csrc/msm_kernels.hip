@@ -121,31 +121,61 @@ __device__ __forceinline__ int window_digit(const uint32_t *s, uint32_t w, uint3
   return d;
 }
 
+template <int V>
+struct StaticIndex {
+  static constexpr int value = V;
+};
+
 // The same digits read window after window: a 64-bit buffer of the next
-// bits, refilled from the scalar's next word (a uniform index, once every
-// ~32 / c windows) instead of two run-time word selects per window (the
-// select chains were over half of k_msm_sort's VALU instructions).  Equal
-// to window_digit for w = 0, 1, 2, ...  Measured neutral and off by default
-// (TMV_SORT_DIGIT_READER=1): the sort's scalars live in scratch either way
-// (its per-entry loop is not unrolled), and at the bench's size the primary
-// sort took 738 vs 709 us, the located pass's 171 vs 232 us, bench 132.0 /
-// 131.4 vs 132.0 / 131.2 M/s (profiles/r04/ab_sort_reader.txt).
+// bits, refilled from the scalar's next word once every ~32 / c windows,
+// instead of two run-time word selects per window.  Equal to window_digit
+// for w = 0, 1, 2, ...  TMV_SORT_DIGIT_READER=1: the reader took the
+// scalar's words by pointer and refilled from word_at(s, nxt), a run-time
+// index -- measured neutral (the scalars stayed in scratch: at the bench's
+// size the primary sort took 738 vs 709 us, the located pass's 171 vs 232
+// us, bench 132.0 / 131.4 vs 132.0 / 131.2 M/s; profiles/r04/
+// ab_sort_reader.txt).  =2 (default): the reader owns a copy of the words
+// and shifts them down by one at each refill, so every register index is a
+// compile-time constant (no select chain, no scratch, no s_set_gpr_idx).
 #ifndef TMV_SORT_DIGIT_READER
-#define TMV_SORT_DIGIT_READER 0
+#define TMV_SORT_DIGIT_READER 2
 #endif
 template <int NW>
-struct DigitReader {  // the scalar's words stay in the caller's registers (no pointer kept)
+struct DigitReader {
+#if TMV_SORT_DIGIT_READER == 2
+  uint32_t wd[NW];  // the words not yet in buf, lowest first
+#endif
   uint64_t buf;    // bits [pos, pos + avail) of the scalar, zeros above
-  uint32_t avail;  // 32 < avail <= 64 between calls
-  uint32_t nxt;    // next word to load
+  uint32_t avail;
+  uint32_t nxt;    // next word to load (=1)
   int carry;
   __device__ __forceinline__ void init(const uint32_t *s) {
+#if TMV_SORT_DIGIT_READER == 2
+#pragma unroll
+    for (int k = 0; k < NW; k++) wd[k] = s[k];
+    buf = 0;
+    avail = 0;
+#else
     buf = (uint64_t)s[0] | ((uint64_t)(NW > 1 ? s[1] : 0u) << 32);
     avail = 64;
     nxt = 2;
+#endif
     carry = 0;
   }
   __device__ __forceinline__ int next(const uint32_t *s, uint32_t c, bool top) {
+#if TMV_SORT_DIGIT_READER == 2
+    (void)s;
+    if (avail < c) {  // avail + 32 <= 40: fits
+      buf |= (uint64_t)wd[0] << avail;
+#pragma unroll
+      for (int k = 0; k + 1 < NW; k++) wd[k] = wd[k + 1];
+      wd[NW - 1] = 0;
+      avail += 32;
+    }
+    int d = (int)(buf & ((1u << c) - 1)) + carry;
+    buf >>= c;
+    avail -= c;
+#else
     int d = (int)(buf & ((1u << c) - 1)) + carry;
     buf >>= c;
     avail -= c;
@@ -154,6 +184,7 @@ struct DigitReader {  // the scalar's words stay in the caller's registers (no p
       nxt++;
       avail += 32;
     }
+#endif
     if (!top && d >= (1 << (c - 1))) {
       d -= 1 << c;
       carry = 1;
@@ -272,15 +303,19 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   uint32_t acc[9];
 #pragma unroll
   for (int t = 0; t < 9; t++) acc[t] = 0;
-#pragma unroll
-  for (int r = 0; r < R; r++) {
+  // one copy of the weight computation per entry slot r (a compile-time
+  // index): as a loop the body is too large for the unroller, and z[r] /
+  // wv[r] / live[r] became run-time register indices (s_set_gpr_idx) and
+  // scratch
+  auto weigh = [&](auto rc) {
+    constexpr int r = decltype(rc)::value;
     live[r] = false;
 #pragma unroll
     for (int t = 0; t < ZW; t++) z[r][t] = 0;
 #pragma unroll
     for (int t = 0; t < 8; t++) wv[r][t] = 0;
     const uint32_t j = tid + r * BS;
-    if (j >= mlive) continue;
+    if (j >= mlive) return;
     const uint32_t e = e0 + j;
     const uint32_t i = idx ? idx[e] : e;
     uint32_t s_raw[8], s[8];
@@ -305,7 +340,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
         uint4 *wd = reinterpret_cast<uint4 *>(mw.wscal + 8ull * e);
         wd[0] = wd[1] = make_uint4(0, 0, 0, 0);
       }
-      continue;
+      return;
     }
     live[r] = true;
     uint32_t blk[16];
@@ -348,7 +383,12 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       c >>= 32;
     }
     acc[8] += (uint32_t)c;
-  }
+  };
+  weigh(StaticIndex<0>{});
+  weigh(StaticIndex<1>{});
+  weigh(StaticIndex<2>{});
+  weigh(StaticIndex<3>{});
+  static_assert(R == 4, "one weigh() call per entry slot");
   // B scalar = (sum of z_e s_e) mod l: block tree sum (< m l < 2^264), then Barrett
 #pragma unroll
   for (int t = 0; t < 9; t++) red[tid * 9 + t] = acc[t];
@@ -752,6 +792,13 @@ k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 #ifndef TMV_WPART_PREFETCH
 #define TMV_WPART_PREFETCH 0
 #endif
+// One-lane running sums with U held in cached form only (P = 1): U += B
+// adds the P3 bucket sum to the cached U and converts the result straight
+// back to cached, T += U takes that cached U -- 17 multiplications a bucket
+// instead of 18 (B's own cached conversion goes away).
+#ifndef TMV_WPART_CACHED_U
+#define TMV_WPART_CACHED_U 1
+#endif
 
 // A window sum as k_msm_horner reads it: the top window (Horner's start) as a
 // P3Q point (X, Y, Z, T), every other window already in CachedQ order
@@ -785,6 +832,9 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t r = t - g * per_group, wdx = r / p.P, part = r % p.P;
   const uint32_t s = p.H / p.P;
   ge_p3 U, T;
+#if TMV_WPART_CACHED_U
+  ge_cached Uc;  // P = 1: U's only form
+#endif
   bool u_set = false, t_set = false;
   const uint32_t gb = g * p.W * p.H, i0 = part * s;
 #if TMV_WPART_PREFETCH
@@ -810,6 +860,32 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       if (u_set) {
         if (t_set) p3_add(T, U);
         else { T = U; t_set = true; }
+      }
+    }
+  } else
+#endif
+#if TMV_WPART_CACHED_U
+  if (kMsmJoin && p.P == 1) {  // U only as the cached addend; T starts as the first B
+    uint32_t cnt = mw.bk_cnt[gb + p.bucket(wdx, s - 1)];
+    for (int i = (int)s - 1; i >= 0; i--) {
+      const uint32_t c_i = cnt;
+      if (i > 0) cnt = mw.bk_cnt[gb + p.bucket(wdx, (uint32_t)i - 1)];
+      ge_p1p1 rr;
+      bool first = false;
+      if (c_i) {
+        const ge_p3 B = mw.bk_sum[gb + p.bucket(wdx, (uint32_t)i)];
+        if (u_set) {
+          ge_add(rr, B, Uc);
+          ge_p1p1_to_cached(Uc, rr);
+        } else {
+          ge_p3_to_cached(Uc, B);
+          T = B;
+          u_set = t_set = first = true;
+        }
+      }
+      if (u_set && !first) {
+        ge_add(rr, T, Uc);
+        ge_p1p1_to_p3(T, rr);
       }
     }
   } else
