@@ -574,7 +574,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 // ab_accum_r04m.txt, per-launch k_msm_accum at the bench's size relative to
 // the unchanged k_msm_wpart of the same run): TMV_ACCUM_REGIDX=1 (default)
 // loads them as four uint4 into register arrays, which the rolled loop
-// indexes with compare / select chains (~90 VALU instructions per entry, yet
+// indexes by its wave-uniform counter (v_movrels, two VALU per entry, yet
 // the fastest: 2.44x the running sums' time); 0 reads each entry's words
 // from memory one entry ahead (no selects, 2.47x); TMV_ACCUM_PREFETCH=1 also
 // loads the next entry's Niels point during this entry's addition (163
@@ -606,8 +606,8 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t lane = threadIdx.x & 63;
 #if TMV_ACCUM_REGIDX
   // the chunk's words in registers: the loop below is not unrolled (L copies
-  // of a 1,400-instruction body), so bk[q] / pt[q] become 16-way compare /
-  // select chains (~90 VALU instructions per entry)
+  // of a 1,400-instruction body), so bk[q] / pt[q] are read with v_movrels
+  // under s_set_gpr_idx (q is wave-uniform)
   uint32_t bk[L], pt[L];
   {
     const uint4 *b4 = reinterpret_cast<const uint4 *>(mw.ent_bk + base);
