@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=16, help="distinct C2 batches, tiled")
     ap.add_argument("--method", default="batch", choices=["batch", "per-entry", "auto"])
+    ap.add_argument("--group-log2", type=int, default=0, help="batch-equation group size 2^k (0: the library's choice)")
     ap.add_argument("--kind", default="ed25519", choices=["ed25519", "mixed", "mixed-ed", "mixed-sr"],
                     help="mixed-ed / mixed-sr: one kind's entries of the C5 base alone (pure-kind launch)")
     a = ap.parse_args()
@@ -51,6 +52,8 @@ def main():
     from tendermint_amd import _native as N
     dev = torch.device("cuda", 0)
     ctx = N.Context(1)
+    if a.group_log2:
+        ctx.set_batch_options(group_log2=a.group_log2)
     flags = {"batch": N.TMV_FLAG_BATCH_EQUATION, "per-entry": N.TMV_FLAG_PER_ENTRY, "auto": 0}[a.method]
     st = torch.cuda.Stream(dev)
     for n in sizes:
