@@ -127,8 +127,9 @@ int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const ui
  * probability <= 2^-128 per group, as the reference's).
  *   TMV_FLAG_BATCH_EQUATION  use it for this call
  *   TMV_FLAG_PER_ENTRY       never use it for this call
- * Neither flag: batch equation when n >= $TMV_MSM_MIN (default 16384; 0 =
- * never): smaller batches are latency-bound and verify faster per entry.
+ * Neither flag: batch equation when n >= $TMV_MSM_MIN (default 32768, key-
+ * cached batches 16384; the variable sets both, 0 = never): smaller batches
+ * are latency-bound and verify faster per entry.
  * TMV_FLAG_BATCH_EQUATION overrides TMV_FLAG_KEY_CACHE. */
 #define TMV_FLAG_BATCH_EQUATION 2u
 #define TMV_FLAG_PER_ENTRY 4u

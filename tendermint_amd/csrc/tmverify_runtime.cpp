@@ -264,9 +264,15 @@ uint32_t g_quad_max = 0;
 int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
 // Batch equation (msm.h) by default from this many entries up (TMV_MSM_MIN,
 // 0 = never): below it a batch is latency-bound and the per-entry pipeline
-// (0.5 ms for 10k) beats the batch check's longer chain (~1 ms); above it
-// the batch check does 2-3x less work.  Flags override per call.
-uint32_t g_msm_min = 16384;
+// beats the batch check's longer chain; above it the batch check does 2-3x
+// less work.  Set from launches alone at the end of round 4
+// (profiles/r04/crossover.txt): per entry 0.43 / 0.66 / 0.96 / 1.26 ms at
+// 16k / 24k / 32k / 48k C2 entries, the batch equation 0.87 / 0.90 / 0.96 /
+// 1.10 ms -- equal at 32k (was 16384).  Key-cached batches (the key-merged
+// form against the comb kernel) keep 16384 (g_km_min); TMV_MSM_MIN sets
+// both.  Flags override per call.
+uint32_t g_msm_min = 32768;
+uint32_t g_km_min = 16384;
 uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk length (A/B measurement)
 uint32_t g_msm_parts = 0;  // TMV_MSM_PARTS: running-sum lanes per window (power of two <= H; A/B measurement)
 // Key-cached batches up to this size run as one fused latency kernel
@@ -328,7 +334,7 @@ void read_env() {
     const char *t = getenv("TMV_QUAD_MAX");
     g_quad_max = t ? (uint32_t)strtoul(t, nullptr, 10) : 49152u;
     const char *mm = getenv("TMV_MSM_MIN");
-    if (mm) g_msm_min = (uint32_t)strtoul(mm, nullptr, 10);
+    if (mm) g_msm_min = g_km_min = (uint32_t)strtoul(mm, nullptr, 10);
     const char *cf = getenv("TMV_CACHED_FUSED_MAX");
     if (cf) g_cached_fused_max = (uint32_t)strtoul(cf, nullptr, 10);
     const char *zc = getenv("TMV_ZERO_COPY");
@@ -543,7 +549,10 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
   LaunchOpts o;
   if (flags & TMV_FLAG_PER_ENTRY) o.batch_eq = false;
   else if (flags & TMV_FLAG_BATCH_EQUATION) o.batch_eq = true;
-  else o.batch_eq = g_msm_min > 0 && n >= g_msm_min;
+  else {
+    const uint32_t thr = merged ? g_km_min : g_msm_min;
+    o.batch_eq = thr > 0 && n >= thr;
+  }
   if (!o.batch_eq) return o;
   ctx->m_beq += n;
   uint8_t key[32];

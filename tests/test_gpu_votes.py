@@ -97,12 +97,13 @@ def test_verify_votes_sr25519(ctx):
 
 
 def test_verify_votes_large_batch_equation(ctx):
-    """Above the batch-equation threshold (16384): device messages feed the
-    MSM pipeline; honest entries all valid, flipped ones caught."""
+    """Through the batch equation (the flag: 20k is below the default
+    threshold of 32768): device messages feed the MSM pipeline; honest
+    entries all valid, flipped ones caught."""
     rng = random.Random(55)
     n = 20000
     tmpls, votes, b = _signed_votes(rng, 60, n, bad_frac=0.002)
     _, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
     segs = [V.segments(t) for t in tmpls]
-    ok, st = ctx.verify_votes(N.TMV_KIND_ED25519, 0, segs, votes, b.pk, b.sig)
+    ok, st = ctx.verify_votes(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, segs, votes, b.pk, b.sig)
     assert np.array_equal(st.astype(np.uint8), ref)
