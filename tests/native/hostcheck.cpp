@@ -181,3 +181,38 @@ extern "C" int hostcheck_sr25519_challenge(const uint8_t pk[32], const uint8_t r
     for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(k[i] >> (8 * j));
   return 1;
 }
+
+// ge_p1p1_to_cached (the running sums' U) against p1p1_to_p3 + p3_to_cached
+// on points decoded from the given encodings, each added to the next: returns
+// the number of (point, coordinate) pairs that differ (0 expected).
+extern "C" int hostcheck_p1p1_to_cached(const uint8_t *enc, uint32_t n) {
+  int bad = 0;
+  for (uint32_t i = 0; i + 1 < n; i++) {
+    uint32_t w0[8], w1[8];
+    load_words(w0, enc + 32 * i);
+    load_words(w1, enc + 32 * (i + 1));
+    ge_p3 a, b;
+    if (!ge_decode_zip215(a, w0) || !ge_decode_zip215(b, w1)) continue;
+    pairs++;
+    ge_cached bc, direct, via;
+    ge_p3_to_cached(bc, b);
+    ge_p1p1 r;
+    ge_add(r, a, bc);
+    ge_p1p1_to_cached(direct, r);
+    ge_p3 p;
+    ge_p1p1_to_p3(p, r);
+    ge_p3_to_cached(via, p);
+    const fe *x[4] = {&direct.YpX, &direct.YmX, &direct.Z, &direct.T2d};
+    const fe *y[4] = {&via.YpX, &via.YmX, &via.Z, &via.T2d};
+    for (int c = 0; c < 4; c++) {
+      uint32_t u[8], v[8];
+      fe t;
+      fe_carry(t, *x[c]);
+      fe_to_words(u, t);
+      fe_carry(t, *y[c]);
+      fe_to_words(v, t);
+      if (std::memcmp(u, v, sizeof u)) bad++;
+    }
+  }
+  return pairs < 50 ? -1 : bad;
+}

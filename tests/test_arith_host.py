@@ -197,3 +197,19 @@ def test_sr25519_transcript_fast_path(H):
                 eligible += 1
                 assert np.array_equal(gen, fast), mlen
     assert eligible == 30 * 3
+
+
+def test_p1p1_to_cached_matches_two_step(H):
+    """ge_p1p1_to_cached (k_msm_wpart's U, TMV_WPART_CACHED_U) equals
+    p1p1_to_p3 followed by p3_to_cached, coordinate by coordinate."""
+    import random
+    rng = random.Random(1717)
+    enc = []
+    while len(enc) < 400:
+        y = rng.randrange(E.P) if hasattr(E, "P") else rng.randrange(2**255 - 19)
+        b = bytearray(y.to_bytes(32, "little"))
+        b[31] |= rng.randrange(2) << 7
+        enc.append(bytes(b))
+    buf = np.frombuffer(b"".join(enc), np.uint8).copy()
+    H.hostcheck_p1p1_to_cached.restype = ctypes.c_int
+    assert H.hostcheck_p1p1_to_cached(p(buf), len(enc)) == 0
