@@ -186,7 +186,7 @@ extern "C" int hostcheck_sr25519_challenge(const uint8_t pk[32], const uint8_t r
 // on points decoded from the given encodings, each added to the next: returns
 // the number of (point, coordinate) pairs that differ (0 expected).
 extern "C" int hostcheck_p1p1_to_cached(const uint8_t *enc, uint32_t n) {
-  int bad = 0;
+  int bad = 0, pairs = 0;  // -1 when fewer than 50 pairs decoded (nothing checked)
   for (uint32_t i = 0; i + 1 < n; i++) {
     uint32_t w0[8], w1[8];
     load_words(w0, enc + 32 * i);
