@@ -1438,10 +1438,11 @@ static int subcheck_mode() {
 // workgroup left 3 of 4 waves idle but resident through the sort's LDS
 // phases; C2 bench (3,072 steps, round 1, one GPU call): 80.4 / 80.7 ->
 // 84.8 / 84.7 M/s.
+// TMV_SORT_BLOCK=128: two waves per group of <= 256 (A/B).
 static int sort_block() {
   static const int bs = [] {
     const char *e = getenv("TMV_SORT_BLOCK");
-    return (e && !strcmp(e, "256")) ? 256 : 64;
+    return (e && !strcmp(e, "256")) ? 256 : (e && !strcmp(e, "128")) ? 128 : 64;
   }();
   return bs;
 }
@@ -1548,6 +1549,10 @@ static hipError_t launch_sort_buckets(const uint8_t *sig, const uint32_t *idx, c
     const size_t smem = sort_smem(p, 64);
     hipLaunchKernelGGL((k_msm_sort<SR, false, 64>), dim3(p.groups), dim3(64), smem, stream, sig, idx, count_ptr, n,
                        w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr, e_base);
+  } else if (p.m_log2 <= 8 && sort_block() == 128) {
+    const size_t smem = sort_smem(p, 128);
+    hipLaunchKernelGGL((k_msm_sort<SR, false, 128>), dim3(p.groups), dim3(128), smem, stream, sig, idx, count_ptr,
+                       n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr, e_base);
   } else {
     const size_t smem = sort_smem(p, kMsmSortBlock);
     hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx,
@@ -1588,6 +1593,10 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     if (p.m_log2 <= 8 && sort_block() == 64) {
       const size_t smem = sort_smem(p, 64);
       hipLaunchKernelGGL((k_msm_sort<SR, false, 64, true>), dim3(p.groups), dim3(64), smem, stream, sig, idx,
+                         count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
+    } else if (p.m_log2 <= 8 && sort_block() == 128) {
+      const size_t smem = sort_smem(p, 128);
+      hipLaunchKernelGGL((k_msm_sort<SR, false, 128, true>), dim3(p.groups), dim3(128), smem, stream, sig, idx,
                          count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
     } else {
       const size_t smem = sort_smem(p, kMsmSortBlock);
