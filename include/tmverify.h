@@ -62,11 +62,15 @@ typedef struct tmv_ctx tmv_ctx;
 
 /* Open a context on the GPUs selected by device_mask (bit i = HIP device i;
  * 0 = all visible devices).  Builds the per-device base-point tables.
- * Returns NULL on failure (tmv_last_error() says why).
- * Test aid: with TMV_LOGICAL_DEVICES=k in the environment each selected GPU
- * joins the context as k devices (own streams, lanes, workspaces, key cache),
- * so the multi-device shard path runs on one GPU. */
+ * Returns NULL on failure (tmv_last_error() says why). */
 tmv_ctx *tmv_open(uint32_t device_mask);
+/* TEST AID, not for deployments: as tmv_open, but each selected GPU joins the
+ * context as `logical` devices (1..8: own streams, lanes, workspaces, key
+ * cache), so the multi-device shard / harvest path runs on a one-GPU box.
+ * tmv_num_devices then counts logical devices, while the device-pointer entry
+ * points still name a GPU by its HIP id (its first logical device).
+ * Announces itself on stderr when logical > 1. */
+tmv_ctx *tmv_open_logical(uint32_t device_mask, int logical);
 void tmv_close(tmv_ctx *ctx);
 int tmv_num_devices(const tmv_ctx *ctx);
 const char *tmv_last_error(void);

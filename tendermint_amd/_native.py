@@ -43,7 +43,7 @@ VOTE_DTYPE = np.dtype([("ts_seconds", "<i8"), ("ts_nanos", "<i4"), ("tmpl", "<u4
 
 # Every symbol include/tmverify.h declares (checked by tests/test_boundary.py).
 EXPORTS = [
-    "tmv_open", "tmv_close", "tmv_num_devices", "tmv_last_error", "tmv_version",
+    "tmv_open", "tmv_open_logical", "tmv_close", "tmv_num_devices", "tmv_last_error", "tmv_version",
     "tmv_ed25519_verify_batch", "tmv_ed25519_verify", "tmv_sr25519_verify_batch",
     "tmv_verify_mixed_batch", "tmv_ed25519_verify_batch_device", "tmv_verify_mixed_batch_device",
     "tmv_verify_batch_ex", "tmv_key_cache_stats", "tmv_set_batch_options", "tmv_batch_stats",
@@ -125,6 +125,8 @@ def lib() -> ctypes.CDLL:
         vp = ctypes.c_void_p
         L.tmv_open.restype = vp
         L.tmv_open.argtypes = [ctypes.c_uint32]
+        L.tmv_open_logical.restype = vp
+        L.tmv_open_logical.argtypes = [ctypes.c_uint32, ctypes.c_int]
         L.tmv_close.argtypes = [vp]
         L.tmv_num_devices.argtypes = [vp]
         L.tmv_last_error.restype = ctypes.c_char_p
@@ -196,9 +198,12 @@ def _p(a: np.ndarray, t=ctypes.c_uint8):
 class Context:
     """A tmv_ctx on the devices in ``device_mask`` (0 = all visible)."""
 
-    def __init__(self, device_mask: int = 0):
+    def __init__(self, device_mask: int = 0, logical: int = 1):
+        """logical > 1: test aid (tmv_open_logical), every GPU opened as that
+        many logical devices."""
         self._lib = lib()
-        self._h = self._lib.tmv_open(device_mask)
+        self._h = (self._lib.tmv_open(device_mask) if logical == 1
+                   else self._lib.tmv_open_logical(device_mask, logical))
         if not self._h:
             raise NativeError("tmv_open failed: " + last_error())
 

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -247,11 +248,17 @@ int light_verify_slice(tmv_ctx *ctx, const tmv_light_job *jobs, uint32_t n_jobs,
   std::vector<tmh::Bytes> hh, vh;
   int hrc = 0;
   std::string hash_error;
-  std::thread hasher([&] {
+  auto hash_job = [&] {
     hrc = header_hashes(ctx, hq, hh);
     if (hrc >= 0) hrc = valset_hashes(ctx, vq, V.src, vh);
     if (hrc < 0) hash_error = tmv_last_error();
-  });
+  };
+  std::thread hasher;
+  try {
+    hasher = std::thread(hash_job);
+  } catch (const std::system_error &) {
+    hash_job();  // no thread to be had: hash first, inline (the results are the same)
+  }
   struct Join {
     std::thread &t;
     ~Join() { if (t.joinable()) t.join(); }

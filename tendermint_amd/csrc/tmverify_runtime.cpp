@@ -256,6 +256,49 @@ struct Device {
   std::atomic<bool> faulted{false};
 };
 
+// Caller pages that stayed registered after a failed or skipped wait (the
+// chunk's DMA may still be in flight, so they were not unregistered; see the
+// harvest in run_batch).  A stale registration would let a later copy through
+// those virtual addresses -- after the caller freed and the allocator reused
+// them -- hit the old pinned pages, so each range is unregistered as soon as
+// the streams that could still read it report idle: checked (never waited
+// for) at every tmv_open, tmv_close and host-buffer call.
+struct LeakedPin {
+  int dev;
+  hipStream_t copy, stream;
+  void *p;
+};
+std::mutex g_leak_mu;
+std::vector<LeakedPin> g_leaked;
+
+void leak_pins(int dev, HostLane &ln) {
+  std::lock_guard<std::mutex> lk(g_leak_mu);
+  for (void *p : ln.pinned) g_leaked.push_back({dev, ln.copy, ln.stream, p});
+  ln.pinned.clear();
+}
+
+// Unregister every leaked range whose streams have drained (a range whose
+// device never drains stays registered, with that device's leaked buffers).
+void release_leaked_pins() {
+  std::lock_guard<std::mutex> lk(g_leak_mu);
+  if (g_leaked.empty()) return;
+  std::vector<LeakedPin> keep;
+  for (const LeakedPin &x : g_leaked) {
+    (void)hipSetDevice(x.dev);
+    const bool idle = (!x.copy || hipStreamQuery(x.copy) == hipSuccess) &&
+                      (!x.stream || hipStreamQuery(x.stream) == hipSuccess);
+    (void)hipGetLastError();
+    if (idle) (void)hipHostUnregister(x.p);
+    else keep.push_back(x);
+  }
+  g_leaked.swap(keep);
+}
+
+size_t leaked_pin_count() {
+  std::lock_guard<std::mutex> lk(g_leak_mu);
+  return g_leaked.size();
+}
+
 // Kernel choice: the quad (4 lanes / signature) path wins while the batch is
 // too small to fill the chip one lane per signature; the single-lane kernel
 // has less glue per signature and wins on large batches.
@@ -1185,7 +1228,10 @@ int tmv_kernel_timing_read(tmv_ctx *ctx, const char *kernel, double *total_ms, u
 const char *tmv_last_error(void) { return g_last_error.c_str(); }
 void tmv_internal_set_error(const char *msg) { g_last_error = msg ? msg : ""; }
 
-tmv_ctx *tmv_open(uint32_t device_mask) {
+tmv_ctx *tmv_open(uint32_t device_mask) { return tmv_open_logical(device_mask, 1); }
+
+tmv_ctx *tmv_open_logical(uint32_t device_mask, int logical) {
+  release_leaked_pins();
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
   if (e != hipSuccess || count <= 0) {
@@ -1193,13 +1239,14 @@ tmv_ctx *tmv_open(uint32_t device_mask) {
                               : std::string("no HIP device visible"));
     return nullptr;
   }
-  // TMV_LOGICAL_DEVICES=k (test aid, read on every open): each selected GPU
-  // joins the context as k devices -- own streams, lanes, workspaces and key
+  // logical > 1 (test aid, tmv_open_logical only): each selected GPU joins the
+  // context as that many devices -- own streams, lanes, workspaces and key
   // cache -- so the multi-device shard / launch / harvest path of run_batch
   // runs on real streams on a one-GPU box.  Device-pointer entry points name
   // a GPU by its HIP id and reach its first logical device.
-  int logical = 1;
-  if (const char *lg = getenv("TMV_LOGICAL_DEVICES")) logical = std::max(1, std::min(8, atoi(lg)));
+  logical = std::max(1, std::min(8, logical));
+  if (logical > 1)
+    fprintf(stderr, "tmverify: TEST AID tmv_open_logical: every GPU opened as %d logical devices\n", logical);
   auto ctx = std::make_unique<tmv_ctx>();
   for (int i = 0; i < count && i < 32; i++) {
     if (device_mask != 0 && !(device_mask & (1u << i))) continue;
@@ -1222,6 +1269,15 @@ tmv_ctx *tmv_open(uint32_t device_mask) {
 
 void tmv_close(tmv_ctx *ctx) {
   if (!ctx) return;
+  for (auto &d : ctx->devs) {  // drain the healthy devices first, so their leaked ranges are released
+    if (d->faulted) continue;
+    (void)hipSetDevice(d->id);
+    for (HostLane &l : d->lane) {
+      if (l.stream) (void)hipStreamSynchronize(l.stream);
+      if (l.copy) (void)hipStreamSynchronize(l.copy);
+    }
+  }
+  release_leaked_pins();
   for (auto &d : ctx->devs) {
     (void)hipSetDevice(d->id);
     if (d->faulted) continue;  // work still running on its buffers: leak them rather than free them under it
@@ -1608,6 +1664,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     return TMV_ERR_ARG;
   }
   read_env();
+  if (leaked_pin_count()) release_leaked_pins();
   ctx->count_call(n);
   ctx->host_enter();
   struct HostTime {  // busy wall time of host-buffer calls into tmv_metrics, on every return
@@ -1684,7 +1741,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
         // under a DMA in flight, or later, after the caller freed the
         // memory, would be worse (include/tmverify.h, TMV_ERR_TIMEOUT)
         if (r == 0 && (ok || !d.faulted)) ln.unpin();
-        else ln.pinned.clear();
+        else leak_pins(d.id, ln);  // released once its streams drain (release_leaked_pins)
         std::lock_guard<std::mutex> lk(d.mu);
         if (ok && r == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
         ln.n = 0;
@@ -1952,6 +2009,7 @@ int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kin
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const LaunchOpts o = make_opts(ctx, 0, n);
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
@@ -1971,6 +2029,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
@@ -2026,6 +2085,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const uint32_t n = (uint32_t)N;
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
   ctx->count_call(n);
@@ -2087,6 +2147,7 @@ int tmv_validator_set_hashes(tmv_ctx *ctx, const uint8_t *pk, const uint8_t *key
   const size_t o_na = in_bytes, o_nb = o_na + 32ull * n, o_out = o_nb + 32ull * n;
   const size_t dev_bytes = o_out + 32ull * n_sets;
   hipStream_t s = context_stream(d);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   if ((e = wait_stream(d, s)) != hipSuccess) return wait_rc(e);  // staging may still feed an earlier call
   if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
@@ -2145,6 +2206,7 @@ int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off
   const size_t o_na = in_bytes, o_nb = o_na + 32ull * n_leaves, o_out = o_nb + 32ull * n_leaves;
   const size_t dev_bytes = o_out + 32ull * n_trees;
   hipStream_t s = context_stream(d);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   if ((e = wait_stream(d, s)) != hipSuccess) return wait_rc(e);  // staging shared with tmv_validator_set_hashes
   if ((e = d.h_valset.ensure(in_bytes, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
   if ((e = d.d_valset.ensure(dev_bytes, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
@@ -2195,6 +2257,7 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   hipError_t e = hipSetDevice(dev->id);
   if (e != hipSuccess) { set_error("hipSetDevice", e); return TMV_ERR_NO_DEVICE; }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
+  if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const LaunchOpts o = make_opts(ctx, 0, n, false, true);
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);

@@ -7,7 +7,7 @@ next #1):
   8), shard.all_gather_statuses (int8 statuses with the sr25519 Add errors
   -1 / -2) and the MAX all-reduce of the timing -- on device tensors, each
   compared with the local vector.
-* Multi-device contexts: with TMV_LOGICAL_DEVICES=2 / 3, tmv_open gives
+* Multi-device contexts: tmv_open_logical(mask, 2 / 3) (test aid) gives
   GPU 0 to the context as 2 / 3 devices, each with its own streams, host
   lanes, workspaces and key cache, so run_batch's shard plan (one
   contiguous shard per device, chunks over each device's lanes, harvest in
@@ -90,11 +90,7 @@ def contexts():
         pytest.skip("no GPU")
     out = {}
     for k in (1, 2, 3):
-        os.environ["TMV_LOGICAL_DEVICES"] = str(k)
-        try:
-            out[k] = N.Context(1)
-        finally:
-            os.environ.pop("TMV_LOGICAL_DEVICES", None)
+        out[k] = N.Context(1, logical=k)  # tmv_open_logical (test aid)
         assert out[k].num_devices() == k
     yield out
     for c in out.values():

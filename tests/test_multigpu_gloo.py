@@ -136,7 +136,10 @@ def test_bench_control_flow_world2():
     assert len(lines) == 1, out.stdout[-2000:]
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["steps"] == 7 and r["warmup"] == 2 and r["value"] > 0
-    assert r["config"]["parallelism"] == "shard2" and r["config"]["batches_per_step"] == 3
+    # the rank count and backend the process group reported (a SCALE record shows them)
+    assert r["config"]["parallelism"] == "shard2 (gloo, process group world size 2)"
+    assert r["config"]["batches_per_step"] == 3
+    assert r["run_timing"]["setup_s_max_over_ranks"] > 0
     # value = every rank's signatures: 2 ranks x 7 steps x 3 batches x 500
     assert abs(r["value"] * r["ms_per_step"] * 7e-3 / (2 * 7 * 3 * 500) - 1) < 1e-3
     assert "STUB" in r["data"]
