@@ -155,6 +155,44 @@ def accum_entries_per_sig(m: int = 64, c: int = 5, samples: int = 4000, seed: in
     return tot / samples + nonzero(rng.randrange(l_order), w) / m
 
 
+# Algorithmic int32 products of each pipeline kernel per launch (SURVEY 8(d)'s
+# unit: a field multiplication = 100 32x32->64 products; a squaring needs 55).
+FE_MUL, FE_SQ = 100, 55
+# ge_decode_zip215 (255 squarings, 19 multiplications: y^2, d y^2, v^3, v^7,
+# the (p-5)/8 power, the check, T) + the Niels / cached form of the point (1)
+DECODE_PRODUCTS = 255 * FE_SQ + 20 * FE_MUL
+BARRETT_PRODUCTS = 9 * 9 + 9 * 8  # sc_reduce512 (32x32 word products)
+QDBL = 4 * FE_SQ + 4 * FE_MUL     # one point doubling (quad: a squaring + a multiply per lane)
+QADD = 8 * FE_MUL                 # one point addition + conversion to extended
+QCACHED = 4 * FE_MUL              # extended -> cached
+QTABLE = QDBL + 6 * QADD + 8 * QCACHED  # (m+1) P, m < 8, cached
+WPART_BUCKET = 17 * FE_MUL        # running sums per bucket: U += B (cached U: 9), T += U (8)
+
+
+def kernel_products(n, m, c, fallback_entries=0, groups_failed=0, located=False, half_scalars=True):
+    """Algorithmic products of each kernel of one batch-equation launch of n
+    ed25519 entries (groups of m, c-bit windows): prep (two decodes + the
+    Barrett reduction of the hash; SHA-512 has no products), bucket sums
+    (one mixed addition per bucket entry), running sums (17 multiplications
+    per bucket), Horner ((W-1) c + 3 doublings + W-1 additions per group), the
+    per-entry fallback (half-size scalars: two 8-entry tables, 124 doublings,
+    96 additions; full k: 252 doublings) and, located, the second MSM over
+    the failing groups (the same bucket and running-sum work per group, the R
+    weights a few bits longer)."""
+    W, H = -(-254 // c), 1 << (c - 1)
+    G = -(-n // m)
+    e = accum_entries_per_sig(m=m, c=c)
+    Gl = groups_failed if located else 0
+    per_entry = 2 * QTABLE + QCACHED + ((124 + 3) * QDBL + 96 * QADD if half_scalars else (252 + 3) * QDBL + 96 * QADD)
+    return {
+        "k_prep_fused": n * (2 * DECODE_PRODUCTS + BARRETT_PRODUCTS),
+        "k_msm_accum": (n + Gl * m) * e * 7 * FE_MUL,
+        "k_msm_wpart": (G + Gl) * W * (H * WPART_BUCKET + FE_MUL),
+        "k_msm_horner": (G + Gl) * (((W - 1) * c + 3) * QDBL + (W - 1) * QADD),
+        "fallback": fallback_entries * per_entry,
+    }
+
+
 def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: int = 150_000):
     """The runtime's batch-equation shape for an uncached ed25519 launch of
     n_launch entries (tmverify_runtime.cpp msm_params): groups of 128 from
@@ -390,12 +428,31 @@ class _HostEvent:
         return (other.t - self.t) * 1e3
 
 
-def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method):
-    """The whole pipeline against SURVEY 8(d)'s canonical unit: verifies/s x
-    2.7e5 int32 products per single-verify-equivalent signature / the
-    multiply peak.  The batch equation executes fewer products than that
-    unit, so the ratio can exceed 1: it is reported as canonical_ratio, never
-    as the roofline fraction."""
+KFRACS_FILE = os.path.join("profiles", "r05", "kernel_fracs.json")
+
+
+def _kernel_fracs():
+    """Per-kernel fractions of single launches (tools/kernel_fracs.py over the
+    committed kernel trace and PMC pass of tools/launch_alone.py --stats)."""
+    try:
+        with open(os.path.join(REPO, KFRACS_FILE)) as f:
+            return json.load(f)
+    except Exception:
+        return {}
+
+
+def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method, n_launch=0, ms_per_step=0.0):
+    """The whole pipeline.  executed_mad_frac: the v_mad_i64_i32 lane-ops one
+    launch of this size executes (PMC SQ_INSTS_VALU_INT64 per kernel x its
+    static v_mad_i64_i32 share, tools/isa_mix.py; committed pass at this
+    launch size) / this run's ms_per_step / the measured multiply peak -- a
+    true fraction (each counted op is one issued multiply-add).  Also the
+    per-kernel algorithmic fractions of single launches of this size and of
+    the 125k shard (the 1/8 of the north_star's 1M batch), and
+    canonical_ratio: verifies/s x SURVEY 8(d)'s 2.7e5 products per
+    single-verify-equivalent signature / peak, which the batch equation
+    exceeds (it does less work than single verifies): a ratio, never the
+    roofline fraction."""
     out = {"canonical_ratio": round(gpu_rate * MULS_PER_SIG / peak, 4),
            "canonical_note": "verifies/s of this GPU x 2.7e5 canonical products per signature (SURVEY 8(d)) / peak: "
                              "the batch equation does less work than a single verify, so this ratio exceeds 1 and is "
@@ -408,12 +465,31 @@ def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method):
            "executed": pmc.get("executed"),
            "pmc_kernels": _pmc_kernels(method),
            "peak": round(peak / 1e12, 4), "unit": "Tmul/s"}
-    ex = pmc.get("executed") or {}
-    if ex.get("int64_lane_ops_per_sig"):
-        # every 64-bit VALU lane-op (products, carry adds, shifts) per second
-        # against the v_mad_i64_i32 peak: an op rate, not a fraction of peak
-        # multiply work (it can exceed 1), so reported as a ratio
-        out["executed_int64_op_ratio"] = round(gpu_rate * ex["int64_lane_ops_per_sig"] / peak, 4)
+    kf = _kernel_fracs()
+    by_n = {L["n"]: L for L in kf.get("launches", [])}
+    if method == "batch" and n_launch in by_n:
+        L = by_n[n_launch]
+        mads = sum(k["int64_lane_ops"] * k["mad_share_static"] for k in L["kernels"].values()
+                   if "int64_lane_ops" in k)
+        if mads and ms_per_step:
+            out["executed_mad_frac"] = round(mads / (ms_per_step * 1e-3) / peak, 4)
+            out["executed_mad_note"] = (f"{mads:.4g} v_mad_i64_i32 lane-ops per launch of {n_launch} signatures (PMC "
+                                        "SQ_INSTS_VALU_INT64 x 64 lanes x each kernel's static v_mad_i64_i32 share, "
+                                        f"{KFRACS_FILE}) / this run's ms_per_step / peak; the same launch alone: "
+                                        f"{L.get('pipeline_executed_mad_frac')}")
+    if kf:
+        out["kernel_fracs"] = {
+            str(L["n"]): {"launch_span_us": L["launch_span_us"], "verifies_per_s": L["verifies_per_s"],
+                          "pipeline_algorithmic_frac": L["pipeline_algorithmic_frac"],
+                          "pipeline_executed_mad_frac": L.get("pipeline_executed_mad_frac"),
+                          "kernels": {k: {x: v[x] for x in ("us", "frac", "executed_mad_frac") if x in v}
+                                      for k, v in L["kernels"].items()}}
+            for L in kf.get("launches", [])}
+        out["kernel_fracs_note"] = (f"single launches alone ({KFRACS_FILE}: rocprofv3 kernel trace + PMC of "
+                                    "tools/launch_alone.py --stats): frac = the kernel's algorithmic products "
+                                    "(bench.kernel_products: decodes, bucket entries, running sums, Horner, fallback "
+                                    "entries of that launch) / its time / peak; executed_mad_frac = its executed "
+                                    "v_mad_i64_i32 lane-ops / its time / peak")
     return out
 
 
@@ -431,6 +507,13 @@ def _dominant_file():
 def _isa_mix():
     """Static instruction mix of k_msm_accum<16> (tools/isa_mix.py), newest
     committed profile first."""
+    path = os.path.join(REPO, "profiles", "r05", "isa_mix.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            m = json.load(f).get("kernels", {}).get("k_msm_accum<16>")
+        if m and m.get("mad_share_of_int64"):
+            m["source"] = "profiles/r05/isa_mix.json"
+            return m
     for d in ("r04", "r03", "r02_close"):
         path = os.path.join(REPO, "profiles", d, "isa_mix_accum.json")
         if os.path.exists(path):
@@ -995,7 +1078,7 @@ def main():
                                    "batches, context / workspaces, warmup); device memory = total - free on the "
                                    "rank's GPU after the timed region (every process on that GPU)"},
             **extras,
-            "roofline": _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, args.method),
+            "roofline": _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, args.method, K * n, elapsed / steps * 1e3),
         }
         if ktimes.get("k_msm_accum", (0, 0))[1] and args.method == "batch":
             result["roofline"] = _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps,

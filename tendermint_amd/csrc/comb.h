@@ -20,6 +20,22 @@ __device__ __forceinline__ void recode16_store(int8_t *dst, const uint32_t s[8],
   }
 }
 
+// Signed radix-16 recoding into ND digits, the top one absorbing the carry
+// (a value below 2^(4 ND - 1) gives a top digit <= 8)
+template <int ND>
+__device__ __forceinline__ void recode16_n(int8_t *dst, const uint32_t s[8]) {
+  int carry = 0;
+#pragma unroll
+  for (int i = 0; i < ND; i++) {
+    int e = (int)((s[i >> 3] >> (4 * (i & 7))) & 15) + carry;
+    if (i < ND - 1) {
+      carry = (e + 8) >> 4;
+      e -= carry * 16;
+    }
+    dst[i] = (int8_t)e;
+  }
+}
+
 // Signed radix-256 recoding (32 digits in [-128, 127], top digit absorbs the
 // carry) for the fixed base B, written to LDS.
 __device__ __forceinline__ void recode256_store(int8_t *dst, const uint32_t s[8]) {

@@ -47,6 +47,7 @@
 namespace tmv {
 
 constexpr uint32_t kMsmWideRows = 65536;     // (group, window) rows from which k_msm_wpart runs one lane per window
+constexpr uint32_t kLocParts = 4;            // running-sum lanes per window of the located pass (few live groups)
 constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 8, 16 or 32
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
@@ -120,6 +121,13 @@ struct MsmParams {
   // profiles/r03/ab_join_compact.txt.)
   TMV_HD uint32_t bucket(uint32_t w, uint32_t i) const { return w * H + i; }
   TMV_HD uint32_t chunks_per_group() const { return cap / L; }
+  // running-sum lanes per window of the located fallback's second MSM: its
+  // grid covers every group but only the failing ones (~10-25%) are live, so
+  // the chain, not the work, sets its time -- 2 H / P + 3 P + log2(H / P)
+  // additions instead of 2 H (c = 6: 31 instead of 64)
+  TMV_HD uint32_t loc_parts() const { return merged ? P : (H >= kLocParts ? (P > kLocParts ? P : kLocParts) : P); }
+  // window-part slots the workspace holds per (group, window)
+  TMV_HD uint32_t wpart_slots() const { return loc_parts() > P ? loc_parts() : P; }
 
   static MsmParams make(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false) {
     MsmParams p;
@@ -211,7 +219,7 @@ struct MsmWork {
     const size_t G = p.groups, bk = (size_t)G * p.buckets_per_group(), ent = (size_t)G * p.cap;
     const size_t chunks = ent / p.L;
     size_t b = (2ull * n + 1) * kNielsPer * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
-               2 * chunks * sizeof(ge_p3) + 4 * chunks + G * p.W * (2ull * p.P + 1) * sizeof(ge_p3) + G + 2 * G +
+               2 * chunks * sizeof(ge_p3) + 4 * chunks + G * p.W * (2ull * p.wpart_slots() + 1) * sizeof(ge_p3) + G + 2 * G +
                17 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
     else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
@@ -234,7 +242,7 @@ struct MsmWork {
     w.part_first = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.part_last = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.join_b = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * chunks);
-    w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.P * sizeof(ge_p3));
+    w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.wpart_slots() * sizeof(ge_p3));
     w.wsum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * sizeof(ge_p3));
     w.group_ok = b + o; o = up(o + G);
     w.sort_ovf = b + o; o = up(o + 2 * G);

@@ -1477,6 +1477,16 @@ static uint32_t locate_min() {
 
 uint32_t locate_min_entries() { return locate_min(); }
 
+// TMV_LOC_PARTS=1: the located pass's running sums on one lane per window
+// (as the primary pass of a wide launch), for A/B
+static bool loc_parts_env() {
+  static const bool one = [] {
+    const char *e = getenv("TMV_LOC_PARTS");
+    return e && !strcmp(e, "1");
+  }();
+  return one;
+}
+
 // TMV_LOC_SUBCHECK=1: groups the located search cannot name (two or more
 // bad entries, ~2% of C2's groups of 128) get sub-group checks before the
 // per-entry fallback instead of all their entries verified one by one.  Less
@@ -1510,7 +1520,7 @@ static Ed25519Work work_view(Ed25519Work w, uint64_t e0) {
   w.Rc += 4 * e0;
   w.k += 8 * e0;
   w.flags += 4 * e0;
-  w.tabA += 32 * e0;
+  w.tabA += 64 * e0;  // k_verify_quad's stride (k_msm_subcheck, tail only, uses 32 of it)
   return w;
 }
 static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0) {
@@ -1606,9 +1616,11 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t n_slots = p.groups << p.m_log2;
-    if ((e = launch_buckets(mw.loc_count, n_slots, mw, p, stream, false)) != hipSuccess) return e;
+    MsmParams pl = p;  // running sums split over loc_parts() lanes per window (TMV_LOC_PARTS=1: one)
+    pl.P = loc_parts_env() ? p.P : p.loc_parts();
+    if ((e = launch_buckets(mw.loc_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
-                       mw.loc_count, n_slots, mw, p, nullptr, 0u);
+                       mw.loc_count, n_slots, mw, pl, nullptr, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int sub2 = loc_subcheck() ? 1 : 0;
     hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p, sub2);
@@ -1700,6 +1712,35 @@ hipError_t launch_batch_check_tail(bool sr, const uint8_t *pk, const uint8_t *si
                                    stream);
   return launch_tail<false>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(),
                             stream);
+}
+
+hipError_t launch_batch_check_part_idx(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                       const uint32_t *msg_off, const uint32_t *idx, uint32_t nb, uint32_t e0,
+                                       uint32_t e1, const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                                       const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (e0 >= e1 || e1 > nb || (e0 & (p.m() - 1))) return hipErrorInvalidValue;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  const uint32_t g0 = e0 >> p.m_log2;
+  MsmParams pp = p;
+  pp.groups = ((e1 - e0) + p.m() - 1) >> p.m_log2;
+  w.niels = mw.pts;
+  // the entries stay where they are (idx holds their global indices, out is
+  // indexed by them); the work arrays are views at slot e0
+  if (sr)
+    return launch_part<true>(pk, sig, msg, msg_off, idx + e0, nullptr, e1 - e0, e0, btab_q, prefix, work_view(w, e0),
+                             msm_view(mw, p, nb, g0), pp, seed, out, aligned, fallback_compact(), stream);
+  return launch_part<false>(pk, sig, msg, msg_off, idx + e0, nullptr, e1 - e0, e0, btab_q, prefix, work_view(w, e0),
+                            msm_view(mw, p, nb, g0), pp, seed, out, aligned, fallback_compact(), stream);
+}
+
+hipError_t launch_batch_check_tail_idx(bool sr, const uint8_t *pk, const uint8_t *sig, const uint32_t *idx, uint32_t n,
+                                       const fe *btab_q, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                                       const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
+  w.niels = mw.pts;
+  if (sr) return launch_tail<true>(sig, idx, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(), stream);
+  return launch_tail<false>(sig, idx, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(), stream);
 }
 
 // Key-merged form: one quad per item.  Items [0, n_runs) are runs of one key

@@ -324,6 +324,16 @@ TMV_DEV bool is_identity_times8(const fe &p) {
   return (z0 & z1) != 0;
 }
 
+// Ristretto identity of a P3Q point (equal to O modulo the 4-torsion: X == 0
+// or Y == 0).  Quad verdict on every lane.
+TMV_DEV bool is_ristretto_identity(const fe &p) {
+  const int c = lane4();
+  const int zero = (c <= 1 && fe_is_zero(p)) ? 1 : 0;  // lane 0: X, lane 1: Y
+  const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
+  const int z1 = __builtin_amdgcn_mov_dpp(zero, qp(1, 1, 1, 1), 0xF, 0xF, false);
+  return (z0 | z1) != 0;
+}
+
 // Equality of two P3Q points: X1 Z2 == X2 Z1 and Y1 Z2 == Y2 Z1.  Quad
 // verdict on every lane.
 TMV_DEV bool p3_equal(const fe &a, const fe &b) {

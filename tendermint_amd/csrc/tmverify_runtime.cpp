@@ -200,6 +200,8 @@ struct HostLane {
   // `join` orders the launch's tail after them
   hipStream_t helper = nullptr;
   hipEvent_t join = nullptr;
+  // streamed mixed chunks: one event per part after its kind partition
+  std::vector<hipEvent_t> part_split;
   // caller pages pinned for the chunk in flight (streamed path, direct DMA);
   // unregistered when the chunk is harvested
   std::vector<void *> pinned;
@@ -334,6 +336,13 @@ uint32_t g_host_chunk = 262144;
 // other host batches -- 1M entries in two 500k chunks, the second's copy
 // beside the first's kernels (TMV_MIXED_CHUNK).
 uint32_t g_mixed_chunk = 786432;
+// Mixed batches on the batch equation are streamed like one-kind ones
+// (mixed_check_streamed): TMV_MIXED_STREAM=0 turns it off (then g_mixed_chunk
+// applies).  Read at every call (A/B and tests).
+static bool mixed_stream_on() {
+  const char *e = getenv("TMV_MIXED_STREAM");
+  return !(e && !strcmp(e, "0"));
+}
 // Lanes the chunks rotate over (TMV_HOST_LANES, 1..kLanes).
 uint32_t g_host_lanes = 2;
 // Bound on every wait for device work (TMV_DEVICE_TIMEOUT_MS, 0 = none).
@@ -360,6 +369,7 @@ uint32_t g_sr_group_log2 = 0;      // TMV_SR_GROUP_LOG2: group size of uncached 
 // call: chunks of up to 4 M (one pipeline) 106 M/s, 2 M (two pipelines of
 // 1.28 M on two lanes) 98 M/s, 1 M 87 M/s (profiles/r03/e2e_chunk.txt)
 uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 22;
+constexpr uint32_t kMaxStreamParts = 512;  // bound on a streamed mixed chunk's parts (4 M / 128k + 1 = 33 by default)
 // Streamed parts DMA straight from the caller's buffers: each part pins the
 // whole pages of its pk / sig / msg spans (hipHostRegister, disjoint page
 // ranges part to part) while earlier parts run, and only the bytes outside
@@ -709,24 +719,35 @@ static int init_device(Device &d) {
   if (e != hipSuccess) { set_error("hipMalloc(btable)", e); return TMV_ERR_NOMEM; }
   e = hipMemcpy(d.d_btable, table.data(), bytes, hipMemcpyHostToDevice);
   if (e != hipSuccess) { set_error("hipMemcpy(btable)", e); return TMV_ERR_NO_DEVICE; }
-  // quad B table: entry m = (m+1)B, m < kBaseQuadEntries, as (ymx, ypx, xy2d, 1)
-  std::vector<tmv::fe> bq(4 * tmv::kBaseQuadEntries);
+  // quad B tables: entry m = (m+1)B, then entry kBaseQuadEntries + m =
+  // (m+1)[2^128]B (the half-size scalars' top digits), m < kBaseQuadEntries,
+  // as (ymx, ypx, xy2d, 1)
+  std::vector<tmv::fe> bq(2 * 4 * tmv::kBaseQuadEntries);
   {
-    tmv::ge_p3 B, P;
+    tmv::ge_p3 B;
     tmv::ed25519_base_point(B);
-    tmv::ge_cached bc;
-    tmv::ge_p3_to_cached(bc, B);
-    P = B;
-    for (int m = 0; m < tmv::kBaseQuadEntries; m++) {
-      tmv::ge_precomp pc;
-      tmv::ge_p3_to_precomp(pc, P);
-      bq[4 * m + 0] = pc.ymx;
-      bq[4 * m + 1] = pc.ypx;
-      bq[4 * m + 2] = pc.xy2d;
-      tmv::fe_one(bq[4 * m + 3]);
-      tmv::ge_p1p1 t;
-      tmv::ge_add(t, P, bc);
-      tmv::ge_p1p1_to_p3(P, t);
+    for (int h = 0; h < 2; h++) {
+      if (h == 1)
+        for (int d = 0; d < 128; d++) {  // B <- [2^128]B
+          tmv::ge_p1p1 t;
+          tmv::ge_p3_dbl(t, B);
+          tmv::ge_p1p1_to_p3(B, t);
+        }
+      tmv::ge_cached bc;
+      tmv::ge_p3_to_cached(bc, B);
+      tmv::ge_p3 P = B;
+      for (int m = 0; m < tmv::kBaseQuadEntries; m++) {
+        tmv::ge_precomp pc;
+        tmv::ge_p3_to_precomp(pc, P);
+        tmv::fe *o = &bq[4 * (h * tmv::kBaseQuadEntries + m)];
+        o[0] = pc.ymx;
+        o[1] = pc.ypx;
+        o[2] = pc.xy2d;
+        tmv::fe_one(o[3]);
+        tmv::ge_p1p1 t;
+        tmv::ge_add(t, P, bc);
+        tmv::ge_p1p1_to_p3(P, t);
+      }
     }
   }
   e = hipMalloc(&d.d_btab_q, bq.size() * sizeof(tmv::fe));
@@ -996,7 +1017,7 @@ static Workspace *reserve_work(Device &d, uint32_t n, bool mixed, hipStream_t s,
   }
   Workspace &w = *slot;
   const size_t need = tmv::Ed25519Work::bytes(n);
-  const size_t idx_need = 2ull * 4 * n + 64;
+  const size_t idx_need = 2ull * 4 * n + 64 + 4ull * 2 * kMaxStreamParts;  // + streamed mixed parts' cursors
   const size_t msm_need = mp ? tmv::MsmWork::bytes(n, *mp) : 0;
   const size_t msm2_need = mp ? tmv::MsmWork::bytes(n, mp2 ? *mp2 : *mp) : 0;
   if (need > w.work.cap || (mixed && (need > w.work2.cap || idx_need > w.idx.cap)) || msm_need > w.msm.cap ||
@@ -1082,6 +1103,116 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   ws->counts = nullptr;
   ws->loc[0] = tmv::locate_enabled(n, o.p) ? mw.loc_count : nullptr;
   ws->loc[1] = nullptr;
+  (void)hipEventRecord(ws->done, s);
+  return 0;
+}
+
+// Streamed mixed ed25519 + sr25519 chunk (SURVEY 8(a) rows 7 / G-I with
+// crypto/batch/batch.go:11-21's mixed batches): the inputs land part by part
+// (feed), each part is split by key kind on the device into the two kinds'
+// work-slot lists at bases the host knows (it counts each part's kinds from
+// the caller's kind array), and each kind's pipeline runs the throughput
+// stages of the groups the parts so far complete -- the ed25519 pipeline on
+// s, the sr25519 one on s2 -- then one tail per kind (Horner, fallback).  The
+// same kernels and the same validity vector as the unstreamed mixed launch;
+// only the part schedule differs.
+static int mixed_check_streamed(Device &d, const LaunchOpts &o, const uint8_t *kind_h, const uint8_t *kind_d,
+                                const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
+                                uint32_t n, uint8_t *out, hipStream_t s, hipStream_t s2, hipEvent_t join,
+                                std::vector<hipEvent_t> &split_ev, const PartFeeder &feed) {
+  int rc;
+  Workspace *ws = reserve_work(d, n, true, s, &rc, &o.p_ed, &o.p);
+  if (!ws) return rc;
+  if (!s2) s2 = s;
+  tmv::Ed25519Work w_ed = tmv::Ed25519Work::carve(ws->work.ptr, n);
+  tmv::Ed25519Work w_sr = tmv::Ed25519Work::carve(ws->work2.ptr, n);
+  // workspaces carved for n slots per kind (the kinds' counts are known only
+  // part by part); the pipelines' B point sits at slot 2n of each
+  tmv::MsmWork m_ed = tmv::MsmWork::carve(ws->msm.ptr, n, o.p_ed);
+  tmv::MsmWork m_sr = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p);
+  uint32_t *ib = static_cast<uint32_t *>(ws->idx.ptr);
+  uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n, *cursor = ib + 16 + 2ull * n;
+  // parts: the one-kind schedule (a short first part), at most kMaxStreamParts
+  uint32_t part_len = g_stream_part;
+  while ((n - std::min(n, g_stream_first) + part_len - 1) / part_len + 1 > kMaxStreamParts) part_len *= 2;
+  std::vector<uint32_t> b{0};
+  for (uint32_t want = g_stream_first; b.back() < n; want = part_len) b.push_back(std::min<uint64_t>(n, (uint64_t)b.back() + want));
+  const size_t parts = b.size() - 1;
+  hipError_t e;
+  if ((e = hipMemsetAsync(ib, 0, 64, s)) != hipSuccess ||
+      (e = hipMemsetAsync(cursor, 0, 8ull * parts, s)) != hipSuccess) {
+    set_error("hipMemsetAsync", e);
+    return TMV_ERR_LAUNCH;
+  }
+  while (split_ev.size() < parts) {
+    hipEvent_t ev;
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) {
+      set_error("hipEventCreate", e);
+      return TMV_ERR_NO_DEVICE;
+    }
+    split_ev.push_back(ev);
+  }
+  const uint32_t g_ed = o.p_ed.m(), g_sr = o.p.m();  // group sizes
+  uint32_t base_ed = 0, base_sr = 0, done_ed = 0, done_sr = 0;  // slots assigned / slots launched
+  for (size_t j = 0; j < parts; j++) {
+    const uint32_t a = b[j], z = b[j + 1];
+    hipEvent_t ready = nullptr;
+    if ((rc = feed(a, z, &ready)) != 0) return rc;
+    uint32_t c_ed = 0, c_sr = 0;
+    for (uint32_t i = a; i < z; i++) {
+      c_ed += kind_h[i] == TMV_KIND_ED25519;
+      c_sr += kind_h[i] == TMV_KIND_SR25519;
+    }
+    if ((e = hipStreamWaitEvent(s, ready, 0)) != hipSuccess) { set_error("part wait", e); return TMV_ERR_LAUNCH; }
+    if ((e = tmv::launch_partition_range(kind_d, a, z, base_ed, base_sr, cursor + 2 * j, counts, idx_ed, idx_sr, out,
+                                         s)) != hipSuccess ||
+        (e = hipEventRecord(split_ev[j], s)) != hipSuccess) {
+      set_error("part partition", e);
+      return TMV_ERR_LAUNCH;
+    }
+    base_ed += c_ed;
+    base_sr += c_sr;
+    const bool last = j + 1 == parts;
+    // slots of whole groups now assigned (the last part: every slot)
+    const uint32_t hi_ed = last ? base_ed : base_ed / g_ed * g_ed, hi_sr = last ? base_sr : base_sr / g_sr * g_sr;
+    if (hi_ed > done_ed) {
+      e = tmv::launch_batch_check_part_idx(false, pk, sig, msg, off, idx_ed, n, done_ed, hi_ed, d.d_btab_q, d.d_prefix,
+                                           w_ed, m_ed, o.p_ed, o.seed[0], out, s);
+      if (e != hipSuccess) { set_error("mixed part launch", e); return TMV_ERR_LAUNCH; }
+      done_ed = hi_ed;
+    }
+    if (hi_sr > done_sr) {
+      if ((e = hipStreamWaitEvent(s2, split_ev[j], 0)) != hipSuccess) { set_error("part wait", e); return TMV_ERR_LAUNCH; }
+      e = tmv::launch_batch_check_part_idx(true, pk, sig, msg, off, idx_sr, n, done_sr, hi_sr, d.d_btab_q, d.d_prefix,
+                                           w_sr, m_sr, o.p, o.seed[1], out, s2);
+      if (e != hipSuccess) { set_error("mixed part launch", e); return TMV_ERR_LAUNCH; }
+      done_sr = hi_sr;
+    }
+  }
+  // the tails: ed25519 on s, sr25519 on s2 (after its last partition), joined into s
+  if ((e = hipStreamWaitEvent(s2, split_ev[parts - 1], 0)) != hipSuccess) { set_error("part wait", e); return TMV_ERR_LAUNCH; }
+  if ((e = tmv::launch_batch_check_tail_idx(true, pk, sig, idx_sr, base_sr, d.d_btab_q, w_sr, m_sr, o.p, o.seed[1], out,
+                                            s2)) != hipSuccess ||
+      (e = tmv::launch_batch_check_tail_idx(false, pk, sig, idx_ed, base_ed, d.d_btab_q, w_ed, m_ed, o.p_ed, o.seed[0],
+                                            out, s)) != hipSuccess) {
+    set_error("mixed tail launch", e);
+    return TMV_ERR_LAUNCH;
+  }
+  if (s2 != s && ((e = hipEventRecord(join, s2)) != hipSuccess || (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess)) {
+    set_error("part join", e);
+    return TMV_ERR_LAUNCH;
+  }
+  ws->group_ok[0] = m_ed.group_ok;
+  ws->group_ok[1] = m_sr.group_ok;
+  ws->sub_ok[0] = o.p_ed.sub ? m_ed.sub_ok : nullptr;
+  ws->sub_ok[1] = o.p.sub ? m_sr.sub_ok : nullptr;
+  ws->groups = (base_ed + g_ed - 1) / g_ed;
+  ws->m_log2 = o.p_ed.m_log2;
+  ws->m_log2_sr = o.p.m_log2;
+  ws->n = n;
+  ws->counts = counts;
+  ws->loc[0] = tmv::locate_enabled(base_ed, o.p_ed) ? m_ed.loc_count : nullptr;
+  ws->loc[1] = tmv::locate_enabled(base_sr, o.p) ? m_sr.loc_count : nullptr;
   (void)hipEventRecord(ws->done, s);
   return 0;
 }
@@ -1287,6 +1418,8 @@ void tmv_close(tmv_ctx *ctx) {
       if (l.copy) (void)hipStreamSynchronize(l.copy);
       for (hipEvent_t ev : l.part_ready) (void)hipEventDestroy(ev);
       l.part_ready.clear();
+      for (hipEvent_t ev : l.part_split) (void)hipEventDestroy(ev);
+      l.part_split.clear();
       if (l.copy) (void)hipStreamDestroy(l.copy);
       l.copy = nullptr;
       if (l.helper) (void)hipStreamSynchronize(l.helper);
@@ -1399,11 +1532,14 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
   }
   if (cached && !merged) o.batch_eq = false;  // key-cached per-entry path
   read_env();
-  if (g_stream && !cached && !vs && (sch == Scheme::Ed25519 || sch == Scheme::Sr25519) && o.batch_eq &&
-      n > g_stream_first) {
-    // streamed: stage and copy part by part, each part's kernels behind its copy
-    if ((e = ln.h_in.ensure(L.total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
-    if ((e = ln.d_in.ensure(L.total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
+  const bool mixed_stream = sch == Scheme::Mixed && mixed_stream_on();
+  if (g_stream && !cached && !vs && (sch == Scheme::Ed25519 || sch == Scheme::Sr25519 || mixed_stream) &&
+      o.batch_eq && n > g_stream_first) {
+    // streamed: stage and copy part by part, each part's kernels behind its
+    // copy (mixed chunks: the kind bytes too, after the other inputs)
+    const size_t kind_at = L.total, in_total = L.total + (mixed_stream ? align16(n) : 0);
+    if ((e = ln.h_in.ensure(in_total, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
+    if ((e = ln.d_in.ensure(in_total, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
     if ((e = ln.h_out.ensure(n, true)) != hipSuccess) { set_error("hipHostMalloc", e); return TMV_ERR_NOMEM; }
     if ((e = ln.d_out.ensure(n, false)) != hipSuccess) { set_error("hipMalloc", e); return TMV_ERR_NOMEM; }
     if (!ln.copy && (e = hipStreamCreateWithFlags(&ln.copy, hipStreamNonBlocking)) != hipSuccess) {
@@ -1415,7 +1551,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
     const uint32_t base = msg_off[lo];
     size_t part = 0;
-    if (g_stream_two && !ln.helper) {
+    if ((g_stream_two || (mixed_stream && g_mixed_two)) && !ln.helper) {
       if (hipStreamCreateWithFlags(&ln.helper, hipStreamNonBlocking) != hipSuccess) ln.helper = nullptr;
       else if (hipEventCreateWithFlags(&ln.join, hipEventDisableTiming) != hipSuccess) ln.join = nullptr;
     }
@@ -1431,9 +1567,10 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
         const uint8_t *src;
         size_t len;
         size_t d0, d1;  // [d0, d1): DMA'd from the caller's pinned pages
-      } sp[3] = {{L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a), 0, 0},
+      } sp[4] = {{L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a), 0, 0},
                  {L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a), 0, 0},
-                 {L.msg + m0, msg + base + m0, m1 - m0, 0, 0}};
+                 {L.msg + m0, msg + base + m0, m1 - m0, 0, 0},
+                 {kind_at + a, mixed_stream ? kind + lo + a : nullptr, mixed_stream ? (size_t)(b - a) : 0, 0, 0}};
       constexpr uintptr_t kPage = 4096;
       const auto t0 = std::chrono::steady_clock::now();
       for (Span &x : sp) {
@@ -1455,9 +1592,10 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
         x.d1 = r1 - s0;
       }
       pin_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      CopySpan cs[6];
+      CopySpan cs[8];
       size_t ncs = 0;
       for (const Span &x : sp) {
+        if (!x.len) continue;
         if (x.d1 == 0) {
           cs[ncs++] = {h + x.at, x.src, x.len};
           continue;
@@ -1498,9 +1636,15 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       return 0;
     };
     tm.mark("stage", n);
-    const int rc = batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off),
-                               n, static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed,
-                               g_stream_two ? ln.helper : nullptr, g_stream_two ? ln.join : nullptr);
+    const int rc =
+        mixed_stream
+            ? mixed_check_streamed(d, o, kind + lo, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg,
+                                   reinterpret_cast<const uint32_t *>(dd + L.off), n,
+                                   static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, g_mixed_two ? ln.helper : nullptr,
+                                   ln.join, ln.part_split, feed)
+            : batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off), n,
+                          static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed, g_stream_two ? ln.helper : nullptr,
+                          g_stream_two ? ln.join : nullptr);
     if (rc != 0) {  // parts already enqueued still use the lane's buffers: drain before returning
       const bool drained = wait_stream(d, ln.copy) == hipSuccess;
       if (ln.helper) (void)wait_stream(d, ln.helper);
@@ -1680,8 +1824,10 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
                           ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
   const bool mixed_batch_eq = sch == Scheme::Mixed && !vs && !(flags & TMV_FLAG_PER_ENTRY) &&
                               ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
+  const bool mixed_streamed = mixed_batch_eq && g_stream && mixed_stream_on();
   const tmh::ShardPlan plan = tmh::plan_shards(
-      n, (uint32_t)ctx->devs.size(), streamable ? g_stream_chunk : (mixed_batch_eq ? g_mixed_chunk : g_host_chunk));
+      n, (uint32_t)ctx->devs.size(),
+      streamable || mixed_streamed ? g_stream_chunk : (mixed_batch_eq ? g_mixed_chunk : g_host_chunk));
   const uint32_t shards = plan.shards;
   // claim g_host_lanes lanes per device (devices in order, so concurrent
   // calls cannot deadlock); released on every return

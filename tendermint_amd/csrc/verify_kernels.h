@@ -10,7 +10,7 @@ namespace tmv {
 
 constexpr int kVerifyBlock = 256;
 constexpr int kQuadBlock = 64;    // one wave = 16 signatures per block
-constexpr int kBaseQuadEntries = 128;  // (m+1)B, m < 128, CachedQ layout (20 KB)
+constexpr int kBaseQuadEntries = 128;  // (m+1)B, m < 128, CachedQ layout (20 KB), then (m+1)[2^128]B
 
 // Per-signature workspace of the latency path (device memory).
 struct Ed25519Work {
@@ -19,8 +19,8 @@ struct Ed25519Work {
   uint32_t *k;     // n x 8 words, k mod l
   uint8_t *flags;  // 4n bytes: decode ok for A (4e), R (4e+1)
   niels_pt *niels; // batch check only (else null): [2e] = -R_e, [2e+1] = -A_e
-  fe *tabA;        // n x 8 x 4 fe: k_verify_quad's tables of -A when kept in global memory
-  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4 + 1280) + 256; }
+  fe *tabA;        // n x 16 x 4 fe: k_verify_quad's tables of -A (8 x 4 fe) and -R (8 x 4 fe) when kept in global memory
+  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4 + 2560) + 256; }
   // carve a workspace for n entries out of base (16-byte aligned pieces)
   static Ed25519Work carve(void *base, uint32_t n) {
     uint8_t *b = static_cast<uint8_t *>(base);
@@ -129,6 +129,24 @@ uint32_t locate_min_entries();
 bool locate_enabled(uint32_t n, const MsmParams &p);
 hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,
                             uint8_t *out, hipStream_t stream);
+// Streamed mixed launches: the entries [lo, hi) of a part go to
+// idx_ed[base_ed ..] / idx_sr[base_sr ..] (bases from the host's count of the
+// earlier parts' kinds; cursor: 2 zeroed words per part).
+hipError_t launch_partition_range(const uint8_t *kind, uint32_t lo, uint32_t hi, uint32_t base_ed, uint32_t base_sr,
+                                  uint32_t *cursor, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, uint8_t *out,
+                                  hipStream_t stream);
+// One kind's pipeline of a streamed mixed launch, over work slots whose
+// entries are idx[e] (global indices into pk / sig / msg_off / out): the
+// throughput stages of slots [e0, e1) (e0 on a group edge, e1 too unless it
+// is the kind's last slot), then, after every part, the tail over n slots.
+// nb (>= n) is the slot bound the workspaces were carved for.
+hipError_t launch_batch_check_part_idx(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
+                                       const uint32_t *msg_off, const uint32_t *idx, uint32_t nb, uint32_t e0,
+                                       uint32_t e1, const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
+                                       const MsmParams &p, const MsmSeed &seed, uint8_t *out, hipStream_t stream);
+hipError_t launch_batch_check_tail_idx(bool sr, const uint8_t *pk, const uint8_t *sig, const uint32_t *idx, uint32_t n,
+                                       const fe *btab_q, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                                       const MsmSeed &seed, uint8_t *out, hipStream_t stream);
 
 // Multi-batch launches (gather_kernels.hip): up to kMaxBatches device
 // batches, passed by value as kernel arguments.

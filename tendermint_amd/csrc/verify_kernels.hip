@@ -15,6 +15,7 @@
 #include "verify_kernels.h"
 #include "kernel_util.h"
 #include "comb.h"
+#include "halfscalar.h"
 #include "ktimer.h"
 
 namespace tmv {
@@ -170,22 +171,83 @@ k_prep_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, co
 
 constexpr int kQuadSigs = kQuadBlock / 4;
 
-// k_verify_quad: acc = sum over 64 signed radix-16 windows of
-// 16*acc + e_i(k)(-A) [+ d_{i/2}(s)B on even windows, radix-256 digits of s
-// against a 128-entry table of B multiples] (Straus, shared doublings), then
-//   ed25519: [8](acc - R) == O          (ZIP-215 cofactored)
-//   sr25519: acc == R (Ristretto equality)
-// Each signature occupies one quad; writes out[i] (ed25519 1/0; sr25519
-// 1/0/-1/-2 as int8).
-// GT: the 8-entry tables of -A live in a global scratch (w.tabA, L2-resident
-// while the wave runs) instead of LDS, so LDS (22.5 KB per wave otherwise)
-// no longer caps residency; each window's entry is loaded before its four
-// doublings, like the B entry.
+// Digits of one quad's scalars in LDS: v (the -A scalar, radix 16: 32
+// digits, 64 on the slow path), b (the B scalar, radix 256: 32 digits), u
+// (the -R scalar, radix 16: 32 digits).
+constexpr int kDigV = 0, kDigB = 64, kDigU = 96, kDigBytes = 128;
+
+// (m+1) P, m < 8, in CachedQ layout, for a P3Q point P (one doubling, six
+// additions; tab[4 m + c] is lane c's coordinate)
+TMV_DEV void quad_multiples(fe *tab, const fe &P) {
+  const int c = threadIdx.x & 3;
+  fe r, Pm, Q, Q0;
+  quad::to_cached(Q0, P);
+  tab[0 * 4 + c] = Q0;
+  quad::dbl(r, P);
+  quad::p1p1_to_p3(Pm, r);
+  quad::to_cached(Q, Pm);
+  tab[1 * 4 + c] = Q;
+  for (int t = 2; t < 8; t++) {
+    quad::add(r, Pm, Q0);
+    quad::p1p1_to_p3(Pm, r);
+    quad::to_cached(Q, Pm);
+    tab[t * 4 + c] = Q;
+  }
+}
+
+// -R in P3Q layout from the prep's R: sr25519 keeps R itself in P3Q (negate
+// X and T); ed25519 keeps its CachedQ (Y-X, Y+X, 2dT, Z), from which
+// (-2X, 2Y, 2Z, -2T) -- the same projective point -- is one multiply per
+// lane: lanes 0 / 1 re-carry (Y-X) -+ (Y+X), lane 2 doubles Z, lane 3
+// scales 2dT by -1/d.
+template <bool SR>
+TMV_DEV void neg_r_p3(fe &P, const fe &Rc) {
+  const int c = threadIdx.x & 3;
+  if (SR) {
+    if (c == 0 || c == 3) fe_neg(P, Rc);
+    else P = Rc;
+    return;
+  }
+  fe o, t, K;
+  quad::fe_dpp<quad::qp(1, 0, 3, 2)>(o, Rc);  // lane 0 <- Y+X, 1 <- Y-X, 2 <- Z, 3 <- 2dT
+  if (c == 0) fe_sub(t, Rc, o);
+  else if (c == 1) fe_add(t, Rc, o);
+  else t = o;
+  if (c == 3) {
+    const uint32_t w[8] = {0x323607aau, 0xda1f0d89u, 0xbd86abd1u, 0xf4a22967u,
+                           0x32463099u, 0xd4e9deebu, 0xeb2a31bcu, 0x3f6f812du};  // -1/d mod p
+    fe_from_words(K, w);
+  } else {
+    fe_zero(K);
+    K.v[0] = c == 2 ? 2 : 1;
+  }
+  quad::qmul(P, t, K);
+}
+
+// k_verify_quad: one signature per quad, with half-size scalars
+// (halfscalar.h): every lane reduces k to (u, v), v == u k (mod l), |u|, v <
+// 2^127, and b = |u| s mod l, then the quad evaluates
+//   acc = sum over 32 signed radix-16 windows of 16 acc + v_i(-A) + u_i(-R)
+//         [+ b_j B + b_(j+16) [2^128]B on even windows, radix-256 digits of b
+//          against the 128-entry tables of B and [2^128]B multiples]
+// (Straus, 124 shared doublings; the B and R terms negated when u < 0) and
+//   ed25519: [8] acc == O       (ZIP-215 cofactored)
+//   sr25519: acc in E[4]        (Ristretto identity)
+// -- the same validity as [8]([s]B - R - [k]A) == O / Ristretto equality for
+// every input (halfscalar.h).  An entry whose reduction does not finish
+// (quotient >= 2^31, ~2^-24 of hash-derived k) or every entry when half_on
+// == 0 takes the full scalars (u = 1, v = k, b = s: 64 windows, 252
+// doublings -- the check of rounds 1-4).  Writes out[i] (ed25519 1/0;
+// sr25519 1/0/-1/-2 as int8).
+// GT: the 8-entry tables of -A and -R live in a global scratch (w.tabA,
+// L2-resident while the wave runs) instead of LDS (40 KB per wave), so LDS
+// does not cap residency; each window's entries are loaded before its four
+// doublings, like the B entries.
 // One 16-entry block (blk) of k_verify_quad; every return before the
 // __syncthreads is block-uniform except the passing-group branch, which
 // k_verify_quad_list never takes.
 template <bool SR, bool GT>
-__device__ __forceinline__ void quad_block(uint32_t blk, fe *tabA_lds, int8_t (*dig)[2][64],
+__device__ __forceinline__ void quad_block(uint32_t blk, fe *tab_lds, int8_t (*dig)[kDigBytes],
                                            const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
                                            const uint32_t *count_ptr, uint32_t n, const Ed25519Work &w,
                                            const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
@@ -193,7 +255,7 @@ __device__ __forceinline__ void quad_block(uint32_t blk, fe *tabA_lds, int8_t (*
                                            const uint8_t *__restrict__ sub_ok,
                                            const uint32_t *__restrict__ fail_list,
                                            const uint32_t *__restrict__ fail_count,
-                                           const uint32_t *__restrict__ fb_list, uint32_t nl) {
+                                           const uint32_t *__restrict__ fb_list, uint32_t nl, int half_on) {
   const uint32_t m = entry_count(count_ptr, n);
   const int c = threadIdx.x & 3;
   const int q = threadIdx.x >> 2;
@@ -266,82 +328,110 @@ __device__ __forceinline__ void quad_block(uint32_t blk, fe *tabA_lds, int8_t (*
     s_ok = sc_is_canonical(s_w);
   }
   if (!s_ok) s_w[7] &= 0x0fffffffu;  // keep the recoding in range; entry is rejected anyway
+  bool fast, neg_u;
   {
     uint32_t k_w[8];
     const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * e);
     const uint4 k0 = kp[0], k1 = kp[1];
     k_w[0] = k0.x; k_w[1] = k0.y; k_w[2] = k0.z; k_w[3] = k0.w;
     k_w[4] = k1.x; k_w[5] = k1.y; k_w[6] = k1.z; k_w[7] = k1.w;
-    // lane 0: k in signed radix 16 (64 digits); lane 1: s in signed radix 256
-    // (32 digits, |d| <= 128, top digit <= 32 since s < 2^253)
-    if (c == 1) recode256_store(&dig[q][1][0], s_w);
-    else recode16_store(&dig[q][0][0], k_w, c == 0);
+    // every lane of the quad reduces the same k (no exchange needed); lane 0
+    // recodes v, lane 1 b, lane 2 u
+    half::Scalars sc;
+    if (half_on == 1 || (half_on == 2 && e % 3 != 0)) {  // 2 (tests): every third entry on the full-k path
+      half::scalars(sc, k_w, s_w);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; t++) { sc.u[t] = t == 0; sc.v[t] = k_w[t]; sc.b[t] = s_w[t]; }
+      sc.fast = false;
+      sc.u_neg = false;
+    }
+    fast = sc.fast;
+    neg_u = sc.u_neg;
+    if (c == 0) {
+      if (fast) recode16_n<32>(&dig[q][kDigV], sc.v);
+      else recode16_n<64>(&dig[q][kDigV], sc.v);
+    } else if (c == 1) {
+      recode256_store(&dig[q][kDigB], sc.b);
+    } else if (c == 2) {
+      recode16_n<32>(&dig[q][kDigU], sc.u);
+    }
   }
   const bool a_ok = w.flags[4 * e] != 0;
   const bool r_ok = w.flags[4 * e + 1] != 0;
 
-  // table of (m+1)(-A), m < 8, in CachedQ layout
-  fe *tabA = GT ? w.tabA + 32ull * e : tabA_lds + q * 32;
-  fe P = w.negA[4ull * e + c];
-  fe r, Pm, Q, Q0;
-  quad::to_cached(Q0, P);
-  tabA[0 * 4 + c] = Q0;
-  quad::dbl(r, P);
-  quad::p1p1_to_p3(Pm, r);
-  quad::to_cached(Q, Pm);
-  tabA[1 * 4 + c] = Q;
-  for (int t = 2; t < 8; t++) {
-    quad::add(r, Pm, Q0);
-    quad::p1p1_to_p3(Pm, r);
-    quad::to_cached(Q, Pm);
-    tabA[t * 4 + c] = Q;
+  // tables of (m+1)(-A) and (m+1)(-R), m < 8, in CachedQ layout
+  fe *tabA = GT ? w.tabA + 64ull * e : tab_lds + q * 64;
+  fe *tabR = tabA + 32;
+  quad_multiples(tabA, w.negA[4ull * e + c]);
+  {
+    fe nR;
+    neg_r_p3<SR>(nR, w.Rc[4ull * e + c]);
+    quad_multiples(tabR, nR);
   }
-  __syncthreads();  // digits (and the LDS table) written by other lanes
+  __syncthreads();  // digits (and the LDS tables) written by other lanes
 
-  fe acc;
+  fe acc, r;
   quad::p3_identity(acc);
-  // The 20 KB table of B multiples is read through L1 (not staged in LDS,
-  // which would cap the kernel near one wave per SIMD); each even window's
-  // entry is loaded before its four doublings so the latency is hidden.
-  for (int wdx = 63; wdx >= 0; wdx--) {
-    const int db = dig[q][1][wdx >> 1];
-    const int ab = db < 0 ? -db : db;
-    const int da = dig[q][0][wdx];
-    const int aa = da < 0 ? -da : da;
-    fe bent, ent;
-    if ((wdx & 1) == 0) bent = btab_q[(ab ? ab - 1 : 0) * 4 + c];
-    ent = tabA[(aa ? aa - 1 : 0) * 4 + c];
-    if (wdx != 63) {
+  fe idq;
+  quad::cached_identity(idq);
+  // windows: 32 (fast) or 64 (full k); the wave runs to its longest quad
+  const int nw = fast ? 32 : 64;
+  const int nw_wave = __ballot(!fast) ? 64 : 32;
+  const fe *btab_hi = btab_q + 4 * kBaseQuadEntries;  // (m+1) [2^128]B
+  // The 40 KB of B tables are read through L1 (not staged in LDS, which
+  // would cap the kernel near one wave per SIMD); each window's entries are
+  // loaded before its four doublings so the latency is hidden.
+  for (int wdx = nw_wave - 1; wdx >= 0; wdx--) {
+    if (wdx >= nw) continue;  // quad-uniform: only the full-k quads run windows 32..63
+    const bool even = (wdx & 1) == 0;
+    const int da = dig[q][kDigV + wdx];
+    const int du = wdx < 32 ? dig[q][kDigU + wdx] : 0;
+    const int db = even ? dig[q][kDigB + (wdx >> 1)] : 0;
+    const int dh = (even && fast) ? dig[q][kDigB + 16 + (wdx >> 1)] : 0;
+    const int aa = da < 0 ? -da : da, au = du < 0 ? -du : du, ab = db < 0 ? -db : db, ah = dh < 0 ? -dh : dh;
+    fe aent = tabA[(aa ? aa - 1 : 0) * 4 + c];
+    fe rent = tabR[(au ? au - 1 : 0) * 4 + c];
+    fe bent, hent;
+    if (even) {
+      bent = btab_q[(ab ? ab - 1 : 0) * 4 + c];
+      if (fast) hent = btab_hi[(ah ? ah - 1 : 0) * 4 + c];
+    }
+    if (wdx != nw - 1) {
 #pragma unroll
       for (int d = 0; d < 4; d++) {
         quad::dbl(r, acc);
         quad::p1p1_to_p3(acc, r);
       }
     }
-    fe idq;
-    quad::cached_identity(idq);
-    fe_cmov(ent, idq, aa == 0);
-    quad::cached_cneg(ent, da < 0);
-    quad::add(r, acc, ent);
+    fe_cmov(aent, idq, aa == 0);
+    quad::cached_cneg(aent, da < 0);
+    quad::add(r, acc, aent);
     quad::p1p1_to_p3(acc, r);
-    if ((wdx & 1) == 0) {  // B digit d_j weighs 256^j = 16^(2j)
-      ent = bent;
-      fe_cmov(ent, idq, ab == 0);
-      quad::cached_cneg(ent, db < 0);
-      quad::add(r, acc, ent);
+    if (wdx < 32) {  // u's digits (the slow path: u = 1, only window 0)
+      fe_cmov(rent, idq, au == 0);
+      quad::cached_cneg(rent, (du < 0) != neg_u);
+      quad::add(r, acc, rent);
       quad::p1p1_to_p3(acc, r);
+    }
+    if (even) {  // b digit j weighs 256^j = 16^(2j); the top 16 digits on [2^128]B
+      fe_cmov(bent, idq, ab == 0);
+      quad::cached_cneg(bent, (db < 0) != neg_u);
+      quad::add(r, acc, bent);
+      quad::p1p1_to_p3(acc, r);
+      if (fast) {
+        fe_cmov(hent, idq, ah == 0);
+        quad::cached_cneg(hent, (dh < 0) != neg_u);
+        quad::add(r, acc, hent);
+        quad::p1p1_to_p3(acc, r);
+      }
     }
   }
   int status;
   if (SR) {
-    const fe Rq = w.Rc[4ull * e + c];
-    const bool eq = quad::ristretto_equal(acc, Rq);
+    const bool eq = quad::is_ristretto_identity(acc);
     status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
   } else {
-    fe Rq = w.Rc[4ull * e + c];
-    quad::cached_cneg(Rq, true);
-    quad::add(r, acc, Rq);
-    quad::p1p1_to_p3(acc, r);
     const bool ok = quad::is_identity_times8(acc) && s_ok && a_ok && r_ok;
     status = ok ? 1 : 0;
   }
@@ -355,11 +445,11 @@ k_verify_quad(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
               uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out, int aligned,
               const uint8_t *__restrict__ group_ok, uint32_t group_log2, const uint8_t *__restrict__ sub_ok,
               const uint32_t *__restrict__ fail_list, const uint32_t *__restrict__ fail_count,
-              const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count) {
-  __shared__ fe tabA_lds[GT ? 4 : kQuadSigs * 8 * 4];
-  __shared__ int8_t dig[kQuadSigs][2][64];
-  quad_block<SR, GT>(blockIdx.x, tabA_lds, dig, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok,
-                     group_log2, sub_ok, fail_list, fail_count, fb_list, fb_list ? *fb_count : 0u);
+              const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count, int half_on) {
+  __shared__ fe tab_lds[GT ? 4 : kQuadSigs * 16 * 4];
+  __shared__ int8_t dig[kQuadSigs][kDigBytes];
+  quad_block<SR, GT>(blockIdx.x, tab_lds, dig, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok,
+                     group_log2, sub_ok, fail_list, fail_count, fb_list, fb_list ? *fb_count : 0u, half_on);
 }
 
 // The located fallback's entry list (k_loc_search) is usually a few entries
@@ -370,13 +460,14 @@ template <bool SR>
 __global__ void __launch_bounds__(kQuadBlock)
 k_verify_quad_list(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
                    uint32_t n, Ed25519Work w, const fe *__restrict__ btab_q, uint8_t *__restrict__ out,
-                   int aligned, const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count) {
-  __shared__ fe tabA_lds[4];
-  __shared__ int8_t dig[kQuadSigs][2][64];
+                   int aligned, const uint32_t *__restrict__ fb_list, const uint32_t *__restrict__ fb_count,
+                   int half_on) {
+  __shared__ fe tab_lds[4];
+  __shared__ int8_t dig[kQuadSigs][kDigBytes];
   const uint32_t nl = *fb_count;
   for (uint32_t blk = blockIdx.x; blk * kQuadSigs < nl; blk += gridDim.x) {
-    quad_block<SR, true>(blk, tabA_lds, dig, sig, idx, count_ptr, n, w, btab_q, out, aligned, nullptr, 0u, nullptr,
-                         nullptr, nullptr, fb_list, nl);
+    quad_block<SR, true>(blk, tab_lds, dig, sig, idx, count_ptr, n, w, btab_q, out, aligned, nullptr, 0u, nullptr,
+                         nullptr, nullptr, fb_list, nl, half_on);
     __syncthreads();  // dig is rewritten by the next block
   }
 }
@@ -408,6 +499,41 @@ k_partition(const uint8_t *__restrict__ kind, uint32_t n, uint32_t *counts, uint
   if (threadIdx.x < 2) {
     const uint32_t t = threadIdx.x;
     base[t] = atomicAdd(&counts[t], wcnt[t][0] + wcnt[t][1] + wcnt[t][2] + wcnt[t][3]);
+  }
+  __syncthreads();
+  if (k > 1) return;
+  uint32_t at = base[k] + (uint32_t)__popcll((k == 0 ? b0 : b1) & below);
+  for (uint32_t w = 0; w < wave; w++) at += wcnt[k][w];
+  (k == 0 ? idx_ed : idx_sr)[at] = i;
+}
+
+// The same split for the entries [lo, hi) of a streamed mixed launch: a
+// part's entries of kind k go to idx_k[base_k + j], j < the part's count of
+// that kind (the host counts each part's kinds, so base_k is known before the
+// part lands); cursor (2 words, zeroed) numbers them, counts[k] accumulates
+// the launch's totals (tmv_metrics / tmv_batch_stats).
+__global__ void __launch_bounds__(256)
+k_partition_range(const uint8_t *__restrict__ kind, uint32_t lo, uint32_t hi, uint32_t base_ed, uint32_t base_sr,
+                  uint32_t *cursor, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, uint8_t *out) {
+  __shared__ uint32_t wcnt[2][4];
+  __shared__ uint32_t base[2];
+  const uint32_t i = lo + blockIdx.x * 256 + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool in = i < hi;
+  const uint8_t k = in ? kind[i] : 255;
+  if (in && k > 1) out[i] = 0;  // unknown key kind: not verified
+  const uint64_t b0 = __ballot(k == 0), b1 = __ballot(k == 1);
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  if (lane == 0) {
+    wcnt[0][wave] = (uint32_t)__popcll(b0);
+    wcnt[1][wave] = (uint32_t)__popcll(b1);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t tot = wcnt[t][0] + wcnt[t][1] + wcnt[t][2] + wcnt[t][3];
+    base[t] = (t ? base_sr : base_ed) + atomicAdd(&cursor[t], tot);
+    atomicAdd(&counts[t], tot);
   }
   __syncthreads();
   if (k > 1) return;
@@ -1031,6 +1157,15 @@ static int quad_table_env() {
   return g;
 }
 
+// Half-size scalars in the per-entry checks (halfscalar.h); TMV_HALF_SCALARS=0
+// verifies with the full k, =2 (tests) puts every third entry on the full-k
+// path beside half-size quads of the same wave (read at every launch, so
+// tests can compare the modes in one process).
+static int half_scalars_on() {
+  const char *e = getenv("TMV_HALF_SCALARS");
+  return !e ? 1 : !strcmp(e, "0") ? 0 : !strcmp(e, "2") ? 2 : 1;
+}
+
 template <bool SR>
 static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig, const uint32_t *idx,
                         const uint32_t *count_ptr, uint32_t n, Ed25519Work w, const fe *btab_q, uint8_t *out,
@@ -1039,14 +1174,18 @@ static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig
                         const uint32_t *fail_count = nullptr, const uint32_t *fb_list = nullptr,
                         const uint32_t *fb_count = nullptr, bool fallback = false) {
   const int forced = quad_table_env();
-  if (forced == 1 || (forced == 0 && fallback))
+  const int half = half_scalars_on();
+  // LDS tables hold 40 KB per wave (3 waves per CU): only while the grid fits
+  // that residency, else global
+  const bool global = forced == 1 || (forced == 0 && (fallback || qblocks > 3u * 256u));
+  if (global)
     hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
                        w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count, fb_list,
-                       fb_count);
+                       fb_count, half);
   else
     hipLaunchKernelGGL((k_verify_quad<SR, false>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
                        w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count, fb_list,
-                       fb_count);
+                       fb_count, half);
 }
 
 static int is_aligned(const void *a, const void *b) {
@@ -1084,7 +1223,7 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
     // at most 16 waves per CU (the kernel fits 5 per SIMD); blocks stride over the list
     const uint32_t grid = qblocks < 256u * 16u ? qblocks : 256u * 16u;
     hipLaunchKernelGGL(k_verify_quad_list<SR>, dim3(grid), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
-                       btab_q, out, aligned, fb_list, fb_count);
+                       btab_q, out, aligned, fb_list, fb_count, half_scalars_on());
     return hipGetLastError();
   }
   launch_quad<SR>(qblocks, stream, sig, idx, count_ptr, n, w, btab_q, out, aligned, group_ok, group_log2, sub_ok,
@@ -1167,6 +1306,15 @@ hipError_t launch_mixed_verify(const uint8_t *kind, const uint8_t *pk, const uin
   e = launch_pipeline<false>(pk, sig, msg, msg_off, idx_ed, counts, n, btab_q, prefix, w_ed, out, stream);
   if (e != hipSuccess) return e;
   return launch_pipeline<true>(pk, sig, msg, msg_off, idx_sr, counts + 1, n, btab_q, prefix, w_sr, out, stream);
+}
+
+hipError_t launch_partition_range(const uint8_t *kind, uint32_t lo, uint32_t hi, uint32_t base_ed, uint32_t base_sr,
+                                  uint32_t *cursor, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr, uint8_t *out,
+                                  hipStream_t stream) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_partition_range, dim3((hi - lo + 255) / 256), dim3(256), 0, stream, kind, lo, hi, base_ed,
+                     base_sr, cursor, counts, idx_ed, idx_sr, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_partition(const uint8_t *kind, uint32_t n, uint32_t *counts, uint32_t *idx_ed, uint32_t *idx_sr,

@@ -6,6 +6,7 @@
 #include <vector>
 #include "../../tendermint_amd/csrc/ed25519_core.h"
 #include "../../tendermint_amd/csrc/sr25519_core.h"
+#include "../../tendermint_amd/csrc/halfscalar.h"
 
 using namespace tmv;
 
@@ -215,4 +216,89 @@ extern "C" int hostcheck_p1p1_to_cached(const uint8_t *enc, uint32_t n) {
     }
   }
   return pairs < 50 ? -1 : bad;
+}
+
+// ---------------------------------------------------------------------------
+// Half-size scalars (halfscalar.h): the lattice reduction and the short
+// verification equation, on the host with single-lane point arithmetic.
+
+// k (32 bytes LE, k < l) -> u (16 bytes, magnitude), v (16 bytes), *u_neg;
+// returns 1 when the reduction finished (fast path), 0 for the slow path.
+extern "C" int hostcheck_half_reduce(const uint8_t k32[32], uint8_t u16[16], uint8_t v16[16], int *u_neg) {
+  uint32_t k[8], u[4], v[4];
+  load_words(k, k32);
+  bool neg = false;
+  const bool ok = half::reduce(u, neg, v, k);
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      u16[4 * i + j] = (uint8_t)(u[i] >> (8 * j));
+      v16[4 * i + j] = (uint8_t)(v[i] >> (8 * j));
+    }
+  *u_neg = neg ? 1 : 0;
+  return ok ? 1 : 0;
+}
+
+// acc = sigma ([b]B + [|u|](-R)) + [v](-A) with single-lane arithmetic
+static void half_acc(ge_p3 &acc, const half::Scalars &sc, const ge_p3 &A, const ge_p3 &R) {
+  ge_p3 nA, nR, bB, uR, vA;
+  ge_p3_neg(nA, A);
+  ge_p3_neg(nR, R);
+  ge_scalarmult_base(bB, sc.b, g_table.data());
+  ge_scalarmult_var(uR, sc.u, nR);
+  ge_scalarmult_var(vA, sc.v, nA);
+  ge_cached c;
+  ge_p1p1 t;
+  ge_p3 x;
+  ge_p3_to_cached(c, uR);
+  ge_add(t, bB, c);
+  ge_p1p1_to_p3(x, t);
+  if (sc.u_neg) ge_p3_neg(x, x);
+  ge_p3_to_cached(c, vA);
+  ge_add(t, x, c);
+  ge_p1p1_to_p3(acc, t);
+}
+
+// ed25519 (sr = 0: 1 / 0) or sr25519 (sr = 1: 1 / 0 / -1 / -2) verification
+// through the half-size scalars; *n_slow counts entries on the slow path.
+extern "C" void hostcheck_verify_half(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
+                                      uint32_t n, int sr, int8_t *out, int *n_slow) {
+  if (g_table.empty()) {
+    g_table.resize(kBaseTableRows * kBaseTableCols);
+    build_base_table(g_table.data());
+  }
+  strobe_t prefix;
+  sr25519_context_prefix(prefix);
+  int slow = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t a[8], r[8], s[8], k[8];
+    load_words(a, pk + 32 * i);
+    load_words(r, sig + 64 * i);
+    load_words(s, sig + 64 * i + 32);
+    ge_p3 A, R, acc;
+    const uint8_t *m = msg + off[i];
+    const uint32_t mlen = off[i + 1] - off[i];
+    if (sr) {
+      uint32_t sd[8];
+      if (!ristretto_decode(A, a)) { out[i] = -1; continue; }
+      if (!sr25519_decode_s(sd, s)) { out[i] = -2; continue; }
+      if (!ristretto_decode(R, r)) { out[i] = 0; continue; }
+      sr25519_challenge(k, prefix, a, r, m, mlen);
+      half::Scalars sc;
+      half::scalars(sc, k, sd);
+      slow += sc.fast ? 0 : 1;
+      half_acc(acc, sc, A, R);
+      out[i] = (fe_is_zero(acc.X) || fe_is_zero(acc.Y)) ? 1 : 0;  // Ristretto identity
+    } else {
+      if (!sc_is_canonical(s) || !ge_decode_zip215(A, a) || !ge_decode_zip215(R, r)) { out[i] = 0; continue; }
+      uint32_t h[16];
+      sha512_pq_msg(h, r, a, m, mlen);
+      sc_reduce512(k, h);
+      half::Scalars sc;
+      half::scalars(sc, k, s);
+      slow += sc.fast ? 0 : 1;
+      half_acc(acc, sc, A, R);
+      out[i] = ge_p3_is_small_order_or_identity_times8(acc) ? 1 : 0;
+    }
+  }
+  *n_slow = slow;
 }

@@ -1,0 +1,84 @@
+"""Streamed mixed ed25519 + sr25519 host batches (tmverify_runtime.cpp
+mixed_check_streamed): the caller's pages DMA'd part by part, each part split
+by key kind on the device into the two kinds' work-slot lists at bases the
+host counted, each kind's pipeline running the groups the parts complete,
+one tail per kind.  The statuses must equal the C oracle's and the
+unstreamed path's (TMV_MIXED_STREAM=0) for every layout of kinds over the
+parts: runs of one kind longer than a part (a kind absent from whole parts,
+groups spanning parts), alternating kinds, unknown kinds (status 0) and a
+kind absent altogether (crypto/batch/batch.go:11-21 mixed batches)."""
+import numpy as np
+import pytest
+
+import oracle_c as C
+from tendermint_amd import _native as N
+from tendermint_amd.testing.factory import make_mixed_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def base():
+    kind, mb = make_mixed_batch(20_000, seed=0x5EED)
+    ed, sr = np.flatnonzero(kind == 0), np.flatnonzero(kind == 1)
+    want = np.zeros(mb.n, np.int8)
+    be, bs = mb.take(ed), mb.take(sr)
+    want[ed] = C.ed25519_verify_packed(be.pk, be.sig, be.msg, be.off, threads=16)[1]
+    want[sr] = C.sr25519_status_packed(bs.pk, bs.sig, bs.msg, bs.off, threads=16)
+    return kind, mb, want
+
+
+def _layout(kind, name, n):
+    """Entry order over the base (indices) for a named layout."""
+    ed, sr = np.flatnonzero(kind == 0), np.flatnonzero(kind == 1)
+    if name == "interleaved":
+        return np.arange(n) % len(kind)
+    if name == "runs":  # 150k ed25519, then 150k sr25519, then interleaved (runs longer than a part)
+        a = ed[np.arange(150_000) % len(ed)]
+        b = sr[np.arange(150_000) % len(sr)]
+        c = np.arange(n - 300_000) % len(kind)
+        return np.concatenate([a, b, c])
+    if name == "ed_only":
+        return ed[np.arange(n) % len(ed)]
+    if name == "sr_only":
+        return sr[np.arange(n) % len(sr)]
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("layout", ["interleaved", "runs", "ed_only", "sr_only"])
+def test_mixed_streamed_vs_oracle(ctx, base, layout, monkeypatch):
+    kind, mb, want1 = base
+    n = 420_000
+    idx = _layout(kind, layout, n)
+    hb = mb.take(idx)
+    kinds = np.ascontiguousarray(kind[idx]).astype(np.uint8)
+    want = want1[idx].copy()
+    if layout == "interleaved":  # unknown key kinds: status 0, never verified
+        kinds[::997] = 7
+        want[::997] = 0
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("TMV_MIXED_STREAM", mode)
+        _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
+        got[mode] = np.asarray(st, np.int8)
+        bad = np.flatnonzero(got[mode] != want)
+        assert not len(bad), f"{layout}, TMV_MIXED_STREAM={mode}: entries {bad[:8]}: {got[mode][bad[:8]]} vs {want[bad[:8]]}"
+    assert np.array_equal(got["1"], got["0"])
+
+
+def test_mixed_streamed_stats(ctx, base, monkeypatch):
+    """The batch statistics see both kinds' groups on the streamed path (the
+    partition's device counts), as on the unstreamed one."""
+    kind, mb, _ = base
+    idx = np.arange(300_000) % mb.n
+    hb = mb.take(idx)
+    kinds = np.ascontiguousarray(kind[idx])
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("TMV_MIXED_STREAM", mode)
+        ctx.set_batch_options(stats=True)
+        g0 = ctx.batch_stats()["groups"]
+        ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
+        out[mode] = ctx.batch_stats()["groups"] - g0
+        ctx.set_batch_options()
+    assert out["1"] == out["0"] and out["1"] >= 300_000 // 64

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--distinct", type=int, default=16, help="distinct C2 batches, tiled")
     ap.add_argument("--method", default="batch", choices=["batch", "per-entry", "auto"])
     ap.add_argument("--group-log2", type=int, default=0, help="batch-equation group size 2^k (0: the library's choice)")
+    ap.add_argument("--stats", action="store_true", help="also count the launch's groups / failing groups / fallback "
+                                                         "entries (one extra host-buffer call)")
     ap.add_argument("--kind", default="ed25519", choices=["ed25519", "mixed", "mixed-ed", "mixed-sr"],
                     help="mixed-ed / mixed-sr: one kind's entries of the C5 base alone (pure-kind launch)")
     a = ap.parse_args()
@@ -81,6 +83,19 @@ def main():
         if a.kind == "ed25519":
             want = np.array([k in C2_VALID_KINDS for k in hb.kinds], np.int8)
             line["exact"] = bool(np.array_equal(out.cpu().numpy(), want))
+        if a.stats and kk == N.TMV_KIND_ED25519 and a.method == "batch":
+            # the same batch once through the host C-ABI with group verdicts
+            # counted (the device-pointer calls keep no statistics): groups,
+            # failing groups, entries verified one by one
+            ctx.set_batch_options(group_log2=a.group_log2, stats=True)
+            g0, m0 = ctx.batch_stats(), ctx.metrics()
+            ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, hb.pk, hb.sig, hb.msg, hb.off)
+            g1, m1 = ctx.batch_stats(), ctx.metrics()
+            ctx.set_batch_options(group_log2=a.group_log2)
+            line["groups"] = g1["groups"] - g0["groups"]
+            line["groups_failed"] = g1["failed"] - g0["failed"]
+            line["fallback_signatures"] = m1["fallback_signatures"] - m0["fallback_signatures"]
+            line["located_groups"] = m1["located_groups"] - m0["located_groups"]
         print(json.dumps(line), flush=True)
         del d, out
     ctx.close()
