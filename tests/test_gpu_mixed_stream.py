@@ -81,4 +81,4 @@ def test_mixed_streamed_stats(ctx, base, monkeypatch):
         ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
         out[mode] = ctx.batch_stats()["groups"] - g0
         ctx.set_batch_options()
-    assert out["1"] == out["0"] and out["1"] >= 300_000 // 64
+    assert out["1"] == out["0"] and out["1"] >= 300_000 // 128  # ed25519 groups of 128 (>= 150k), sr25519 of 64
