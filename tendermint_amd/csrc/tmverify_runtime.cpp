@@ -548,6 +548,7 @@ struct LaunchOpts {
   bool batch_eq = false;
   tmv::MsmParams p{};      // single-kind launches; the sr25519 half of a mixed one
   tmv::MsmParams p_ed{};   // the ed25519 half of a mixed launch
+  tmv::MsmParams p_ed_streamed{};  // ... of a streamed one (mixed_check_streamed)
   tmv::MsmSeed seed[2]{};  // [kind]
 };
 
@@ -618,6 +619,14 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
     // the located-fallback groups of 128 at the size ed25519-only launches
     // do, sr25519 keeps 64 (msm_params); both stay the caller's when set
     o.p_ed = merged || ed_only ? o.p : msm_params(n, ctx->msm_m_log2, ctx->msm_c, false, true, ctx->msm_sub);
+    // streamed, the ed25519 half keeps groups of 64 too: a part's window
+    // parts are latency-bound (~1k groups per part and kind), and c = 6's
+    // 2H = 64-addition running sums (groups of 128) cost more than the
+    // located fallback saves -- C5 1M mixed end to end 11.6 -> 11.2 ms
+    // (profiles/r05/mixed_stream/)
+    o.p_ed_streamed = merged || ed_only ? o.p
+                                        : msm_params(n, ctx->msm_m_log2 ? ctx->msm_m_log2 : 6, ctx->msm_c, false, true,
+                                                     ctx->msm_sub);
     fixed = ctx->fixed_seed;
     if (fixed) std::memcpy(key, ctx->seed, 32);
   }
@@ -1116,10 +1125,12 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
 // s, the sr25519 one on s2 -- then one tail per kind (Horner, fallback).  The
 // same kernels and the same validity vector as the unstreamed mixed launch;
 // only the part schedule differs.
-static int mixed_check_streamed(Device &d, const LaunchOpts &o, const uint8_t *kind_h, const uint8_t *kind_d,
+static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t *kind_h, const uint8_t *kind_d,
                                 const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
                                 uint32_t n, uint8_t *out, hipStream_t s, hipStream_t s2, hipEvent_t join,
                                 std::vector<hipEvent_t> &split_ev, const PartFeeder &feed) {
+  LaunchOpts o = o_in;
+  o.p_ed = o_in.p_ed_streamed;
   int rc;
   Workspace *ws = reserve_work(d, n, true, s, &rc, &o.p_ed, &o.p);
   if (!ws) return rc;

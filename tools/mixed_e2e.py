@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--group-log2", type=int, default=0, help="batch-equation group size 2^k (0: the library's)")
+    ap.add_argument("--window-bits", type=int, default=0, help="window bits c (0: the library's)")
     a = ap.parse_args()
     from tendermint_amd.testing.factory import make_mixed_batch
     import oracle_c as C  # checker only
@@ -43,6 +45,8 @@ def main():
     from tendermint_amd import _native as N
     dev = torch.device("cuda", 0)
     ctx = N.Context(1)
+    if a.group_log2 or a.window_bits:
+        ctx.set_batch_options(group_log2=a.group_log2, window_bits=a.window_bits)
     flags = N.TMV_FLAG_BATCH_EQUATION
     e2e = []
     for r in range(a.reps + 2):
@@ -72,6 +76,7 @@ def main():
             ker.append(e0.elapsed_time(e1))
     em, km = statistics.median(e2e), statistics.median(ker)
     print(json.dumps({"n": a.n, "env": {k: v for k, v in os.environ.items() if k.startswith("TMV_")},
+                      "group_log2": a.group_log2, "window_bits": a.window_bits,
                       "end_to_end_ms": round(em, 3), "end_to_end_verifies_per_s": round(a.n / em * 1e3, 1),
                       "kernel_only_ms": round(km, 3), "kernel_only_verifies_per_s": round(a.n / km * 1e3, 1),
                       "e2e_reps_ms": [round(x, 3) for x in e2e], "exact_vs_oracle": True}), flush=True)
