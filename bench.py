@@ -79,7 +79,7 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-PMC_DIRS = ("r04", "r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
+PMC_DIRS = ("r05", "r04", "r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
 
 
 def _load_pmc(method: str, batches_per_step: int = 32):
@@ -188,12 +188,13 @@ def kernel_products(n, m, c, fallback_entries=0, groups_failed=0, located=False,
         "k_prep_fused": n * (2 * DECODE_PRODUCTS + BARRETT_PRODUCTS),
         "k_msm_accum": (n + Gl * m) * e * 7 * FE_MUL,
         "k_msm_wpart": (G + Gl) * W * (H * WPART_BUCKET + FE_MUL),
-        "k_msm_horner": (G + Gl) * (((W - 1) * c + 3) * QDBL + (W - 1) * QADD),
+        "k_msm_horner": G * (((W - 1) * c + 3) * QDBL + (W - 1) * QADD),
+        "k_msm_horner_loc": Gl * (((W - 1) * c + 3) * QDBL + (W - 1) * QADD),  # the located pass's own Horner
         "fallback": fallback_entries * per_entry,
     }
 
 
-def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: int = 150_000):
+def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: int = 400_000):
     """The runtime's batch-equation shape for an uncached ed25519 launch of
     n_launch entries (tmverify_runtime.cpp msm_params): groups of 128 from
     the located-fallback size up, else 64; the window from the same cost
@@ -493,7 +494,7 @@ def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method, n_launch=0, ms_pe
     return out
 
 
-DOMINANT_FILE = os.path.join("profiles", "r04", "dominant_kernel.json")
+DOMINANT_FILE = os.path.join("profiles", "r05", "dominant_kernel.json")
 
 
 def _dominant_file():
@@ -536,7 +537,7 @@ def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, 
     shares the chip -- against the measured v_mad_i64_i32 peak.  The
     committed rocprofv3 --kernel-trace --stats of bench.py --inflight 1 (one
     launch at a time) gives the same kernel's average dispatch
-    (profiles/r04/dominant_kernel.json); traffic = its HBM bytes per launch
+    (profiles/r05/dominant_kernel.json); traffic = its HBM bytes per launch
     from PMC passes at this launch size (256 x 10k)."""
     m_grp, c_win = msm_shape(K * n, args.group_log2, args.window)
     per_launch = K * n * accum_entries_per_sig(m=m_grp, c=c_win) * ACCUM_PRODUCTS_PER_ENTRY

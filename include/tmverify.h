@@ -144,7 +144,7 @@ int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const ui
  * costs one small device read per call); TMV_BATCHOPT_SUBCHECK_ON / _OFF =
  * re-check failing groups by sub-groups of 8 before the per-entry fallback
  * (default: for groups of >= 256, $TMV_SUBCHECK overrides); with it off,
- * launches of >= $TMV_LOCATE_MIN (150000) entries locate a failing group's
+ * launches of >= $TMV_LOCATE_MIN (400000) entries locate a failing group's
  * one bad entry by a second, index-weighted equation. */
 #define TMV_BATCHOPT_STATS 1u
 #define TMV_BATCHOPT_SUBCHECK_ON 2u

@@ -1466,13 +1466,14 @@ static bool fallback_compact() {
 // fall back to all of them.  Less work (the second MSM costs about one
 // group's share of the pipeline, the per-entry fallback ~64 verifications),
 // a longer chain (a second Horner), so it pays where throughput, not the
-// launch's latency, sets the rate.
+// launch's latency, sets the rate.  C2 launches alone (profiles/r05/
+// ab_locate_min.txt), located vs not: 250k 2.99 vs 2.65-2.70 ms, 500k 4.80 vs
+// 4.73-4.81, 1M 8.67-8.92 vs 9.40 -- with the half-size scalars the
+// per-entry fallback got cheaper, so the crossover moved up from 150k.
+// (Read at every launch: tests cover the located path below the default.)
 static uint32_t locate_min() {
-  static const uint32_t v = [] {
-    const char *e = getenv("TMV_LOCATE_MIN");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 150000u;
-  }();
-  return v;
+  const char *e = getenv("TMV_LOCATE_MIN");
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : 400000u;
 }
 
 uint32_t locate_min_entries() { return locate_min(); }

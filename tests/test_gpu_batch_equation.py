@@ -257,12 +257,14 @@ def test_multi_batch_launch(bctx, flags):
 
 
 @pytest.mark.parametrize("kind,m_log2", [(ED, 0), (ED, 6), (SR, 0)], ids=["ed-default", "ed-64", "sr-default"])
-def test_located_fallback_placements(bctx, kind, m_log2):
-    """Launches of >= 150k entries (TMV_LOCATE_MIN) re-check a failing group
+def test_located_fallback_placements(bctx, kind, m_log2, monkeypatch):
+    """Launches of >= TMV_LOCATE_MIN entries (400k by default; 150k here, read
+    at every launch) re-check a failing group
     with index weights (j + 1) z_j and verify only the entry that locates;
     groups with two or more bad entries fall back to every entry.  One bad
     entry at each group edge (j = 0, 31, 63), pairs, a whole bad group and a
     ragged tail: the vector equals the oracle's."""
+    monkeypatch.setenv("TMV_LOCATE_MIN", "150000")
     n = 150_000 + 37
     base = make_commit_batch(1500, seed=21) if kind == ED else make_sr25519_batch(1500, seed=22, bad_frac=0.0)
     b = base.tile(n)
@@ -360,13 +362,14 @@ def _located_case(n=150_000 + 91, m=256):
 
 
 @pytest.mark.parametrize("m_log2,c", [(8, 8), (8, 6), (10, 9), (7, 6)])
-def test_located_pass_width_and_metrics(bctx, m_log2, c):
+def test_located_pass_width_and_metrics(bctx, m_log2, c, monkeypatch):
     """the located pass's weights z (j + 1) < 2^(128 + m_log2) need
     ceil((129 + m_log2) / c) windows.  With groups of 256 / 1024 (sub-group
     checks off) the located pass must still name every single bad entry:
     tmv_metrics counts one located group and one per-entry verification per
     single-bad group, and whole groups only for the two-bad ones; the vector
     equals the oracle's."""
+    monkeypatch.setenv("TMV_LOCATE_MIN", "150000")  # the launch (150k + 91) runs the located pass
     m = 1 << m_log2
     b, sig, singles, pairs = _located_case(m=m)
     n = b.n
@@ -443,7 +446,7 @@ def test_located_then_subgroups_option():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, TMV_LOC_SUBCHECK="1")
+    env = dict(os.environ, TMV_LOC_SUBCHECK="1", TMV_LOCATE_MIN="150000")
     out = subprocess.run([sys.executable, "-c", LOC_SUB], cwd=root, env=env, capture_output=True, text=True,
                          timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]

@@ -4,7 +4,7 @@ k_verify_quad / k_verify_quad_list): [8]([b]B + [u](-R) + [v](-A)) == O with
 validity bit for every input.  Every path that runs the per-entry kernels --
 the per-entry pipeline with LDS tables (<= 12,288 entries) and with global
 tables, the batch equation's compacted fallback of failing groups, the
-located fallback's entry list (launches >= 150k entries) -- is compared with
+located fallback's entry list (launches >= TMV_LOCATE_MIN entries) -- is compared with
 the C oracle in three modes: TMV_HALF_SCALARS=1 (the default), 0 (the full
 253-bit k, the rounds 1-4 check) and 2 (every third entry on the full-k path
 beside half-size quads of the same wave)."""
@@ -88,6 +88,7 @@ def test_located_fallback_list(ctx, mode, monkeypatch):
     """A 160k-entry C2-shaped launch runs the located fallback: its entry
     list goes through k_verify_quad_list (global tables, grid-stride)."""
     monkeypatch.setenv("TMV_HALF_SCALARS", mode)
+    monkeypatch.setenv("TMV_LOCATE_MIN", "150000")  # 160k entries: the located pass
     base = [make_c2_batch(10_000, seed=0xC0 + j) for j in range(4)]
     want1 = [C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=16)[1] for b in base]
     b = Batch.concat([base[j % 4] for j in range(16)])

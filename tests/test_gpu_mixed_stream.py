@@ -56,21 +56,24 @@ def test_mixed_streamed_vs_oracle(ctx, base, layout, monkeypatch):
     if layout == "interleaved":  # unknown key kinds: status 0, never verified
         kinds[::997] = 7
         want[::997] = 0
-    got = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("TMV_MIXED_STREAM", mode)
-        _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
-        got[mode] = np.asarray(st, np.int8)
-        bad = np.flatnonzero(got[mode] != want)
-        assert not len(bad), f"{layout}, TMV_MIXED_STREAM={mode}: entries {bad[:8]}: {got[mode][bad[:8]]} vs {want[bad[:8]]}"
-    assert np.array_equal(got["1"], got["0"])
+    for lmin in ("150000", "400000"):  # each kind's half with and without the located fallback
+        monkeypatch.setenv("TMV_LOCATE_MIN", lmin)
+        for mode in ("1", "0"):
+            monkeypatch.setenv("TMV_MIXED_STREAM", mode)
+            _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
+            got = np.asarray(st, np.int8)
+            bad = np.flatnonzero(got != want)
+            assert not len(bad), (f"{layout}, TMV_MIXED_STREAM={mode} TMV_LOCATE_MIN={lmin}: entries {bad[:8]}: "
+                                  f"{got[bad[:8]]} vs {want[bad[:8]]}")
 
 
 def test_mixed_streamed_stats(ctx, base, monkeypatch):
     """The batch statistics see both kinds' groups on the streamed path (the
     partition's device counts), as on the unstreamed one: ed25519 in groups
     of 64 streamed (tmverify_runtime.cpp make_opts: p_ed_streamed), of 128
-    unstreamed (>= 150k entries), sr25519 in groups of 64."""
+    unstreamed (>= TMV_LOCATE_MIN entries, 150k here), sr25519 in groups of
+    64."""
+    monkeypatch.setenv("TMV_LOCATE_MIN", "150000")
     kind, mb, _ = base
     idx = np.arange(300_000) % mb.n
     hb = mb.take(idx)

@@ -32,9 +32,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import bench  # noqa: E402  (the product model and peak)
 
-PRODUCT_KEY = {  # trace name prefix -> bench.kernel_products key
+PRODUCT_KEY = {  # trace name prefix -> bench.kernel_products key (first match; the located Horner first)
     "k_prep_fused": "k_prep_fused", "k_msm_accum": "k_msm_accum", "k_msm_wpart": "k_msm_wpart",
-    "k_msm_horner": "k_msm_horner", "k_verify_quad": "fallback", "k_verify_quad_list": "fallback",
+    "k_msm_horner<false, false, true>": "k_msm_horner_loc", "k_msm_horner": "k_msm_horner",
+    "k_verify_quad": "fallback", "k_verify_quad_list": "fallback",
 }
 
 
@@ -70,6 +71,8 @@ def main():
     ap.add_argument("--pmc", default="")
     ap.add_argument("--isa", default=os.path.join(REPO, "profiles", "r05", "isa_mix.json"))
     ap.add_argument("--skip", type=int, default=3)
+    ap.add_argument("--locate-min", type=int, default=400_000,
+                    help="the profiled build's TMV_LOCATE_MIN (groups of 128 and the located pass from it)")
     a = ap.parse_args()
     peak = bench._load_peak()
     rows = sorted((r for r in csv.DictReader(open(a.trace)) if r["Kind"] == "KERNEL_DISPATCH"),
@@ -90,8 +93,8 @@ def main():
         Ls = tl.get(grid_of(n), [])[a.skip:]
         if not Ls:
             continue
-        m, c = bench.msm_shape(n)
-        located = n >= 150_000
+        m, c = bench.msm_shape(n, locate_min=a.locate_min)
+        located = n >= a.locate_min
         prods = bench.kernel_products(n, m, c, sh.get("fallback_signatures", 0), sh.get("groups_failed", 0), located)
         names = sorted({k for L in Ls for k in L if not k.startswith("_")})
         span = statistics.median((L["_span"][1] - L["_span"][0]) / 1e3 for L in Ls)
