@@ -206,7 +206,7 @@ def msm_shape(n_launch: int, group_log2: int = 0, window: int = 0, locate_min: i
     best, c = None, 5
     for cc in range(4, 10):
         w, wr, h = -(-254 // cc), -(-129 // cc), 1 << (cc - 1)
-        cost = m * (w + wr) + 2.2 * w * h
+        cost = m * (w + wr) + 3.0 * w * h  # tmverify_runtime.cpp kRunningSumWeight
         if best is None or cost < best:
             best, c = cost, cc
     return m, c

@@ -502,14 +502,18 @@ struct ge_precomp { fe ypx, ymx, xy2d; };      // affine Niels form, Z = 1
 TMV_HD void ge_p3_identity(ge_p3 &h) { fe_zero(h.X); fe_one(h.Y); fe_one(h.Z); fe_zero(h.T); }
 TMV_HD void ge_precomp_identity(ge_precomp &h) { fe_one(h.ypx); fe_one(h.ymx); fe_zero(h.xy2d); }
 
-TMV_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
+TMV_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {  // (Z Y: Z's x2 form shared with Z T)
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
 }
+// (X T, Z Y, Z T, X Y: the right operands -- T, Y -- and the left ones -- X,
+// Z -- each serve two products, so their x19 and odd-limb x2 forms are built
+// once per conversion: 25 fewer VALU instructions than (X T, Y Z, Z T, X Y),
+// the same limbs -- a product's columns do not depend on operand order)
 TMV_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
 }

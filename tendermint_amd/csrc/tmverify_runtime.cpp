@@ -485,6 +485,17 @@ int faulted_rc(Device &d) {
 // The key-merged form (merged = true; keyed batches are commit traffic,
 // nearly always valid) defaults to groups of 256: its MSM has only the R
 // points and its fallback is the cheaper key-cached comb.
+// Cost of a bucket's running sum relative to a bucket entry's addition in the
+// window choice below.  2.2 from the kernels' per-item times picked c = 6 for
+// groups of 128; c = 5 measured faster (2.56M launch alone 20.95 -> 19.94 ms,
+// profiles/r05/ab_window.txt): fuller buckets (16 entries, one chunk) split
+// and join less, and the 2H-addition running-sum chain halves.  3.0 keeps
+// c = 5 for groups of 64 and 128.
+constexpr double kRunningSumWeight = 3.0;
+static double running_sum_weight() {  // TMV_RS_WEIGHT: A/B of the weight (read per launch)
+  const char *e = getenv("TMV_RS_WEIGHT");
+  return e ? atof(e) : kRunningSumWeight;
+}
 tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false, bool ed_only = false,
                           int sub = -1) {
   // uncached ed25519 launches large enough for the located fallback
@@ -498,11 +509,11 @@ tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged =
   if (m_log2 == 0) m_log2 = merged ? 8 : (ed_only && lmin && n >= lmin ? 7 : 6);
   m_log2 = std::max<uint32_t>(5, std::min<uint32_t>(10, m_log2));
   if (c == 0) {
-    const double m = double(1u << m_log2);
+    const double m = double(1u << m_log2), rsw = running_sum_weight();
     double best = 1e30;
     for (uint32_t cc = 4; cc <= 9; cc++) {
       const double W = (254 + cc - 1) / cc, WR = (129 + cc - 1) / cc, H = double(1u << (cc - 1));
-      const double cost = merged ? m * WR + 2.2 * WR * H : m * (W + WR) + 2.2 * W * H;
+      const double cost = merged ? m * WR + 2.2 * WR * H : m * (W + WR) + rsw * W * H;
       if (cost < best) { best = cost; c = cc; }
     }
   }

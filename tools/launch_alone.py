@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--distinct", type=int, default=16, help="distinct C2 batches, tiled")
     ap.add_argument("--method", default="batch", choices=["batch", "per-entry", "auto"])
     ap.add_argument("--group-log2", type=int, default=0, help="batch-equation group size 2^k (0: the library's choice)")
+    ap.add_argument("--window-bits", type=int, default=0, help="batch-equation window bits c (0: the library's choice)")
     ap.add_argument("--stats", action="store_true", help="also count the launch's groups / failing groups / fallback "
                                                          "entries (one extra host-buffer call)")
     ap.add_argument("--kind", default="ed25519", choices=["ed25519", "mixed", "mixed-ed", "mixed-sr"],
@@ -54,8 +55,8 @@ def main():
     from tendermint_amd import _native as N
     dev = torch.device("cuda", 0)
     ctx = N.Context(1)
-    if a.group_log2:
-        ctx.set_batch_options(group_log2=a.group_log2)
+    if a.group_log2 or a.window_bits:
+        ctx.set_batch_options(group_log2=a.group_log2, window_bits=a.window_bits)
     flags = {"batch": N.TMV_FLAG_BATCH_EQUATION, "per-entry": N.TMV_FLAG_PER_ENTRY, "auto": 0}[a.method]
     st = torch.cuda.Stream(dev)
     for n in sizes:
@@ -87,11 +88,11 @@ def main():
             # the same batch once through the host C-ABI with group verdicts
             # counted (the device-pointer calls keep no statistics): groups,
             # failing groups, entries verified one by one
-            ctx.set_batch_options(group_log2=a.group_log2, stats=True)
+            ctx.set_batch_options(group_log2=a.group_log2, window_bits=a.window_bits, stats=True)
             g0, m0 = ctx.batch_stats(), ctx.metrics()
             ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, hb.pk, hb.sig, hb.msg, hb.off)
             g1, m1 = ctx.batch_stats(), ctx.metrics()
-            ctx.set_batch_options(group_log2=a.group_log2)
+            ctx.set_batch_options(group_log2=a.group_log2, window_bits=a.window_bits)
             line["groups"] = g1["groups"] - g0["groups"]
             line["groups_failed"] = g1["failed"] - g0["failed"]
             line["fallback_signatures"] = m1["fallback_signatures"] - m0["fallback_signatures"]
