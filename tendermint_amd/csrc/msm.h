@@ -207,6 +207,11 @@ struct MsmWork {
   // their 8-entry sub-groups are checked (k_msm_subcheck) before the fallback
   uint32_t *l2_list;     // groups
   uint32_t *l2_count;
+  // bisection of those groups (k_msm_sort<.., 2> .. k_loc_search2): slot 2t /
+  // 2t+1 hold the sums of the first half of the t-th listed group with
+  // weights z / (j+1) z; its entry count (slots << m_log2) in l2e_count
+  fe *l2_T;              // groups x 4 fe (P3Q lanes)
+  uint32_t *l2e_count;
   // key-merged form only (null otherwise)
   uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
   uint32_t *bscal;     // groups x 8 words: B scalar of the group
@@ -223,7 +228,7 @@ struct MsmWork {
                17 * 16;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
     else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
-              G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16 + 4 * G + 2 * 16;
+              G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16 + 4 * G + 2 * 16 + G * 4 * sizeof(fe) + 16;
     return b;
   }
   static MsmWork carve(void *base, uint32_t n, const MsmParams &p) {
@@ -254,7 +259,8 @@ struct MsmWork {
     w.tabR = nullptr;
     w.fail_T = nullptr;
     w.loc_count = w.fb_count = w.fb_list = w.loc_found = nullptr;
-    w.l2_list = w.l2_count = nullptr;
+    w.l2_list = w.l2_count = w.l2e_count = nullptr;
+    w.l2_T = nullptr;
     if (!p.merged) {
       w.fail_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
       w.fail_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
@@ -263,10 +269,12 @@ struct MsmWork {
       w.fail_T = reinterpret_cast<fe *>(b + o); o = up(o + G * 8 * sizeof(fe));
       w.loc_count = reinterpret_cast<uint32_t *>(b + o);
       w.fb_count = w.loc_count + 1;
-      w.loc_found = w.loc_count + 2; o = up(o + 16);
+      w.loc_found = w.loc_count + 2;
+      w.l2e_count = w.loc_count + 3; o = up(o + 16);
       w.fb_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4ull * n);
       w.l2_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
       w.l2_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
+      w.l2_T = reinterpret_cast<fe *>(b + o); o = up(o + G * 4 * sizeof(fe));
     }
     if (p.merged) {
       w.wscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32ull * n);

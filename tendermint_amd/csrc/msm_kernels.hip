@@ -255,8 +255,9 @@ __device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &o
 // group into slot f with every weight multiplied by (j + 1), j the entry's
 // index in its group, so the same bucket stages compute
 // T'_f = sum (j+1) z_j Delta_j (z_j (j+1) < 2^(128 + m_log2): p.WL() R
-// windows).
-template <bool SR, bool KM, int BS = kMsmSortBlock, bool LOC = false>
+// windows).  LOC = 2 (bisection, k_loc_search2): slot s holds the first half
+// of group fail_list[l2_list[s / 2]], weights z (even s) or (j + 1) z (odd).
+template <bool SR, bool KM, int BS = kMsmSortBlock, int LOC = 0>
 __global__ void __launch_bounds__(BS)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
            Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned,
@@ -266,7 +267,12 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   const uint32_t cnt = entry_count(count_ptr, n);
   const uint32_t tid = threadIdx.x;
   uint32_t g = blockIdx.x;  // LOC: the slot; the group is fail_list[slot]
-  if (LOC) {
+  if (LOC == 2) {
+    const uint32_t ns = min(2u * *mw.l2_count, p.groups);
+    if (g == 0 && tid == 0) *mw.l2e_count = ns << p.m_log2;  // the bucket stages' entry count
+    if (g >= ns) return;  // block-uniform
+  }
+  if (LOC == 1) {
     const uint32_t nf = *mw.fail_count;
     if (g == 0 && tid == 0) {
       *mw.loc_count = nf << p.m_log2;  // the bucket stages' entry count: nf slots
@@ -277,7 +283,8 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     if (g >= nf) return;  // block-uniform
   }
   const uint32_t slot = g;
-  if (LOC) g = mw.fail_list[slot];
+  if (LOC == 1) g = mw.fail_list[slot];
+  if (LOC == 2) g = mw.fail_list[mw.l2_list[slot >> 1]];
   const uint32_t e0 = g << p.m_log2;
   if (!KM && !LOC && g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
     niels_pt bp;
@@ -289,7 +296,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     if (mw.fail_count) *mw.fail_count = 0;  // k_msm_horner appends the failing groups
   }
   if (e0 >= cnt) return;  // block-uniform
-  const uint32_t mlive = min(p.m(), cnt - e0);
+  const uint32_t mlive = min(LOC == 2 ? p.m() >> 1 : p.m(), cnt - e0);
   const uint32_t WH = p.W * p.H;
   uint32_t *hist = smem;                       // WH counters, then cursors
   uint32_t *red = smem + WH;                   // BS x 9 words
@@ -354,7 +361,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
     sc_mul_mod(wv[r], z[r], 4, k);
     if (LOC) {  // weights times (j + 1): z (j + 1) exactly, z k (j + 1) mod l
-      const uint32_t jj = j + 1;
+      const uint32_t jj = (LOC == 2 && !(slot & 1)) ? 1u : j + 1;
       uint64_t cy = 0;
 #pragma unroll
       for (int t = 0; t < 4; t++) {
@@ -1016,8 +1023,9 @@ static uint32_t wpart_quad_rows() {
 //   ed25519: [8] T_g == O;  sr25519: T_g is the Ristretto identity.
 // A failing group's T_g goes to mw.fail_T at its place in the failing list.
 // LOC: the same Horner over the locate MSM's slots (count_ptr = loc_count),
-// T'_f to mw.fail_T, no verdict.
-template <bool SR, bool KM, bool LOC = false>
+// T'_f to mw.fail_T, no verdict; LOC = 2: the bisection slots' sums to
+// mw.l2_T (count_ptr = l2e_count).
+template <bool SR, bool KM, int LOC = 0>
 __global__ void __launch_bounds__(64)
 k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, const uint32_t *__restrict__ group_run0,
              uint32_t n_runs) {
@@ -1052,7 +1060,10 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
     }
   }
   if (LOC) {
-    if (live) mw.fail_T[8ull * g + 4 + c] = acc;
+    if (live) {
+      if (LOC == 2) mw.l2_T[4ull * g + c] = acc;
+      else mw.fail_T[8ull * g + 4 + c] = acc;
+    }
     return;
   }
   bool ok;
@@ -1136,20 +1147,129 @@ k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, int
   __syncthreads();
   const uint32_t e0 = mw.fail_list[f] << p.m_log2;
   const uint32_t mlive = min(m, entry_count(count_ptr, n) - e0);
-  if (s_cnt == 1 && (uint32_t)s_j < mlive && !mw.sort_ovf[p.groups + f]) {  // block-uniform
+  const bool ovf = mw.sort_ovf[p.groups + f];
+  if (s_cnt == 1 && (uint32_t)s_j < mlive && !ovf) {  // block-uniform
     if (threadIdx.x == 0) {
       mw.fb_list[atomicAdd(mw.fb_count, 1u)] = e0 + (uint32_t)s_j;
       atomicAdd(mw.loc_found, 1u);
     }
     return;
   }
-  if (sub2) {  // two or more bad entries: its sub-groups are checked next
+  if (sub2 == 1) {  // two or more bad entries: its sub-groups are checked next
     if (threadIdx.x == 0) mw.l2_list[atomicAdd(mw.l2_count, 1u)] = mw.fail_list[f];
+    return;
+  }
+  if (sub2 == 2 && !ovf) {  // two or more bad entries: bisected next (k_loc_search2)
+    if (threadIdx.x == 0) mw.l2_list[atomicAdd(mw.l2_count, 1u)] = f;
     return;
   }
   if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < mlive; t += 64) mw.fb_list[s_base + t] = e0 + t;
+}
+
+// Bisection of the groups k_loc_search could not name (two or more bad
+// entries; ~9% of C2's failing groups of 128, each of which cost 128
+// one-by-one verifications): one wave per listed group t.  The bisection
+// MSM gave the first half's sums T1 = sum_{j < m/2} z_j Delta_j (slot 2t)
+// and T1' = sum_{j < m/2} (j+1) z_j Delta_j (slot 2t + 1); the second half's
+// are T - T1 and T' - T1' (the group's own sums from k_msm_horner and the
+// located pass).  Per half: [8] T_h == O (sr25519: the Ristretto identity) --
+// no bad entry, every entry keeps its pre-check status; else the search of
+// k_loc_search on (T_h, T_h') names its one bad entry, or, with two or more,
+// every entry of the half is verified one by one.  Two bad entries in
+// different halves (about half of such groups) cost two verifications
+// instead of 128, in one half 64.
+template <bool SR>
+__global__ void __launch_bounds__(64)
+k_loc_search2(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  __shared__ int s_cnt, s_j;
+  __shared__ uint32_t s_base;
+  const uint32_t t = blockIdx.x;
+  const uint32_t nl2 = *mw.l2_count;
+  if (t >= nl2) return;  // block-uniform
+  const uint32_t f = mw.l2_list[t];
+  const uint32_t m = p.m(), half = m >> 1;
+  const uint32_t e0 = mw.fail_list[f] << p.m_log2;
+  const uint32_t mlive = min(m, entry_count(count_ptr, n) - e0);
+  const uint32_t ns = min(2u * nl2, p.groups);
+  const int c = (int)(threadIdx.x & 3), q = (int)(threadIdx.x >> 2);
+  // slots past the workspace's capacity (more listed groups than half the
+  // groups) or an overflowed sort: every entry of the group one by one
+  if (2 * t + 1 >= ns || mw.sort_ovf[p.groups + 2 * t] || mw.sort_ovf[p.groups + 2 * t + 1]) {  // block-uniform
+    if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
+    __syncthreads();
+    for (uint32_t u = threadIdx.x; u < mlive; u += 64) mw.fb_list[s_base + u] = e0 + u;
+    return;
+  }
+  const fe T = mw.fail_T[8ull * f + c], Tp = mw.fail_T[8ull * f + 4 + c];
+  const fe A = mw.l2_T[4ull * (2 * t) + c], Ap = mw.l2_T[4ull * (2 * t + 1) + c];
+  fe Bh, Bp, nc, r;
+  quad::to_cached(nc, A);  // second half: T - T1, T' - T1'
+  quad::cached_cneg(nc, true);
+  quad::add(r, T, nc);
+  quad::p1p1_to_p3(Bh, r);
+  quad::to_cached(nc, Ap);
+  quad::cached_cneg(nc, true);
+  quad::add(r, Tp, nc);
+  quad::p1p1_to_p3(Bp, r);
+  for (int h = 0; h < 2; h++) {
+    const uint32_t lo = (uint32_t)h * half, hi = min(lo + half, mlive);
+    if (lo >= hi) break;  // block-uniform (a short last group)
+    fe M = h ? Bh : A, Mp = h ? Bp : Ap;
+    const bool clean = SR ? quad::is_ristretto_identity(M) : quad::is_identity_times8(M);
+    if (clean) continue;  // block-uniform: every quad holds the same sums
+    if (!SR) {
+      for (int i = 0; i < 3; i++) {
+        quad::dbl(r, M);
+        quad::p1p1_to_p3(M, r);
+        quad::dbl(r, Mp);
+        quad::p1p1_to_p3(Mp, r);
+      }
+    }
+    if (threadIdx.x == 0) {
+      s_cnt = 0;
+      s_j = -1;
+    }
+    fe Mc, Dc, P = M, D = M;
+    quad::to_cached(Mc, M);
+    const int k = q + 1;  // <= 16; quad-uniform
+    for (int b = 30 - __builtin_clz((unsigned)k); b >= 0; b--) {
+      quad::dbl(r, P);
+      quad::p1p1_to_p3(P, r);
+      if ((k >> b) & 1) {
+        quad::add(r, P, Mc);
+        quad::p1p1_to_p3(P, r);
+      }
+    }
+    for (int i = 0; i < 4; i++) {
+      quad::dbl(r, D);
+      quad::p1p1_to_p3(D, r);
+    }
+    quad::to_cached(Dc, D);
+    __syncthreads();  // s_cnt / s_j initialised
+    for (uint32_t j = (uint32_t)q; j < m; j += 16) {
+      const bool eq = SR ? quad::ristretto_equal(P, Mp) : quad::p3_equal(P, Mp);
+      if (eq && c == 0) {
+        atomicAdd(&s_cnt, 1);
+        s_j = (int)j;
+      }
+      quad::add(r, P, Dc);
+      quad::p1p1_to_p3(P, r);
+    }
+    __syncthreads();
+    if (s_cnt == 1 && (uint32_t)s_j >= lo && (uint32_t)s_j < hi) {  // block-uniform
+      if (threadIdx.x == 0) {
+        mw.fb_list[atomicAdd(mw.fb_count, 1u)] = e0 + (uint32_t)s_j;
+        atomicAdd(mw.loc_found, 1u);
+      }
+    } else {
+      if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, hi - lo);
+      __syncthreads();
+      for (uint32_t u = threadIdx.x; u < hi - lo; u += 64) mw.fb_list[s_base + u] = e0 + lo + u;
+    }
+    __syncthreads();  // s_cnt / s_j / s_base reused by the next half
+  }
 }
 
 // After k_msm_subcheck over the groups the search could not name: the
@@ -1502,6 +1622,19 @@ static bool loc_subcheck() {
   return on;
 }
 
+// Bisection of the groups the located search cannot name (k_loc_search2)
+// for launches of at least this many entries (TMV_LOC_BISECT_MIN; default 0
+// = never).  Measured and not kept (profiles/r05/ab_loc_bisect.txt, one box):
+// it cuts the one-by-one entries of a 2.56M C2 launch from 46,416 to 13,040,
+// but its second MSM, Horner and search lengthen the chain -- launch alone
+// 19.42 -> 19.88 ms at 2.56M, 8.21 -> 8.87 ms at 1M -- and with 4 launches in
+// flight the bench does not gain either (135.9 / 136.6 off vs 135.4 / 136.1
+// M/s on).  (Read at every launch: the tests switch it on.)
+static uint32_t loc_bisect_min() {
+  const char *e = getenv("TMV_LOC_BISECT_MIN");
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+}
+
 bool locate_enabled(uint32_t n, const MsmParams &p) {
   const uint32_t lmin = locate_min();
   return fallback_compact() && lmin && n >= lmin && !p.sub && p.WL() <= p.W;
@@ -1620,13 +1753,33 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     MsmParams pl = p;  // running sums split over loc_parts() lanes per window (TMV_LOC_PARTS=1: one)
     pl.P = loc_parts_env() ? p.P : p.loc_parts();
     if ((e = launch_buckets(mw.loc_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
+    hipLaunchKernelGGL((k_msm_horner<SR, false, 1>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
                        mw.loc_count, n_slots, mw, pl, nullptr, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const int sub2 = loc_subcheck() ? 1 : 0;
+    const uint32_t bmin = loc_bisect_min();
+    const int sub2 = loc_subcheck() ? 1 : (bmin && n >= bmin ? 2 : 0);
     hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p, sub2);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (sub2) {  // groups the search could not name: sub-group checks, then their failing sub-groups' entries
+    if (sub2 == 2) {  // bisection MSM over the first halves of the unnamed groups, then its search
+      if (p.m_log2 <= 8 && sort_block() == 64) {
+        hipLaunchKernelGGL((k_msm_sort<SR, false, 64, 2>), dim3(p.groups), dim3(64), sort_smem(p, 64), stream, sig,
+                           idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
+      } else if (p.m_log2 <= 8 && sort_block() == 128) {
+        hipLaunchKernelGGL((k_msm_sort<SR, false, 128, 2>), dim3(p.groups), dim3(128), sort_smem(p, 128), stream,
+                           sig, idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
+      } else {
+        hipLaunchKernelGGL((k_msm_sort<SR, false, kMsmSortBlock, 2>), dim3(p.groups), dim3(kMsmSortBlock),
+                           sort_smem(p, kMsmSortBlock), stream, sig, idx, count_ptr, n, w, mw, p, seed, btab_q,
+                           aligned, nullptr, nullptr, nullptr, 0u);
+      }
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      if ((e = launch_buckets(mw.l2e_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
+      hipLaunchKernelGGL((k_msm_horner<SR, false, 2>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
+                         mw.l2e_count, n_slots, mw, pl, nullptr, 0u);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_loc_search2<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (sub2) {  // groups the search could not name: sub-group checks, then their failing sub-groups' entries
       const uint64_t subs = (uint64_t)p.groups << (p.m_log2 - kSubGroupLog2);
       hipLaunchKernelGGL(k_msm_subcheck<SR>, dim3((uint32_t)((subs + 15) / 16)), dim3(64), 0, stream, sig, idx,
                          count_ptr, n, w, mw, p, seed, btab_q, aligned, (const uint32_t *)mw.l2_list,

@@ -417,6 +417,85 @@ def test_metrics_counts_calls_and_resets(bctx):
     assert all(v == 0 for k, v in met.items() if k not in ("key_cache_hits", "key_cache_misses"))
 
 
+def _bisect_case(kind, m, n=150_000 + 91):
+    """Bad entries (S's low bit flipped: every pre-check passes) placed so
+    that failing groups of m hold one bad entry, two in the same half (either
+    half), two in different halves, three (two + one), and two in the ragged
+    last group."""
+    base = make_commit_batch(1500, seed=23) if kind == ED else make_sr25519_batch(1500, seed=24, bad_frac=0.0)
+    b = base.tile(n)
+    sig = b.sig.copy()
+    h = m // 2
+    bad = [0, m + m - 1, 5 * m + 17,                      # one bad entry
+           12 * m + 1, 12 * m + 9,                        # two, first half
+           14 * m + h + 3, 14 * m + m - 1,                # two, second half
+           30 * m + 3, 30 * m + h + 4,                    # one in each half
+           40 * m + 1, 40 * m + 2, 40 * m + m - 2,        # two + one
+           n - 1, n - 2]                                  # the ragged last group
+    for i in bad:
+        sig[64 * i + 32] ^= 0x01
+    return b, sig, bad
+
+
+def _bisect_expect(bad, n, m):
+    """(located, one-by-one) the bisection gives: a group with one bad entry
+    names it; with more, each half names its one bad entry, or is verified
+    whole when it holds two or more (a clean half costs nothing)."""
+    groups = {}
+    for i in bad:
+        groups.setdefault(i // m, []).append(i)
+    located = fallback = 0
+    for g, es in groups.items():
+        if len(es) == 1:
+            located += 1
+            fallback += 1
+            continue
+        lo_g, h = g * m, m // 2
+        for lo in (lo_g, lo_g + h):
+            hi = min(lo + h, n)
+            k = sum(lo <= i < hi for i in es)
+            if k == 1:
+                located += 1
+                fallback += 1
+            elif k >= 2:
+                fallback += hi - lo
+    return located, fallback
+
+
+@pytest.mark.parametrize("kind,m_log2", [(ED, 7), (ED, 8), (SR, 6)], ids=["ed-128", "ed-256", "sr-64"])
+def test_located_bisection(bctx, kind, m_log2, monkeypatch):
+    """TMV_LOC_BISECT_MIN (off by default: measured slower; 150k here, read at
+    every launch):
+    the groups the located search cannot name are bisected -- the first
+    half's sums T1, T1' by a second MSM, the second half's as differences --
+    and each half names its one bad entry or, with two or more, is verified
+    one by one.  tmv_metrics counts exactly the entries the rule implies, and
+    the vector equals the oracle's."""
+    monkeypatch.setenv("TMV_LOCATE_MIN", "150000")
+    monkeypatch.setenv("TMV_LOC_BISECT_MIN", "150000")
+    m = 1 << m_log2
+    b, sig, bad = _bisect_case(kind, m)
+    n = b.n
+    bctx.set_batch_options(group_log2=m_log2, seed=SEED, stats=True, subcheck=False)
+    bctx.metrics_reset()
+    try:
+        ok, st = bctx.verify_batch_ex(kind, BEQ, b.pk, sig, b.msg, b.off)
+        met = bctx.metrics()
+    finally:
+        bctx.set_batch_options(seed=SEED, stats=True)
+    if kind == ED:
+        ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
+        assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
+        assert int((ref == 0).sum()) == len(bad)
+    else:
+        ref = C.sr25519_status_packed(b.pk, sig, b.msg, b.off, threads=16)
+        assert np.array_equal(st, ref)
+        assert int((ref != 1).sum()) == len(bad)
+    located, fallback = _bisect_expect(bad, n, m)
+    assert met["groups_failed"] == len({i // m for i in bad})
+    assert (met["located_groups"], met["fallback_signatures"]) == (located, fallback), met
+
+
 LOC_SUB = r"""
 import sys, numpy as np
 sys.path.insert(0, '.'); sys.path.insert(0, 'oracle'); sys.path.insert(0, 'tests')
