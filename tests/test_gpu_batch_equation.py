@@ -417,6 +417,41 @@ def test_metrics_counts_calls_and_resets(bctx):
     assert all(v == 0 for k, v in met.items() if k not in ("key_cache_hits", "key_cache_misses"))
 
 
+@pytest.mark.parametrize("kind", [ED, SR], ids=["ed25519", "sr25519"])
+def test_duplicate_entries(bctx, kind):
+    """The same signature many times in one group (a replayed vote): each copy
+    gets its own random weight, but the points coincide, so one bucket adds a
+    point to itself (and to its negation, digits of opposite sign) -- the
+    complete addition law must hold there.  Groups of copies of a valid
+    signature pass the equation; a group holding a copy of an invalid one
+    fails, and every copy of it is invalid, as the oracle says."""
+    base = make_commit_batch(200, seed=31) if kind == ED else make_sr25519_batch(200, seed=32, bad_frac=0.0)
+    sig = base.sig.copy()
+    bad = 5
+    sig[64 * bad + 32] ^= 0x01  # S stays canonical: the entry fails the equation only
+    idx = ([0] * 64                                  # one valid signature 64 times
+           + [1 + (i // 2) for i in range(64)]       # 32 valid ones twice each
+           + [bad] * 64                              # one invalid signature 64 times
+           + [3] * 63 + [bad]                        # 63 copies of a valid one, one invalid
+           + list(range(40, 104))                    # 64 distinct
+           + [7, bad] * 16 + [8] * 7)                # alternating, then a ragged tail
+    ents = [(bytes(base.pk[32 * i:32 * i + 32]), bytes(base.msg[base.off[i]:base.off[i + 1]]),
+             bytes(sig[64 * i:64 * i + 64])) for i in idx]
+    b = _B(*C.pack(ents))
+    ok, st, groups, failed = _run(bctx, kind, b, group_log2=6)
+    if kind == ED:
+        ok_o, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+        assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
+    else:
+        ref = C.sr25519_status_packed(b.pk, b.sig, b.msg, b.off, threads=8)
+        assert np.array_equal(st, ref)
+    assert int((ref != 1).sum()) == idx.count(bad)
+    assert groups == (len(idx) + 63) // 64 == 6
+    # the groups holding a copy of the invalid signature (the pairs' group too:
+    # entry 5 is among them)
+    assert failed == len({j // 64 for j, i in enumerate(idx) if i == bad}) == 4
+
+
 def _bisect_case(kind, m, n=150_000 + 91):
     """Bad entries (S's low bit flipped: every pre-check passes) placed so
     that failing groups of m hold one bad entry, two in the same half (either
