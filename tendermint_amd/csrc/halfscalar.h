@@ -84,6 +84,27 @@ TMV_HD double floor_div(double n, double d) {
   return q;
 }
 
+// floor(n / d) for integers 0 <= n < 2^53, 0 < d < 2^53 held in doubles,
+// from a reciprocal (v_rcp_f64 on the device, no IEEE division sequence) and
+// a remainder correction; *ok = false when the result is not certified
+// exactly (the caller then ends its Lehmer round early -- always safe).
+// The division sequence was most of reduce()'s cost: 70.7 field multiplies
+// of chip time per reduction (tools/reduce_bench.hip), nearly all of it in
+// the two IEEE divisions of every Lehmer step.
+TMV_HD double floor_div_rcp(double n, double d, bool &ok) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double r = __builtin_amdgcn_rcp(d);
+#else
+  const double r = 1.0 / d;
+#endif
+  double q = floor(n * r);
+  double rem = fma(-q, d, n);
+  q = rem < 0 ? q - 1 : (rem >= d ? q + 1 : q);
+  rem = fma(-q, d, n);
+  ok = rem >= 0 && rem < d;
+  return q;
+}
+
 // x = a * y (a < 2^32): 9 words
 TMV_HD void mul_1(uint32_t x[9], uint32_t a, const uint32_t y[8]) {
   uint64_t c = 0;
@@ -155,9 +176,13 @@ TMV_HD bool reduce(uint32_t u_out[4], bool &u_neg, uint32_t v_out[4], const uint
     int steps = 0;
     for (int it = 0; it < 64; it++) {  // ~12 steps per round; bounded
       const double dc = vh + C, dd = vh + D;
-      if (dc == 0 || dd == 0) break;
-      const double q = floor_div(uh + A, dc);
-      if (q != floor_div(uh + B, dd)) break;  // Lehmer's test: the quotient is not certain
+      if (!(dc > 0 && dd > 0)) break;
+      bool exact;
+      const double q = floor_div_rcp(uh + A, dc, exact);
+      // Lehmer's test: the quotient must also be floor((uh + B) / dd), i.e.
+      // 0 <= (uh + B) - q dd < dd (one multiply-add, not a second division)
+      const double rem2 = fma(-q, dd, uh + B);
+      if (!exact || rem2 < 0 || rem2 >= dd) break;  // not certain
       const double nC = fma(-q, C, A), nD = fma(-q, D, B);
       if (fabs(nC) >= kMaxCof || fabs(nD) >= kMaxCof) break;
       A = C; B = D; C = nC; D = nD;
