@@ -266,6 +266,23 @@ struct Scalars {
   uint32_t u[8], v[8], b[8];
   bool u_neg, fast;
 };
+// The same from a reduction done elsewhere (u4, u_neg, v4, fast: reduce()'s outputs).
+TMV_HD void scalars_from(Scalars &o, const uint32_t u4[4], bool neg, const uint32_t v4[4], bool fast,
+                         const uint32_t k[8], const uint32_t s[8]) {
+  o.fast = fast;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    o.u[i] = o.fast ? (i < 4 ? u4[i] : 0u) : (i == 0 ? 1u : 0u);
+    o.v[i] = o.fast ? (i < 4 ? v4[i] : 0u) : k[i];
+  }
+  o.u_neg = o.fast && neg;
+  if (o.fast) sc_mul_mod(o.b, o.u, 4, s);
+  else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.b[i] = s[i];
+  }
+}
+
 TMV_HD void scalars(Scalars &o, const uint32_t k[8], const uint32_t s[8]) {
   uint32_t u4[4], v4[4];
   bool neg = false;

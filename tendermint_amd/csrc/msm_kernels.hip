@@ -1655,6 +1655,7 @@ static Ed25519Work work_view(Ed25519Work w, uint64_t e0) {
   w.k += 8 * e0;
   w.flags += 4 * e0;
   w.tabA += 64 * e0;  // k_verify_quad's stride (k_msm_subcheck, tail only, uses 32 of it)
+  w.hs_buf += 12 * e0;  // (w.hs stays null: the batch paths reduce in their fallback)
   return w;
 }
 static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0) {

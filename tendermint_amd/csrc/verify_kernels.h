@@ -20,7 +20,13 @@ struct Ed25519Work {
   uint8_t *flags;  // 4n bytes: decode ok for A (4e), R (4e+1)
   niels_pt *niels; // batch check only (else null): [2e] = -R_e, [2e+1] = -A_e
   fe *tabA;        // n x 16 x 4 fe: k_verify_quad's tables of -A (8 x 4 fe) and -R (8 x 4 fe) when kept in global memory
-  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4 + 2560) + 256; }
+  // per-entry pipeline only (launch_pipeline sets hs = hs_buf; null
+  // elsewhere): the prep's hash lane reduces k to the half-size scalars once
+  // per entry -- n x 12 words: |u| (4), v (4), fast | u_neg << 1, 3 spare --
+  // instead of every lane of the entry's quad repeating the reduction
+  uint32_t *hs;
+  uint32_t *hs_buf;
+  static size_t bytes(uint32_t n) { return (size_t)n * (160 + 160 + 32 + 4 + 2560 + 48) + 256; }
   // carve a workspace for n entries out of base (16-byte aligned pieces)
   static Ed25519Work carve(void *base, uint32_t n) {
     uint8_t *b = static_cast<uint8_t *>(base);
@@ -30,6 +36,8 @@ struct Ed25519Work {
     w.k = reinterpret_cast<uint32_t *>(b + 320ull * n);
     w.flags = b + 352ull * n;
     w.tabA = reinterpret_cast<fe *>(b + ((356ull * n + 15) & ~15ull));
+    w.hs_buf = reinterpret_cast<uint32_t *>(b + ((356ull * n + 15) & ~15ull) + 2560ull * n);
+    w.hs = nullptr;
     w.niels = nullptr;
     return w;
   }

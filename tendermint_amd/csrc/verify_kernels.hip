@@ -140,6 +140,15 @@ __device__ __forceinline__ void prep_hash_block(uint32_t bx, const uint8_t *__re
   uint4 *kd = reinterpret_cast<uint4 *>(w.k + 8ull * e);
   kd[0] = make_uint4(k[0], k[1], k[2], k[3]);
   kd[1] = make_uint4(k[4], k[5], k[6], k[7]);
+  if (w.hs) {  // per-entry pipeline: the half-size scalars, once per entry
+    uint32_t u[4], v[4];
+    bool neg = false;
+    const bool fast = half::reduce(u, neg, v, k);
+    uint4 *hd = reinterpret_cast<uint4 *>(w.hs + 12ull * e);
+    hd[0] = make_uint4(u[0], u[1], u[2], u[3]);
+    hd[1] = make_uint4(v[0], v[1], v[2], v[3]);
+    hd[2] = make_uint4((fast ? 1u : 0u) | (neg ? 2u : 0u), 0u, 0u, 0u);
+  }
 }
 
 template <bool SR>
@@ -338,7 +347,12 @@ __device__ __forceinline__ void quad_block(uint32_t blk, fe *tab_lds, int8_t (*d
     // every lane of the quad reduces the same k (no exchange needed); lane 0
     // recodes v, lane 1 b, lane 2 u
     half::Scalars sc;
-    if (half_on == 1 || (half_on == 2 && e % 3 != 0)) {  // 2 (tests): every third entry on the full-k path
+    if (half_on == 1 && w.hs) {  // reduced once by the prep's hash lane
+      const uint4 *hp = reinterpret_cast<const uint4 *>(w.hs + 12ull * e);
+      const uint4 hu = hp[0], hv = hp[1], hf = hp[2];
+      const uint32_t u4[4] = {hu.x, hu.y, hu.z, hu.w}, v4[4] = {hv.x, hv.y, hv.z, hv.w};
+      half::scalars_from(sc, u4, (hf.x & 2u) != 0, v4, (hf.x & 1u) != 0, k_w, s_w);
+    } else if (half_on == 1 || (half_on == 2 && e % 3 != 0)) {  // 2 (tests): every third entry on the full-k path
       half::scalars(sc, k_w, s_w);
     } else {
 #pragma unroll
@@ -1166,6 +1180,14 @@ static int half_scalars_on() {
   return !e ? 1 : !strcmp(e, "0") ? 0 : !strcmp(e, "2") ? 2 : 1;
 }
 
+// Per-entry pipeline: the half-size scalars reduced once per entry by the
+// prep's hash lane (default) or by every lane of the entry's quad
+// (TMV_HALF_PREP=0; read at every launch, for A/B).
+static bool half_prep_on() {
+  const char *e = getenv("TMV_HALF_PREP");
+  return !(e && !strcmp(e, "0"));
+}
+
 template <bool SR>
 static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig, const uint32_t *idx,
                         const uint32_t *count_ptr, uint32_t n, Ed25519Work w, const fe *btab_q, uint8_t *out,
@@ -1199,6 +1221,7 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
                                   uint8_t *out, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = is_aligned(pk, sig);
+  w.hs = half_prep_on() ? w.hs_buf : nullptr;
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
