@@ -14,6 +14,7 @@
 #include "quad.h"
 #include "ktimer.h"
 #include "verify_kernels.h"
+#include "halfscalar.h"
 
 #include <atomic>
 #include <mutex>
@@ -1025,13 +1026,13 @@ static uint32_t wpart_quad_rows() {
 // LOC: the same Horner over the locate MSM's slots (count_ptr = loc_count),
 // T'_f to mw.fail_T, no verdict; LOC = 2: the bisection slots' sums to
 // mw.l2_T (count_ptr = l2e_count).
-template <bool SR, bool KM, int LOC = 0>
-__global__ void __launch_bounds__(64)
-k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, const uint32_t *__restrict__ group_run0,
-             uint32_t n_runs) {
+template <bool SR, bool KM, int LOC>
+__device__ __forceinline__ void horner_block(uint32_t bx, const uint32_t *count_ptr, uint32_t n, MsmWork mw,
+                                             const MsmParams &p, const uint32_t *__restrict__ group_run0,
+                                             uint32_t n_runs) {
   const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
-  if (blockIdx.x * 16 >= live_groups) return;  // block-uniform
-  const uint32_t raw = blockIdx.x * 16 + (threadIdx.x >> 2);
+  if (bx * 16 >= live_groups) return;  // block-uniform
+  const uint32_t raw = bx * 16 + (threadIdx.x >> 2);
   const bool live = raw < live_groups;
   const uint32_t g = live ? raw : live_groups - 1;  // whole quads stay active for DPP
   const int c = (int)(threadIdx.x & 3);
@@ -1085,6 +1086,50 @@ k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, con
   }
   f = __builtin_amdgcn_mov_dpp(f, quad::qp(0, 0, 0, 0), 0xF, 0xF, false);  // the quad's lane 0
   if (f >= 0 && mw.fail_T) mw.fail_T[8ull * f + c] = acc;
+}
+
+template <bool SR, bool KM, int LOC = 0>
+__global__ void __launch_bounds__(64)
+k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, const uint32_t *__restrict__ group_run0,
+             uint32_t n_runs) {
+  horner_block<SR, KM, LOC>(blockIdx.x, count_ptr, n, mw, p, group_run0, n_runs);
+}
+
+// Horner with helpers (launches below the located fallback's size): blocks
+// [0, hblocks) are k_msm_horner's, raised to s_setprio 3, and the rest reduce
+// every entry's k to its half-size scalars (halfscalar.h) into w.hs_buf, so
+// the per-entry fallback of the failing groups skips its reduction.  The
+// Horner chain occupies about one SIMD in eight; the reductions run on the
+// idle ones while it does (a 125k launch: ~33 us of chip time inside a
+// ~225 us chain), not after it.
+template <bool SR>
+__global__ void __launch_bounds__(64)
+k_msm_horner_helped(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, Ed25519Work w,
+                    uint32_t hblocks) {
+  if (blockIdx.x < hblocks) {  // block-uniform
+    __builtin_amdgcn_s_setprio(3);
+    horner_block<SR, false, 0>(blockIdx.x, count_ptr, n, mw, p, nullptr, 0u);
+    return;
+  }
+  const uint32_t e = (blockIdx.x - hblocks) * 64 + threadIdx.x;
+  if (e >= entry_count(count_ptr, n)) return;
+  const uint4 *kp = reinterpret_cast<const uint4 *>(w.k + 8ull * e);
+  const uint4 k0 = kp[0], k1 = kp[1];
+  const uint32_t k[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+  uint32_t u[4], v[4];
+  bool neg = false;
+  const bool fast = half::reduce(u, neg, v, k);
+  uint4 *hd = reinterpret_cast<uint4 *>(w.hs_buf + 12ull * e);
+  hd[0] = make_uint4(u[0], u[1], u[2], u[3]);
+  hd[1] = make_uint4(v[0], v[1], v[2], v[3]);
+  hd[2] = make_uint4((fast ? 1u : 0u) | (neg ? 2u : 0u), 0u, 0u, 0u);
+}
+
+// TMV_HORNER_HELP=0: the plain Horner, and the fallback reduces in its quads
+// (read at every launch, for A/B).
+static bool horner_help() {
+  const char *e = getenv("TMV_HORNER_HELP");
+  return !(e && !strcmp(e, "0"));
 }
 
 // Located fallback, search stage: one wave per failing group (slot f).  With
@@ -1729,8 +1774,16 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
                               const fe *btab_q, Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
                               uint8_t *out, int aligned, bool compact, hipStream_t stream) {
   hipError_t e;
-  hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3((p.groups + 15) / 16), dim3(64), 0, stream, count_ptr, n, mw, p,
-                     nullptr, 0u);
+  const bool helped = compact && !locate_enabled(n, p) && horner_help() && w.hs_buf;
+  const uint32_t hblocks = (p.groups + 15) / 16;
+  if (helped) {
+    hipLaunchKernelGGL(k_msm_horner_helped<SR>, dim3(hblocks + (n + 63) / 64), dim3(64), 0, stream, count_ptr, n, mw,
+                       p, w, hblocks);
+    w.hs = w.hs_buf;  // the fallback below takes the reductions
+  } else {
+    hipLaunchKernelGGL((k_msm_horner<SR, false>), dim3(hblocks), dim3(64), 0, stream, count_ptr, n, mw, p, nullptr,
+                       0u);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (compact && locate_enabled(n, p)) {
     // second MSM over the failing groups (slot f = f-th failing group), then
