@@ -34,7 +34,8 @@ import bench  # noqa: E402  (the product model and peak)
 
 PRODUCT_KEY = {  # trace name prefix -> bench.kernel_products key (first match; the located Horner first)
     "k_prep_fused": "k_prep_fused", "k_msm_accum": "k_msm_accum", "k_msm_wpart": "k_msm_wpart",
-    "k_msm_horner<false, false, true>": "k_msm_horner_loc", "k_msm_horner": "k_msm_horner",
+    "k_msm_horner<false, false, 1>": "k_msm_horner_loc", "k_msm_horner<false, false, true>": "k_msm_horner_loc",
+    "k_msm_horner": "k_msm_horner",  # k_msm_horner_helped too: its helper blocks' reductions are not priced
     "k_verify_quad": "fallback", "k_verify_quad_list": "fallback",
 }
 
