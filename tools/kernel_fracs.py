@@ -19,6 +19,7 @@ pipeline fractions divide the sums by the launch span.
 
   python tools/kernel_fracs.py --trace T.csv --alone A.jsonl [--pmc P.csv] [--isa profiles/r05/isa_mix.json] > out.json
 """
+import gzip
 import argparse
 import csv
 import json
@@ -38,6 +39,11 @@ PRODUCT_KEY = {  # trace name prefix -> bench.kernel_products key (first match; 
     "k_msm_horner": "k_msm_horner",  # k_msm_horner_helped too: its helper blocks' reductions are not priced
     "k_verify_quad": "fallback", "k_verify_quad_list": "fallback",
 }
+
+
+
+def _open(path):  # a committed .csv.gz reads like the .csv
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
 
 
 def short(name):
@@ -76,12 +82,12 @@ def main():
                     help="the profiled build's TMV_LOCATE_MIN (groups of 128 and the located pass from it)")
     a = ap.parse_args()
     peak = bench._load_peak()
-    rows = sorted((r for r in csv.DictReader(open(a.trace)) if r["Kind"] == "KERNEL_DISPATCH"),
+    rows = sorted((r for r in csv.DictReader(_open(a.trace)) if r["Kind"] == "KERNEL_DISPATCH"),
                   key=lambda r: int(r["Start_Timestamp"]))
     tl = launches(rows, lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     pl = {}
     if a.pmc:
-        prow = [r for r in csv.DictReader(open(a.pmc)) if r["Counter_Name"] == "SQ_INSTS_VALU_INT64"]
+        prow = [r for r in csv.DictReader(_open(a.pmc)) if r["Counter_Name"] == "SQ_INSTS_VALU_INT64"]
         prow.sort(key=lambda r: int(r["Start_Timestamp"]))
         pl = launches(prow, lambda r: float(r["Counter_Value"]))
     isa = json.load(open(a.isa))["kernels"] if os.path.exists(a.isa) else {}

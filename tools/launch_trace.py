@@ -10,11 +10,17 @@ time per launch (dispatches of one name inside a launch summed).
 
   python tools/launch_trace.py gpurun_out/NAME/trace_K/run_kernel_trace.csv [--skip 3] [--csv out.csv]
 """
+import gzip
 import argparse
 import csv
 import re
 import statistics
 from collections import defaultdict
+
+
+
+def _open(path):  # a committed .csv.gz reads like the .csv
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
 
 
 def short(name: str) -> str:
@@ -28,7 +34,7 @@ def main():
     ap.add_argument("--skip", type=int, default=3)
     ap.add_argument("--csv", default="")
     a = ap.parse_args()
-    rows = [r for r in csv.DictReader(open(a.trace)) if r["Kind"] == "KERNEL_DISPATCH"]
+    rows = [r for r in csv.DictReader(_open(a.trace)) if r["Kind"] == "KERNEL_DISPATCH"]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     launches = []
     for r in rows:

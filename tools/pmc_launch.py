@@ -11,6 +11,7 @@ the peak of bench._load_peak()).
 
   python tools/pmc_launch.py COUNTERS.csv --n 125000 [--isa profiles/r05/isa_mix.json] > profiles/r05/pmc_125k.json
 """
+import gzip
 import argparse
 import csv
 import json
@@ -27,6 +28,11 @@ from kernel_fracs import short  # noqa: E402
 CLOCK_HZ = 2.4e9  # MI355X_MICROARCH.md: peak engine clock (GRBM_GUI_ACTIVE counts it per XCD)
 
 
+
+def _open(path):  # a committed .csv.gz reads like the .csv
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
@@ -35,7 +41,7 @@ def main():
     ap.add_argument("--isa", default=os.path.join(REPO, "profiles", "r05", "isa_mix.json"))
     a = ap.parse_args()
     grid = (-(-2 * a.n // 256) + -(-a.n // 256)) * 256  # k_prep_fused's grid marks a launch of n entries
-    rows = sorted(csv.DictReader(open(a.csv)), key=lambda r: (int(r["Start_Timestamp"]), r["Counter_Name"]))
+    rows = sorted(csv.DictReader(_open(a.csv)), key=lambda r: (int(r["Start_Timestamp"]), r["Counter_Name"]))
     launches, cur = [], None
     for r in rows:
         nm = short(r["Kernel_Name"])
