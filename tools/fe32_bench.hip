@@ -324,6 +324,24 @@ int main(int argc, char **argv) {
       if (rep) ms[v] += t / 3;
     }
   }
+  // the same chains on one wave per SIMD (1024 one-wave blocks): latency-bound, as the
+  // per-entry check and the Horner chain run
+  const int lreps = 512;
+  float lm[2] = {0, 0};
+  for (int rep = 0; rep < 4; rep++) {
+    for (int v = 0; v < 2; v++) {
+      hipEventRecord(e0, 0);
+      if (v == 0) hipLaunchKernelGGL(k_mul, dim3(1024), dim3(64), 0, 0, din, o1, lreps);
+      else hipLaunchKernelGGL(k_mul32, dim3(1024), dim3(64), 0, 0, din, o2, lreps);
+      hipEventRecord(e1, 0);
+      hipEventSynchronize(e1);
+      float t;
+      hipEventElapsedTime(&t, e0, e1);
+      if (rep) lm[v] += t / 3;
+    }
+  }
+  hipLaunchKernelGGL(k_mul, dim3(blocks), dim3(256), 0, 0, din, o1, reps);
+  hipLaunchKernelGGL(k_mul32, dim3(blocks), dim3(256), 0, 0, din, o2, reps);
   std::vector<uint32_t> r1(8ull * threads), r2(8ull * threads);
   hipMemcpy(r1.data(), o1, r1.size() * 4, hipMemcpyDeviceToHost);
   hipMemcpy(r2.data(), o2, r2.size() * 4, hipMemcpyDeviceToHost);
@@ -377,8 +395,9 @@ int main(int argc, char **argv) {
   const double an = (double)threads * areps;
   printf("{\"fe_mul_ns_chip\": %.5f, \"fe32_mul_ns_chip\": %.5f, \"mul_ratio\": %.3f, \"mul_words_differing\": %zu, "
          "\"madd_ns_chip\": %.5f, \"madd32_ns_chip\": %.5f, \"madd_ratio\": %.3f, \"madd_words_differing\": %zu, "
+         "\"lone_wave_fe_mul_ns\": %.2f, \"lone_wave_fe32_mul_ns\": %.2f, \"lone_wave_ratio\": %.3f, "
          "\"threads\": %d, \"reps\": %d, \"madd_reps\": %d}\n",
          ms[0] * 1e6 / n, ms[1] * 1e6 / n, ms[1] / ms[0], diff, am[0] * 1e6 / an, am[1] * 1e6 / an, am[1] / am[0],
-         adiff, threads, reps, areps);
+         adiff, lm[0] * 1e6 / lreps, lm[1] * 1e6 / lreps, lm[1] / lm[0], threads, reps, areps);
   return 0;
 }
