@@ -565,3 +565,32 @@ def test_located_then_subgroups_option():
                          timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "ok" in out.stdout
+
+
+@pytest.mark.parametrize("help_on,prep_on", [("0", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("kind", [ED, SR])
+def test_chain_knobs(bctx, kind, help_on, prep_on, monkeypatch):
+    """The round-5 paths beside their switched-off forms (defaults: both on;
+    both read at every launch): TMV_HORNER_HELP (helper workgroups reduce
+    every entry's k during the batch equation's Horner, below the located
+    size) and TMV_HALF_PREP (the per-entry pipeline's k reduced once by the
+    prep's hash lane).  Each setting gives the oracle's vector through the
+    batch equation (failing groups re-verified one by one) and per entry."""
+    monkeypatch.setenv("TMV_HORNER_HELP", help_on)
+    monkeypatch.setenv("TMV_HALF_PREP", prep_on)
+    b, sig, bad = _bisect_case(kind, 64, n=20_000 + 37)
+    if kind == ED:
+        ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
+    else:
+        ref = C.sr25519_status_packed(b.pk, sig, b.msg, b.off, threads=16)
+    for flags in (BEQ, N.TMV_FLAG_PER_ENTRY):
+        bctx.set_batch_options(seed=SEED, stats=True)
+        s0 = bctx.batch_stats()
+        ok, st = bctx.verify_batch_ex(kind, flags, b.pk, sig, b.msg, b.off)
+        s1 = bctx.batch_stats()
+        if kind == ED:
+            assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref), flags
+        else:
+            assert np.array_equal(st, ref), flags
+        if flags == BEQ:
+            assert s1["failed"] - s0["failed"] == len({i // 64 for i in bad if i < b.n})
