@@ -755,8 +755,15 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 // chunk but its last, part_first of the last).  Each wave scans
 // kJoinScan x 64 chunks' join_b words (coalesced), gathers the named
 // buckets into a wave-local LDS list and joins them 64 at a time, so the
-// grid is small and no wave walks the join for one lane.
-constexpr uint32_t kJoinScan = 16;
+// grid is small and no wave walks the join for one lane.  The join is
+// latency-bound (its waves wait on the partials' loads), so more, shorter
+// waves pay: 8 x 64 chunks per wave, k_msm_join per launch at 1M / 2.56M
+// 150 / 338 us vs 171 / 345 (16), 197 / 357 (32), 245 / 386 (64), 216 /
+// 483 (4) (profiles/r05/ab_join_scan.txt).
+#ifndef TMV_JOIN_SCAN
+#define TMV_JOIN_SCAN 8
+#endif
+constexpr uint32_t kJoinScan = TMV_JOIN_SCAN;
 __global__ void __launch_bounds__(256)
 k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   __shared__ uint32_t list[4][kJoinScan * 64];
