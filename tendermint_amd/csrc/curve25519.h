@@ -601,8 +601,12 @@ TMV_HD void ge_p3_neg(ge_p3 &r, const ge_p3 &p) {
   fe_neg(r.X, p.X); r.Y = p.Y; r.Z = p.Z; fe_neg(r.T, p.T);
 }
 
+// Every verdict below also requires Z != 0: the complete formulas never give a
+// point Z == 0, so only a result never computed (e.g. an unwritten, zeroed
+// workspace slot, (0 : 0 : 0 : 0)) has it -- and it would otherwise pass
+// X == 0, Y == Z.  A missing write then fails a check instead of passing it.
 TMV_HD bool ge_p3_is_identity(const ge_p3 &p) {
-  return fe_is_zero(p.X) && fe_eq(p.Y, p.Z);
+  return fe_is_zero(p.X) && fe_eq(p.Y, p.Z) && !fe_is_zero(p.Z);
 }
 
 // Cofactored identity test: [8]p == O.
@@ -615,7 +619,7 @@ TMV_HD bool ge_p3_is_small_order_or_identity_times8(const ge_p3 &p) {
   ge_p1p1_to_p2(q, t);
   ge_p2_dbl(t, q);
   ge_p1p1_to_p2(q, t);
-  return fe_is_zero(q.X) && fe_eq(q.Y, q.Z);
+  return fe_is_zero(q.X) && fe_eq(q.Y, q.Z) && !fe_is_zero(q.Z);
 }
 
 // ZIP-215 lax decoding of an edwards25519 point (crypto/ed25519/ed25519.go:27-29
@@ -748,8 +752,9 @@ TMV_HD void ristretto_encode(uint32_t out[8], const ge_p3 &p) {
   fe_to_words(out, s);
 }
 
-// Ristretto equality: X1 Y2 == Y1 X2 or Y1 Y2 == X1 X2.
+// Ristretto equality: X1 Y2 == Y1 X2 or Y1 Y2 == X1 X2 (and Z1, Z2 != 0).
 TMV_HD bool ristretto_equal(const ge_p3 &a, const ge_p3 &b) {
+  if (fe_is_zero(a.Z) || fe_is_zero(b.Z)) return false;
   fe l, r;
   fe_mul(l, a.X, b.Y);
   fe_mul(r, a.Y, b.X);

@@ -58,6 +58,12 @@ constexpr int kMsmSortBlock = 256;
 #define TMV_NO_JOIN 0
 #endif
 constexpr bool kMsmJoin = !TMV_NO_JOIN;
+// k_msm_join's input: a packed list appended by k_msm_accum (1) or one word
+// per chunk scanned by k_msm_join (0, rounds 2-5)
+#ifndef TMV_JOIN_LIST
+#define TMV_JOIN_LIST 1
+#endif
+constexpr bool kMsmJoinList = TMV_JOIN_LIST;
 constexpr uint32_t kSubGroupLog2 = 3;        // k_msm_subcheck: 8 entries per sub-group
 constexpr uint32_t kSubGroup = 1u << kSubGroupLog2;
 
@@ -180,7 +186,10 @@ struct MsmWork {
   ge_p3 *bk_sum;       // groups x W x H: sums of buckets that fit in one chunk
   ge_p3 *part_first;   // chunks: run that began in an earlier chunk and ends here
   ge_p3 *part_last;    // chunks: run that continues into the next chunk
-  uint32_t *join_b;    // chunks: bucket whose chunk partials k_msm_join joins (the chunk of its last run), or kMsmEmpty
+  uint32_t *join_b;    // chunks: bucket whose chunk partials k_msm_join joins (the chunk of its last run), or kMsmEmpty;
+                       // TMV_JOIN_LIST: the named buckets packed at the front, *join_count of them
+  uint32_t *join_count;  // groups: [g0] counts the list of the view starting at group g0 (parts of a
+                         // launch may run at once); reset by every k_msm_sort, appended by k_msm_accum
   ge_p3 *wpart;        // groups x W x P x 2: (T, U) of each window part
   ge_p3 *wsum;         // groups x W: window sums
   uint8_t *group_ok;   // groups
@@ -225,7 +234,7 @@ struct MsmWork {
     const size_t chunks = ent / p.L;
     size_t b = (2ull * n + 1) * kNielsPer * sizeof(niels_pt) + 8 * ent + 8 * bk + bk * sizeof(ge_p3) +
                2 * chunks * sizeof(ge_p3) + 4 * chunks + G * p.W * (2ull * p.wpart_slots() + 1) * sizeof(ge_p3) + G + 2 * G +
-               17 * 16;
+               18 * 16 + 4 * G;
     if (p.merged) b += 32ull * n + 32 * G + max_items(n, p) * 4 * sizeof(fe);
     else b += 16 + 4 * G + (G << p.m_log2) / kSubGroup + 16 + (size_t)n * 32 * sizeof(fe) + 3 * 16 +
               G * 8 * sizeof(fe) + 16 + 4ull * n + 2 * 16 + 4 * G + 2 * 16 + G * 4 * sizeof(fe) + 16;
@@ -247,6 +256,7 @@ struct MsmWork {
     w.part_first = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.part_last = reinterpret_cast<ge_p3 *>(b + o); o = up(o + chunks * sizeof(ge_p3));
     w.join_b = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * chunks);
+    w.join_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
     w.wpart = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * 2ull * p.wpart_slots() * sizeof(ge_p3));
     w.wsum = reinterpret_cast<ge_p3 *>(b + o); o = up(o + G * p.W * sizeof(ge_p3));
     w.group_ok = b + o; o = up(o + G);

@@ -268,6 +268,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   const uint32_t cnt = entry_count(count_ptr, n);
   const uint32_t tid = threadIdx.x;
   uint32_t g = blockIdx.x;  // LOC: the slot; the group is fail_list[slot]
+  if (kMsmJoinList && g == 0 && tid == 0) *mw.join_count = 0;  // the next k_msm_accum appends its joins
   if (LOC == 2) {
     const uint32_t ns = min(2u * *mw.l2_count, p.groups);
     if (g == 0 && tid == 0) *mw.l2e_count = ns << p.m_log2;  // the bucket stages' entry count
@@ -636,8 +637,8 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 #define TMV_BK(q) bkp[q]
 #define TMV_PT(q) ptp[q]
 #endif
-  if (TMV_BK(0) == kMsmEmpty) {  // padding: nothing to join (k_msm_join reads every live chunk's word)
-    if (kMsmJoin) mw.join_b[t] = kMsmEmpty;
+  if (TMV_BK(0) == kMsmEmpty) {  // padding: nothing to join (the scan form of k_msm_join reads every live chunk's word)
+    if (kMsmJoin && !kMsmJoinList) mw.join_b[t] = kMsmEmpty;
     return;
   }
   uint32_t join = kMsmEmpty;  // this chunk's join_b
@@ -745,7 +746,20 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     p3_add(acc, first_run[threadIdx.x + 1]);
     mw.bk_sum[cur] = acc;
   }
-  if (kMsmJoin) mw.join_b[t] = join;
+  if (kMsmJoin && kMsmJoinList) {
+    // append this wave's joins to the launch's list: one atomic per wave, by
+    // its lowest joining lane
+    const uint64_t jm = __ballot(join != kMsmEmpty);
+    if (jm) {  // wave-uniform
+      const int leader = __ffsll((unsigned long long)jm) - 1;
+      uint32_t jb = 0;
+      if ((int)lane == leader) jb = atomicAdd(mw.join_count, (uint32_t)__popcll(jm));
+      jb = __shfl(jb, leader);
+      if (join != kMsmEmpty) mw.join_b[jb + __popcll(jm & ((1ull << lane) - 1))] = join;
+    }
+  } else if (kMsmJoin) {
+    mw.join_b[t] = join;
+  }
 }
 #undef TMV_BK
 #undef TMV_PT
@@ -764,6 +778,19 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
 #define TMV_JOIN_SCAN 8
 #endif
 constexpr uint32_t kJoinScan = TMV_JOIN_SCAN;
+// List form (TMV_JOIN_LIST=1): k_msm_accum appends the named buckets to a
+// packed list (one atomic per wave), and k_msm_join strides over it with
+// every lane busy, instead of scanning every chunk's word.
+__global__ void __launch_bounds__(256)
+k_msm_join_list(MsmWork mw, MsmParams p) {
+  const uint32_t cnt = *mw.join_count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const uint32_t b = mw.join_b[i];
+    ge_p3 B;
+    bucket_value(mw, p.L, b, B, mw.bk_cnt[b], mw.bk_start[b]);
+    mw.bk_sum[b] = B;
+  }
+}
 __global__ void __launch_bounds__(256)
 k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   __shared__ uint32_t list[4][kJoinScan * 64];
@@ -1570,7 +1597,12 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
   hipError_t e;
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
-  if (kMsmJoin) {
+  if (kMsmJoin && kMsmJoinList) {
+    // lanes for ~3% of the chunks (C2 names ~2.5%); more joins stride
+    const uint32_t jblocks = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((chunks / 32 + 255) / 256, 1), 8192);
+    hipLaunchKernelGGL(k_msm_join_list, dim3(jblocks), dim3(256), 0, stream, mw, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else if (kMsmJoin) {
     const uint64_t per_block = 4ull * kJoinScan * 64;
     hipLaunchKernelGGL(k_msm_join, dim3((uint32_t)((chunks + per_block - 1) / per_block)), dim3(256), 0, stream,
                        count_ptr, n, mw, p);
@@ -1722,6 +1754,7 @@ static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0)
   mw.part_first += g0 * p.chunks_per_group();
   mw.part_last += g0 * p.chunks_per_group();
   mw.join_b += g0 * p.chunks_per_group();
+  mw.join_count += g0;  // the view's own counter: parts may run at once
   mw.wpart += g0 * p.W * 2ull * p.P;
   mw.wsum += g0 * p.W;
   mw.group_ok += g0;

@@ -317,21 +317,29 @@ TMV_DEV bool is_identity_times8(const fe &p) {
   fe_dpp<qp(2, 2, 2, 2)>(z, q);
   fe_signed(z, z, c == 1 ? 1 : 0);
   fe d;
-  fe_sub(d, q, z);                          // lane 0: X, lane 1: Y - Z
+  fe_sub(d, q, z);                          // lane 0: X, lane 1: Y - Z, lane 2: Z
   const int zero = fe_is_zero(d) ? 1 : 0;
   const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
   const int z1 = __builtin_amdgcn_mov_dpp(zero, qp(1, 1, 1, 1), 0xF, 0xF, false);
-  return (z0 & z1) != 0;
+  const int z2 = __builtin_amdgcn_mov_dpp(zero, qp(2, 2, 2, 2), 0xF, 0xF, false);
+  return (z0 & z1 & (z2 ^ 1)) != 0;         // Z == 0 only for a never-computed point (ge_p3_is_identity)
 }
 
 // Ristretto identity of a P3Q point (equal to O modulo the 4-torsion: X == 0
 // or Y == 0).  Quad verdict on every lane.
 TMV_DEV bool is_ristretto_identity(const fe &p) {
-  const int c = lane4();
-  const int zero = (c <= 1 && fe_is_zero(p)) ? 1 : 0;  // lane 0: X, lane 1: Y
+  const int zero = fe_is_zero(p) ? 1 : 0;  // lane 0: X, lane 1: Y, lane 2: Z
   const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
   const int z1 = __builtin_amdgcn_mov_dpp(zero, qp(1, 1, 1, 1), 0xF, 0xF, false);
-  return (z0 | z1) != 0;
+  const int z2 = __builtin_amdgcn_mov_dpp(zero, qp(2, 2, 2, 2), 0xF, 0xF, false);
+  return ((z0 | z1) & (z2 ^ 1)) != 0;
+}
+
+// Z1 != 0 and Z2 != 0 (lane 2 of each P3Q point): the equalities below hold
+// for a never-computed (0 : 0 : 0 : 0) point against anything.  Quad verdict.
+TMV_DEV bool both_z_nonzero(const fe &a, const fe &b) {
+  const int nz = (fe_is_zero(a) || fe_is_zero(b)) ? 0 : 1;  // lane 2: Z1, Z2
+  return __builtin_amdgcn_mov_dpp(nz, qp(2, 2, 2, 2), 0xF, 0xF, false) != 0;
 }
 
 // Equality of two P3Q points: X1 Z2 == X2 Z1 and Y1 Z2 == Y2 Z1.  Quad
@@ -353,7 +361,7 @@ TMV_DEV bool p3_equal(const fe &a, const fe &b) {
   const int zero = fe_is_zero(d) ? 1 : 0;
   const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
   const int z1 = __builtin_amdgcn_mov_dpp(zero, qp(1, 1, 1, 1), 0xF, 0xF, false);
-  return (z0 & z1) != 0;
+  return (z0 & z1) != 0 && both_z_nonzero(a, b);
 }
 
 // Ristretto equality of two P3Q points a (acc) and b (R):
@@ -368,7 +376,7 @@ TMV_DEV bool ristretto_equal(const fe &a, const fe &b) {
   const int zero = fe_is_zero(d) ? 1 : 0;
   const int z0 = __builtin_amdgcn_mov_dpp(zero, qp(0, 0, 0, 0), 0xF, 0xF, false);
   const int z2 = __builtin_amdgcn_mov_dpp(zero, qp(2, 2, 2, 2), 0xF, 0xF, false);
-  return (z0 | z2) != 0;
+  return (z0 | z2) != 0 && both_z_nonzero(a, b);
 }
 
 }  // namespace quad

@@ -302,3 +302,16 @@ extern "C" void hostcheck_verify_half(const uint8_t *pk, const uint8_t *sig, con
   }
   *n_slow = slow;
 }
+
+// Verdicts on a never-computed point (0 : 0 : 0 : 0) -- e.g. an unwritten,
+// zeroed workspace slot -- and on the identity: returns 1 when every
+// identity / equality check rejects the former and accepts the latter.
+extern "C" int hostcheck_degenerate_verdicts() {
+  ge_p3 z, id;
+  fe_zero(z.X); fe_zero(z.Y); fe_zero(z.Z); fe_zero(z.T);
+  ge_p3_identity(id);
+  const bool rej = !ge_p3_is_identity(z) && !ge_p3_is_small_order_or_identity_times8(z) &&
+                   !ristretto_equal(z, id) && !ristretto_equal(id, z) && !ristretto_equal(z, z);
+  const bool acc = ge_p3_is_identity(id) && ge_p3_is_small_order_or_identity_times8(id) && ristretto_equal(id, id);
+  return rej && acc ? 1 : 0;
+}

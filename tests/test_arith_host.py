@@ -213,3 +213,11 @@ def test_p1p1_to_cached_matches_two_step(H):
     buf = np.frombuffer(b"".join(enc), np.uint8).copy()
     H.hostcheck_p1p1_to_cached.restype = ctypes.c_int
     assert H.hostcheck_p1p1_to_cached(p(buf), len(enc)) == 0
+
+
+def test_degenerate_point_fails_every_verdict(H):
+    """A point never computed ((0 : 0 : 0 : 0), a zeroed slot nobody wrote)
+    passes X == 0, Y == Z and both Ristretto equalities; every verdict also
+    requires Z != 0, so a missing write fails a group instead of passing it
+    (the quad forms in quad.h carry the same test, covered on the GPU)."""
+    assert H.hostcheck_degenerate_verdicts() == 1
