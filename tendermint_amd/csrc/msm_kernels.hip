@@ -785,10 +785,19 @@ __global__ void __launch_bounds__(256)
 k_msm_join_list(MsmWork mw, MsmParams p) {
   const uint32_t cnt = *mw.join_count;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    // a listed bucket spans two or more chunks: the run that left its first
+    // chunk, the middle chunks, the run that ended in its last (bucket_value,
+    // written out so the partials stay in registers, not scratch)
     const uint32_t b = mw.join_b[i];
-    ge_p3 B;
-    bucket_value(mw, p.L, b, B, mw.bk_cnt[b], mw.bk_start[b]);
-    mw.bk_sum[b] = B;
+    const uint32_t bs = mw.bk_start[b], t0 = bs / p.L, t1 = (bs + mw.bk_cnt[b] - 1) / p.L;
+    ge_p3 acc = mw.part_last[t0];
+    for (uint32_t t = t0 + 1; t < t1; t++) {
+      const ge_p3 q = mw.part_last[t];
+      p3_add(acc, q);
+    }
+    const ge_p3 q = mw.part_first[t1];
+    p3_add(acc, q);
+    mw.bk_sum[b] = acc;
   }
 }
 __global__ void __launch_bounds__(256)
