@@ -29,6 +29,7 @@ KERNELS = {
     "k_msm_wpart": ("msm_kernels.hip", "_ZN3tmv11k_msm_wpartE"),
     "k_msm_wsum": ("msm_kernels.hip", "_ZN3tmv10k_msm_wsumE"),
     "k_msm_join": ("msm_kernels.hip", "_ZN3tmv10k_msm_joinE"),
+    "k_msm_join_list": ("msm_kernels.hip", "_ZN3tmv15k_msm_join_listE"),
     "k_msm_horner<false, false, 0>": ("msm_kernels.hip", "_ZN3tmv12k_msm_hornerILb0ELb0ELi0E"),
     "k_msm_horner<false, false, 1>": ("msm_kernels.hip", "_ZN3tmv12k_msm_hornerILb0ELb0ELi1E"),
     "k_msm_horner_helped<false>": ("msm_kernels.hip", "_ZN3tmv19k_msm_horner_helpedILb0E"),
