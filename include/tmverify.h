@@ -47,6 +47,10 @@ extern "C" {
  * device may still read them, so they are never unregistered under it (and
  * the library keeps no record that could unregister them once reused). */
 #define TMV_ERR_TIMEOUT (-5)
+/* The OS random source (getrandom) failed while drawing a batch equation's
+ * weights (the reference's rand.Reader error, crypto/ed25519/ed25519.go:232);
+ * nothing was launched.  tmv_last_error() names the errno. */
+#define TMV_ERR_RANDOM (-6)
 
 /* Per-entry sr25519 status (tmv_sr25519_verify_batch, tmv_verify_mixed_batch):
  *   1 valid, 0 invalid, TMV_SR_ADDERR_* = BatchVerifier.Add would have

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <sys/random.h>
 
+#include <cerrno>
+
 #include <algorithm>
 #include <array>
 #include <atomic>
@@ -284,6 +286,15 @@ void leak_pins(int dev, HostLane &ln) {
 void release_leaked_pins() {
   std::lock_guard<std::mutex> lk(g_leak_mu);
   if (g_leaked.empty()) return;
+  // the caller's current device is restored on return (this runs inside
+  // tmv_open / tmv_close / host-buffer calls, on the caller's thread)
+  int cur = -1;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  struct Restore {
+    bool on;
+    int dev;
+    ~Restore() { if (on) (void)hipSetDevice(dev); }
+  } restore{have_cur, cur};
   std::vector<LeakedPin> keep;
   for (const LeakedPin &x : g_leaked) {
     (void)hipSetDevice(x.dev);
@@ -561,7 +572,40 @@ struct LaunchOpts {
   tmv::MsmParams p_ed{};   // the ed25519 half of a mixed launch
   tmv::MsmParams p_ed_streamed{};  // ... of a streamed one (mixed_check_streamed)
   tmv::MsmSeed seed[2]{};  // [kind]
+  int err = 0;             // < 0: no launch (the weights' key could not be drawn)
 };
+
+// Test aid (tmv_internal_random_fault): the next `count` getrandom calls
+// fail with errno `err` (count < 0: every call).
+std::atomic<int> g_rand_fault_err{0}, g_rand_fault_count{0};
+
+// The key of a launch's ChaCha20 weights from the OS (the reference draws z
+// from rand.Reader, crypto/ed25519/ed25519.go:232, and a Reader error
+// reaches its caller).  Short reads and EINTR are retried; any other failure
+// (ENOSYS, a seccomp EPERM, ...) returns TMV_ERR_RANDOM instead of spinning.
+int draw_weight_key(uint8_t key[32]) {
+  size_t got = 0;
+  while (got < 32) {
+    ssize_t r;
+    int fc = g_rand_fault_count.load();
+    if (fc != 0) {
+      if (fc > 0) g_rand_fault_count.fetch_sub(1);
+      errno = g_rand_fault_err.load();
+      r = -1;
+    } else {
+      r = getrandom(key + got, 32 - got, 0);
+    }
+    if (r > 0) {
+      got += (size_t)r;
+    } else if (r < 0 && errno == EINTR) {
+      continue;
+    } else {
+      set_error(std::string("getrandom: ") + (r < 0 ? strerror(errno) : "no bytes"));
+      return TMV_ERR_RANDOM;
+    }
+  }
+  return 0;
+}
 
 }  // namespace
 
@@ -641,13 +685,7 @@ static LaunchOpts make_opts(tmv_ctx *ctx, uint32_t flags, uint32_t n, bool merge
     fixed = ctx->fixed_seed;
     if (fixed) std::memcpy(key, ctx->seed, 32);
   }
-  if (!fixed) {
-    size_t got = 0;
-    while (got < 32) {  // the reference draws z from rand.Reader (crypto/ed25519/ed25519.go:232)
-      const ssize_t r = getrandom(key + got, 32 - got, 0);
-      if (r > 0) got += (size_t)r;
-    }
-  }
+  if (!fixed && (o.err = draw_weight_key(key)) != 0) return o;
   const uint64_t ctr = ctx->launches.fetch_add(1);
   for (int k = 0; k < 2; k++) {
     std::memcpy(o.seed[k].key, key, 32);
@@ -1145,7 +1183,7 @@ static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t
   int rc;
   Workspace *ws = reserve_work(d, n, true, s, &rc, &o.p_ed, &o.p);
   if (!ws) return rc;
-  if (!s2) s2 = s;
+  if (!s2 || !join) s2 = s;  // no helper stream, or no event to join it back: one stream (as batch_check)
   tmv::Ed25519Work w_ed = tmv::Ed25519Work::carve(ws->work.ptr, n);
   tmv::Ed25519Work w_sr = tmv::Ed25519Work::carve(ws->work2.ptr, n);
   // workspaces carved for n slots per kind (the kinds' counts are known only
@@ -1356,6 +1394,8 @@ static int launch_ed25519(Device &d, const LaunchOpts &o, const uint8_t *pk, con
   return 0;
 }
 
+static uint32_t mixed_stream_chunk(size_t free_bytes);
+
 extern "C" {
 
 int tmv_kernel_timing(tmv_ctx *ctx, int enable) {
@@ -1380,6 +1420,21 @@ int tmv_kernel_timing_read(tmv_ctx *ctx, const char *kernel, double *total_ms, u
 
 const char *tmv_last_error(void) { return g_last_error.c_str(); }
 void tmv_internal_set_error(const char *msg) { g_last_error = msg ? msg : ""; }
+
+// Test aids (tests/test_failure_handling.py): inject getrandom failures and
+// draw one weights key the way every batch-equation launch does.
+void tmv_internal_random_fault(int err, int count) {
+  g_rand_fault_err = err;
+  g_rand_fault_count = count;
+}
+int64_t tmv_internal_mixed_stream_chunk(uint64_t free_bytes) {
+  read_env();
+  return mixed_stream_chunk((size_t)free_bytes);
+}
+int tmv_internal_draw_key(uint8_t *out32) {
+  if (!out32) { set_error("null argument"); return TMV_ERR_ARG; }
+  return draw_weight_key(out32);
+}
 
 tmv_ctx *tmv_open(uint32_t device_mask) { return tmv_open_logical(device_mask, 1); }
 
@@ -1531,6 +1586,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
   }
   tm.mark("keys", n);
   LaunchOpts o = make_opts(ctx, flags, n, cached, sch == Scheme::Ed25519 || sch == Scheme::Ed25519Cached);
+  if (o.err) return o.err;
   // key-merged form: worth it while a group holds few keys (runs <= n / 2)
   bool merged = cached && o.batch_eq;
   uint32_t distinct = 0;
@@ -1817,6 +1873,22 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
   return 0;
 }
 
+// Entries per streamed mixed chunk.  mixed_check_streamed carves both
+// kinds' per-entry scratch and MSM workspaces for the whole chunk (the kinds'
+// counts are known only part by part), ~20 KB per entry, and a lane's
+// workspace only grows: the chunk is capped so that the host lanes' workspaces
+// together take at most half of the device memory free at the call (3.7M
+// entries on an idle MI355X; a smaller device gets smaller chunks instead of
+// TMV_ERR_NOMEM).
+static uint32_t mixed_stream_chunk(size_t free_bytes) {
+  constexpr uint32_t kN = 1u << 20;
+  const tmv::MsmParams p = tmv::MsmParams::make(kN, 6, 5);
+  const double per_entry = (2.0 * tmv::Ed25519Work::bytes(kN) + 2.0 * tmv::MsmWork::bytes(kN, p)) / kN;
+  const double fit = (double)free_bytes / 2.0 / (std::max<uint32_t>(1, g_host_lanes) * per_entry);
+  const uint32_t c = (uint32_t)std::min<double>(g_stream_chunk, fit) & ~65535u;
+  return std::max<uint32_t>(c, 65536u);
+}
+
 // Host-buffer batch: shard by contiguous index ranges over the context's
 // devices, stage, launch, gather.  out gets 1 byte per entry.
 static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_t *pk, const uint8_t *sig,
@@ -1847,9 +1919,16 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
   const bool mixed_batch_eq = sch == Scheme::Mixed && !vs && !(flags & TMV_FLAG_PER_ENTRY) &&
                               ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
   const bool mixed_streamed = mixed_batch_eq && g_stream && mixed_stream_on();
-  const tmh::ShardPlan plan = tmh::plan_shards(
-      n, (uint32_t)ctx->devs.size(),
-      streamable || mixed_streamed ? g_stream_chunk : (mixed_batch_eq ? g_mixed_chunk : g_host_chunk));
+  uint32_t chunk = streamable ? g_stream_chunk : (mixed_batch_eq ? g_mixed_chunk : g_host_chunk);
+  if (mixed_streamed) {
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(ctx->devs[0]->id) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+      (void)hipGetLastError();
+      free_b = 0;
+    }
+    chunk = free_b ? mixed_stream_chunk(free_b) : g_mixed_chunk;
+  }
+  const tmh::ShardPlan plan = tmh::plan_shards(n, (uint32_t)ctx->devs.size(), chunk);
   const uint32_t shards = plan.shards;
   // claim g_host_lanes lanes per device (devices in order, so concurrent
   // calls cannot deadlock); released on every return
@@ -2179,6 +2258,7 @@ int tmv_verify_mixed_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_kin
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const LaunchOpts o = make_opts(ctx, 0, n);
+  if (o.err) return o.err;
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc = launch_mixed(*dev, o, d_kind, d_pk, d_sig, d_msg, d_msg_off, n, d_status, s);
@@ -2199,6 +2279,7 @@ int tmv_verify_batch_device_ex(tmv_ctx *ctx, int device, uint8_t key_kind, uint3
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
+  if (o.err) return o.err;
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   uint8_t *out = reinterpret_cast<uint8_t *>(d_status);
@@ -2256,6 +2337,7 @@ int tmv_verify_batches_device(tmv_ctx *ctx, int device, uint8_t key_kind, uint32
   if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const uint32_t n = (uint32_t)N;
   const LaunchOpts o = make_opts(ctx, flags, n, false, key_kind == TMV_KIND_ED25519);
+  if (o.err) return o.err;
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc;
@@ -2427,6 +2509,7 @@ int tmv_ed25519_verify_batch_device(tmv_ctx *ctx, int device, const uint8_t *d_p
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : context_stream(*dev);
   if (!s) { set_error("hipStreamCreate failed"); return TMV_ERR_NO_DEVICE; }
   const LaunchOpts o = make_opts(ctx, 0, n, false, true);
+  if (o.err) return o.err;
   ctx->count_call(n);
   std::lock_guard<std::mutex> lk(dev->mu);
   int rc = launch_ed25519(*dev, o, d_pk, d_sig, d_msg, d_msg_off, n, d_valid, s);

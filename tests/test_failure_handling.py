@@ -109,3 +109,50 @@ def test_sliced_call_error_reaches_caller_thread(fake, monkeypatch):
     assert L.commitcheck_verify_commits(pj1.arr, pj1.n, pj1.results, pj1.errs, pj1.stride) == ok >= 0
     assert pj1.decode() == sliced
     assert len(seen) >= 1 and np.all(np.asarray([len(s) for s in seen]) > 0)
+
+
+def test_random_source_failure_is_an_error_not_a_spin():
+    """A getrandom failure while drawing a launch's weights key returns
+    TMV_ERR_RANDOM with the errno in tmv_last_error (it
+    used to loop forever); EINTR and short reads are retried
+    (crypto/ed25519/ed25519.go:232 surfaces rand.Reader errors)."""
+    import errno
+    from tendermint_amd import _native
+    L = _native.lib()
+    L.tmv_internal_random_fault.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.tmv_internal_draw_key.argtypes = [ctypes.c_void_p]
+    L.tmv_last_error.restype = ctypes.c_char_p
+    key = (ctypes.c_uint8 * 32)()
+    try:
+        assert L.tmv_internal_draw_key(key) == 0
+        assert any(key)
+        for err in (errno.ENOSYS, errno.EPERM):
+            L.tmv_internal_random_fault(err, -1)  # every call fails
+            assert L.tmv_internal_draw_key(key) == -6  # TMV_ERR_RANDOM, returned at once
+            assert L.tmv_last_error().decode().startswith("getrandom: ")
+        L.tmv_internal_random_fault(errno.EINTR, 3)  # interrupted three times, then fine
+        assert L.tmv_internal_draw_key(key) == 0
+    finally:
+        L.tmv_internal_random_fault(0, 0)
+
+
+def test_mixed_stream_chunk_fits_device_memory():
+    """a streamed mixed chunk's workspaces (both kinds'
+    per-entry scratch and MSM workspaces, per host lane) are sized from the
+    device memory free at the call (~20 KB per entry and lane: 3.5M+ entries
+    on an idle 288 GB MI355X, so the bench's 1M mixed batch stays one chunk),
+    smaller chunks on a smaller device instead of TMV_ERR_NOMEM."""
+    from tendermint_amd import _native
+    L = _native.lib()
+    L.tmv_internal_mixed_stream_chunk.restype = ctypes.c_int64
+    L.tmv_internal_mixed_stream_chunk.argtypes = [ctypes.c_uint64]
+    gib = 1 << 30
+    big = L.tmv_internal_mixed_stream_chunk(280 * gib)
+    assert 3 << 20 <= big <= 1 << 22
+    prev = 0
+    for free in (1, 8, 16, 32, 64, 128, 280):
+        c = L.tmv_internal_mixed_stream_chunk(free * gib)
+        assert 65536 <= c <= 1 << 22 and c % 65536 == 0 and c >= prev
+        prev = c
+    c32 = L.tmv_internal_mixed_stream_chunk(32 * gib)
+    assert 65536 < c32 < big // 4
