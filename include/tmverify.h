@@ -147,7 +147,7 @@ int tmv_verify_batch_ex(tmv_ctx *ctx, uint8_t key_kind, uint32_t flags, const ui
  * opt_flags: TMV_BATCHOPT_STATS = count group verdicts (host-buffer calls;
  * costs one small device read per call); TMV_BATCHOPT_SUBCHECK_ON / _OFF =
  * re-check failing groups by sub-groups of 8 before the per-entry fallback
- * (default: for groups of >= 256, $TMV_SUBCHECK overrides); with it off,
+ * (default: for groups of >= 256 entries); with it off,
  * launches of >= $TMV_LOCATE_MIN (400000) entries locate a failing group's
  * one bad entry by a second, index-weighted equation. */
 #define TMV_BATCHOPT_STATS 1u
@@ -183,7 +183,7 @@ int tmv_merkle_roots(tmv_ctx *ctx, const uint8_t *data, const uint32_t *leaf_off
 /* Sub-groups of failing groups checked / failed (k_msm_subcheck: a failing
  * group's sub-groups of 8 entries are re-checked with the same equation
  * before entry-by-entry verification; TMV_BATCHOPT_STATS; 0 with
- * TMV_SUBCHECK=0).  No reference counterpart (voi verifies a failing batch
+ * the sub-group check off).  No reference counterpart (voi verifies a failing batch
  * entry by entry, crypto/ed25519/ed25519.go:231-233). */
 int tmv_subgroup_stats(tmv_ctx *ctx, uint64_t *subgroups, uint64_t *subgroups_failed);
 /* Mixed batch with flags (see tmv_verify_mixed_batch). */

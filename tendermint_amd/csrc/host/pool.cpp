@@ -1,5 +1,6 @@
 // Worker pool behind tmh::pool_for (pool.h).
 #include "pool.h"
+#include "../knobs.h"
 
 #include <algorithm>
 #include <atomic>
@@ -145,9 +146,14 @@ class Reaper {
 };
 }  // namespace
 
+bool host_timing() {
+  static const bool on = std::getenv("TMV_HOST_TIMING") != nullptr;
+  return on;
+}
+
 bool reap(std::unique_ptr<Garbage> &g) {
-  static const bool on = [] {
-    const char *e = std::getenv("TMV_DEFERRED_RELEASE");
+  static const bool on = [] {  // A/B (knobs.h): TMV_DEFERRED_RELEASE=0 frees inline
+    const char *e = tmv::ab_knob("TMV_DEFERRED_RELEASE");
     return !(e && e[0] == '0');
   }();
   if (!on) return false;

@@ -19,6 +19,9 @@ void pool_for(size_t n, size_t max_threads, void (*fn)(void *, size_t), void *ct
 
 // Threads the pool may use: min(16, hardware threads), or TMV_HOST_THREADS.
 size_t pool_threads();
+// TMV_HOST_TIMING set: the engine and the host layer print phase timings to
+// stderr (profiling aid; read once).
+bool host_timing();
 
 // Deferred release: a call's converted objects (validator sets, commits,
 // plans: ~10^4 small heap objects per commit window, 0.3-1.2 ms to free) are

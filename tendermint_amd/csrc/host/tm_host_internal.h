@@ -26,7 +26,7 @@ namespace tmh_internal {
 // variable TMV_HOST_TIMING is set (profiling aid).
 struct PhaseTimer {
   const char *tag;
-  bool on = std::getenv("TMV_HOST_TIMING") != nullptr;
+  bool on = tmh::host_timing();
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   explicit PhaseTimer(const char *tag_) : tag(tag_) {}
   void mark(const char *what) {

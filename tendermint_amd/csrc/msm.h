@@ -48,22 +48,12 @@ namespace tmv {
 
 constexpr uint32_t kMsmWideRows = 65536;     // (group, window) rows from which k_msm_wpart runs one lane per window
 constexpr uint32_t kLocParts = 4;            // running-sum lanes per window of the located pass (few live groups)
-constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 8, 16 or 32
+constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 16 or 32
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
-// Buckets cut by chunk edges joined by k_msm_accum (neighbouring lanes of a
-// wave) and k_msm_join (the rest) before the running sums, which then read
-// whole buckets only.  -DTMV_NO_JOIN=1: k_msm_wpart joins them (round 2).
-#ifndef TMV_NO_JOIN
-#define TMV_NO_JOIN 0
-#endif
-constexpr bool kMsmJoin = !TMV_NO_JOIN;
-// k_msm_join's input: a packed list appended by k_msm_accum (1) or one word
-// per chunk scanned by k_msm_join (0, rounds 2-5)
-#ifndef TMV_JOIN_LIST
-#define TMV_JOIN_LIST 1
-#endif
-constexpr bool kMsmJoinList = TMV_JOIN_LIST;
+// Buckets cut by chunk edges are joined by k_msm_accum (neighbouring lanes of
+// a wave) and k_msm_join_list (the rest, from a packed list) before the
+// running sums, which then read whole buckets only.
 constexpr uint32_t kSubGroupLog2 = 3;        // k_msm_subcheck: 8 entries per sub-group
 constexpr uint32_t kSubGroup = 1u << kSubGroupLog2;
 
@@ -111,7 +101,7 @@ struct MsmParams {
   uint32_t cap;      // sorted-entry slots per group (multiple of kMsmChunkMax)
   uint32_t groups;   // groups allocated = ceil(n / m)
   uint32_t P;        // lanes per window in k_msm_wpart (power of two <= H)
-  uint32_t L;        // sorted entries per k_msm_accum lane (8, 16 or 32)
+  uint32_t L;        // sorted entries per k_msm_accum lane (16 or 32)
   uint32_t merged;   // key-merged form: R points only, W = WR
   uint32_t sub;      // 1: sub-group bisection (k_msm_subcheck) of failing groups; set by the runtime
 
@@ -186,8 +176,8 @@ struct MsmWork {
   ge_p3 *bk_sum;       // groups x W x H: sums of buckets that fit in one chunk
   ge_p3 *part_first;   // chunks: run that began in an earlier chunk and ends here
   ge_p3 *part_last;    // chunks: run that continues into the next chunk
-  uint32_t *join_b;    // chunks: bucket whose chunk partials k_msm_join joins (the chunk of its last run), or kMsmEmpty;
-                       // TMV_JOIN_LIST: the named buckets packed at the front, *join_count of them
+  uint32_t *join_b;    // chunks: the buckets k_msm_join_list joins from their chunk partials, packed at the front,
+                       // *join_count of them
   uint32_t *join_count;  // groups: [g0] counts the list of the view starting at group g0 (parts of a
                          // launch may run at once); reset by every k_msm_sort, appended by k_msm_accum
   ge_p3 *wpart;        // groups x W x P x 2: (T, U) of each window part
@@ -212,15 +202,6 @@ struct MsmWork {
   uint32_t *fb_count;    // entries in fb_list
   uint32_t *loc_found;   // failing groups whose one bad entry the search named (tmv_metrics)
   uint32_t *fb_list;     // n: work indices verified one by one
-  // groups the located search could not name (two or more bad entries):
-  // their 8-entry sub-groups are checked (k_msm_subcheck) before the fallback
-  uint32_t *l2_list;     // groups
-  uint32_t *l2_count;
-  // bisection of those groups (k_msm_sort<.., 2> .. k_loc_search2): slot 2t /
-  // 2t+1 hold the sums of the first half of the t-th listed group with
-  // weights z / (j+1) z; its entry count (slots << m_log2) in l2e_count
-  fe *l2_T;              // groups x 4 fe (P3Q lanes)
-  uint32_t *l2e_count;
   // key-merged form only (null otherwise)
   uint32_t *wscal;     // n x 8 words: z_e k_e mod l (0 for entries left out)
   uint32_t *bscal;     // groups x 8 words: B scalar of the group
@@ -269,8 +250,6 @@ struct MsmWork {
     w.tabR = nullptr;
     w.fail_T = nullptr;
     w.loc_count = w.fb_count = w.fb_list = w.loc_found = nullptr;
-    w.l2_list = w.l2_count = w.l2e_count = nullptr;
-    w.l2_T = nullptr;
     if (!p.merged) {
       w.fail_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
       w.fail_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
@@ -280,11 +259,8 @@ struct MsmWork {
       w.loc_count = reinterpret_cast<uint32_t *>(b + o);
       w.fb_count = w.loc_count + 1;
       w.loc_found = w.loc_count + 2;
-      w.l2e_count = w.loc_count + 3; o = up(o + 16);
+      o = up(o + 16);
       w.fb_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4ull * n);
-      w.l2_list = reinterpret_cast<uint32_t *>(b + o); o = up(o + 4 * G);
-      w.l2_count = reinterpret_cast<uint32_t *>(b + o); o = up(o + 16);
-      w.l2_T = reinterpret_cast<fe *>(b + o); o = up(o + G * 4 * sizeof(fe));
     }
     if (p.merged) {
       w.wscal = reinterpret_cast<uint32_t *>(b + o); o = up(o + 32ull * n);

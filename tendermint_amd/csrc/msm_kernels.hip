@@ -96,76 +96,33 @@ int read(Kernel k, double *ms, uint64_t *launches) {
 
 namespace {
 
-// word i of an nw-word scalar held in registers (static indexing: no scratch)
-template <int NW>
-__device__ __forceinline__ uint32_t word_at(const uint32_t *s, uint32_t i) {
-  uint32_t x = 0;
-#pragma unroll
-  for (int k = 0; k < NW; k++) x = (i == (uint32_t)k) ? s[k] : x;
-  return x;
-}
-
-// Signed c-bit digit of window w given the previous window's carry; the top
-// window keeps [0, 2^(c-1)] (callers size the window count so it fits).
-template <int NW>
-__device__ __forceinline__ int window_digit(const uint32_t *s, uint32_t w, uint32_t c, bool top, int &carry) {
-  const uint32_t bit = w * c;
-  const uint32_t wi = bit >> 5, sh = bit & 31;
-  const uint64_t x = (uint64_t)word_at<NW>(s, wi) | ((uint64_t)word_at<NW>(s, wi + 1) << 32);
-  int d = (int)((x >> sh) & ((1u << c) - 1)) + carry;
-  if (!top && d >= (1 << (c - 1))) {
-    d -= 1 << c;
-    carry = 1;
-  } else {
-    carry = 0;
-  }
-  return d;
-}
-
 template <int V>
 struct StaticIndex {
   static constexpr int value = V;
 };
 
-// The same digits read window after window: a 64-bit buffer of the next
-// bits, refilled from the scalar's next word once every ~32 / c windows,
-// instead of two run-time word selects per window.  Equal to window_digit
-// for w = 0, 1, 2, ...  TMV_SORT_DIGIT_READER=1: the reader took the
-// scalar's words by pointer and refilled from word_at(s, nxt), a run-time
-// index -- measured neutral (the scalars stayed in scratch: at the bench's
-// size the primary sort took 738 vs 709 us, the located pass's 171 vs 232
-// us, bench 132.0 / 131.4 vs 132.0 / 131.2 M/s; profiles/r04/
-// ab_sort_reader.txt).  =2 (default): the reader owns a copy of the words
-// and shifts them down by one at each refill, so every register index is a
-// compile-time constant (no select chain, no scratch, no s_set_gpr_idx).
-#ifndef TMV_SORT_DIGIT_READER
-#define TMV_SORT_DIGIT_READER 2
-#endif
+// Signed c-bit digits of a scalar read window after window: a 64-bit buffer
+// of the next bits, refilled from the scalar's next word once every ~32 / c
+// windows.  The reader owns a copy of the words and shifts them down by one
+// at each refill, so every register index is a compile-time constant (no
+// select chain, no scratch, no s_set_gpr_idx); the top window keeps
+// [0, 2^(c-1)] (callers size the window count so it fits).  Round 4 measured
+// a reader that refilled through a run-time word index: no faster, the
+// scalars in scratch (profiles/r04/ab_sort_reader.txt).
 template <int NW>
 struct DigitReader {
-#if TMV_SORT_DIGIT_READER == 2
   uint32_t wd[NW];  // the words not yet in buf, lowest first
-#endif
-  uint64_t buf;    // bits [pos, pos + avail) of the scalar, zeros above
+  uint64_t buf;     // bits [pos, pos + avail) of the scalar, zeros above
   uint32_t avail;
-  uint32_t nxt;    // next word to load (=1)
   int carry;
   __device__ __forceinline__ void init(const uint32_t *s) {
-#if TMV_SORT_DIGIT_READER == 2
 #pragma unroll
     for (int k = 0; k < NW; k++) wd[k] = s[k];
     buf = 0;
     avail = 0;
-#else
-    buf = (uint64_t)s[0] | ((uint64_t)(NW > 1 ? s[1] : 0u) << 32);
-    avail = 64;
-    nxt = 2;
-#endif
     carry = 0;
   }
-  __device__ __forceinline__ int next(const uint32_t *s, uint32_t c, bool top) {
-#if TMV_SORT_DIGIT_READER == 2
-    (void)s;
+  __device__ __forceinline__ int next(uint32_t c, bool top) {
     if (avail < c) {  // avail + 32 <= 40: fits
       buf |= (uint64_t)wd[0] << avail;
 #pragma unroll
@@ -176,16 +133,6 @@ struct DigitReader {
     int d = (int)(buf & ((1u << c) - 1)) + carry;
     buf >>= c;
     avail -= c;
-#else
-    int d = (int)(buf & ((1u << c) - 1)) + carry;
-    buf >>= c;
-    avail -= c;
-    if (avail <= 32) {
-      if (nxt < (uint32_t)NW) buf |= (uint64_t)word_at<NW>(s, nxt) << avail;
-      nxt++;
-      avail += 32;
-    }
-#endif
     if (!top && d >= (1 << (c - 1))) {
       d -= 1 << c;
       carry = 1;
@@ -199,20 +146,12 @@ struct DigitReader {
 // For every nonzero digit of a scalar: f(bucket within group, negative).
 template <int NW, typename F>
 __device__ __forceinline__ void for_each_digit(const uint32_t *s, uint32_t windows, const MsmParams &p, F f) {
-#if TMV_SORT_DIGIT_READER
   DigitReader<NW> rd;
   rd.init(s);
   for (uint32_t w = 0; w < windows; w++) {
-    const int d = rd.next(s, p.c, w + 1 == windows);
+    const int d = rd.next(p.c, w + 1 == windows);
     if (d != 0) f(p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1)), d < 0);
   }
-#else
-  int carry = 0;
-  for (uint32_t w = 0; w < windows; w++) {
-    const int d = window_digit<NW>(s, w, p.c, w + 1 == windows, carry);
-    if (d != 0) f(p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1)), d < 0);
-  }
-#endif
 }
 
 __device__ __forceinline__ void p3_add(ge_p3 &a, const ge_p3 &b) {
@@ -229,23 +168,9 @@ __device__ __forceinline__ void p3_dbl(ge_p3 &a) {
   ge_p1p1_to_p3(a, r);
 }
 
-// Bucket b's sum; false if the bucket is empty.  A bucket that fits in one
-// chunk was stored whole by k_msm_accum; a longer one is the run that left
-// its first chunk, the middle chunks and the run that ended in its last.
-__device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &out, uint32_t cnt, uint32_t bs) {
-  if (cnt == 0) return false;
-  const uint32_t t0 = bs / L, t1 = (bs + cnt - 1) / L;
-  if (t0 == t1) {
-    out = mw.bk_sum[b];
-    return true;
-  }
-  out = mw.part_last[t0];
-  for (uint32_t t = t0 + 1; t < t1; t++) p3_add(out, mw.part_last[t]);
-  p3_add(out, mw.part_first[t1]);
-  return true;
-}
-
 }  // namespace
+
+// One workgroup per group of m entries}  // namespace
 
 // One workgroup per group of m entries: z_e, z_e k_e mod l, sum z_e s_e mod l
 // (the B scalar), then a counting sort of the (window, |digit|) bucket entries
@@ -256,9 +181,8 @@ __device__ bool bucket_value(const MsmWork &mw, uint32_t L, uint32_t b, ge_p3 &o
 // group into slot f with every weight multiplied by (j + 1), j the entry's
 // index in its group, so the same bucket stages compute
 // T'_f = sum (j+1) z_j Delta_j (z_j (j+1) < 2^(128 + m_log2): p.WL() R
-// windows).  LOC = 2 (bisection, k_loc_search2): slot s holds the first half
-// of group fail_list[l2_list[s / 2]], weights z (even s) or (j + 1) z (odd).
-template <bool SR, bool KM, int BS = kMsmSortBlock, int LOC = 0>
+// windows).
+template <bool SR, bool KM, int BS = kMsmSortBlock, bool LOC = false>
 __global__ void __launch_bounds__(BS)
 k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, const uint32_t *count_ptr, uint32_t n,
            Ed25519Work w, MsmWork mw, MsmParams p, MsmSeed seed, const fe *__restrict__ btab_q, int aligned,
@@ -268,25 +192,18 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   const uint32_t cnt = entry_count(count_ptr, n);
   const uint32_t tid = threadIdx.x;
   uint32_t g = blockIdx.x;  // LOC: the slot; the group is fail_list[slot]
-  if (kMsmJoinList && g == 0 && tid == 0) *mw.join_count = 0;  // the next k_msm_accum appends its joins
-  if (LOC == 2) {
-    const uint32_t ns = min(2u * *mw.l2_count, p.groups);
-    if (g == 0 && tid == 0) *mw.l2e_count = ns << p.m_log2;  // the bucket stages' entry count
-    if (g >= ns) return;  // block-uniform
-  }
-  if (LOC == 1) {
+  if (g == 0 && tid == 0) *mw.join_count = 0;  // the next k_msm_accum appends its joins
+  if (LOC) {
     const uint32_t nf = *mw.fail_count;
     if (g == 0 && tid == 0) {
       *mw.loc_count = nf << p.m_log2;  // the bucket stages' entry count: nf slots
       *mw.fb_count = 0;                // k_loc_search appends the entries left to verify
       *mw.loc_found = 0;
-      *mw.l2_count = 0;                // and the groups it could not name
     }
     if (g >= nf) return;  // block-uniform
   }
   const uint32_t slot = g;
-  if (LOC == 1) g = mw.fail_list[slot];
-  if (LOC == 2) g = mw.fail_list[mw.l2_list[slot >> 1]];
+  if (LOC) g = mw.fail_list[slot];
   const uint32_t e0 = g << p.m_log2;
   if (!KM && !LOC && g == 0 && tid == 0) {  // B as a Niels point (btab_q entry 0 = (ymx, ypx, xy2d, 1) of 1*B)
     niels_pt bp;
@@ -298,7 +215,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     if (mw.fail_count) *mw.fail_count = 0;  // k_msm_horner appends the failing groups
   }
   if (e0 >= cnt) return;  // block-uniform
-  const uint32_t mlive = min(LOC == 2 ? p.m() >> 1 : p.m(), cnt - e0);
+  const uint32_t mlive = min(p.m(), cnt - e0);
   const uint32_t WH = p.W * p.H;
   uint32_t *hist = smem;                       // WH counters, then cursors
   uint32_t *red = smem + WH;                   // BS x 9 words
@@ -363,7 +280,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
     sc_mul_mod(wv[r], z[r], 4, k);
     if (LOC) {  // weights times (j + 1): z (j + 1) exactly, z k (j + 1) mod l
-      const uint32_t jj = (LOC == 2 && !(slot & 1)) ? 1u : j + 1;
+      const uint32_t jj = j + 1;
       uint64_t cy = 0;
 #pragma unroll
       for (int t = 0; t < 4; t++) {
@@ -490,7 +407,6 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   uint32_t *ent_bk = mw.ent_bk + gbase;
   const uint32_t wcap = 2 * p.m() + 1;  // entries one window can hold: m R + m A digits + B
   uint32_t *st_pt = scan + BS + 1, *st_bk = st_pt + wcap;
-#if TMV_SORT_DIGIT_READER
   DigitReader<ZW> rz[R];
   DigitReader<8> rw[R], rb;
 #pragma unroll
@@ -499,11 +415,6 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     rw[r].init(wv[r]);
   }
   rb.init(bsc);
-#else
-  int cz[R], cw[R], cb = 0;  // per-scalar digit carries, window to window
-#pragma unroll
-  for (int r = 0; r < R; r++) cz[r] = cw[r] = 0;
-#endif
   const uint32_t total = scan[BS];
   for (uint32_t w = 0; w < p.W; w++) {
     const uint32_t wbeg = hist[p.bucket(w, 0)];
@@ -514,11 +425,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       if (!live[r]) continue;
       const uint32_t e = e0 + tid + r * BS;
       if (w < WRz) {
-#if TMV_SORT_DIGIT_READER
-        const int d = rz[r].next(z[r], p.c, w + 1 == WRz);
-#else
-        const int d = window_digit<ZW>(z[r], w, p.c, w + 1 == WRz, cz[r]);
-#endif
+        const int d = rz[r].next(p.c, w + 1 == WRz);
         if (d != 0) {
           const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
           const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;  // < cap: checked above
@@ -527,11 +434,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
         }
       }
       if (!KM) {
-#if TMV_SORT_DIGIT_READER
-        const int d = rw[r].next(wv[r], p.c, w + 1 == p.W);
-#else
-        const int d = window_digit<8>(wv[r], w, p.c, w + 1 == p.W, cw[r]);
-#endif
+        const int d = rw[r].next(p.c, w + 1 == p.W);
         if (d != 0) {
           const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
           const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;
@@ -541,11 +444,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
       }
     }
     if (!KM && tid == 0) {
-#if TMV_SORT_DIGIT_READER
-      const int d = rb.next(bsc, p.c, w + 1 == p.W);
-#else
-      const int d = window_digit<8>(bsc, w, p.c, w + 1 == p.W, cb);
-#endif
+      const int d = rb.next(p.c, w + 1 == p.W);
       if (d != 0) {
         const uint32_t bk = p.bucket(w, (uint32_t)((d < 0 ? -d : d) - 1));
         const uint32_t pos = atomicAdd(&hist[bk], 1u) - wbeg;
@@ -562,6 +461,17 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
   for (uint32_t t = total + tid; t < p.cap; t += BS) ent_bk[t] = kMsmEmpty;
 }
 
+#ifdef TMV_CHECKS
+// Test build (-DTMV_CHECKS, tools/build_checks.sh; tests/test_gpu_checks.py
+// reads these through tmv_internal_checks): joins named by k_msm_accum, joins
+// k_msm_join_list found in its list, and buckets with entries whose sum was
+// never written (k_check_buckets).  Round 5's lost-join race -- a part's sort
+// resetting the list counter under another part's appends -- makes the
+// first two differ and the third non-zero, where the product fails the
+// groups closed (Z != 0 verdicts) and pays a fallback.
+__device__ uint32_t g_joins_named, g_joins_done, g_buckets_unwritten;
+#endif
+
 // One lane per chunk of L sorted entries: sums each run of equal
 // bucket ids with mixed additions.  A run that is the whole bucket goes to
 // bk_sum.  A bucket cut by chunk edges: the lane whose run opens it holds
@@ -572,31 +482,16 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
 // adds it after the loop and stores the whole bucket: no partials leave the
 // wave.  The rest (a wave's edge, buckets over three or more chunks) keep
 // their runs in part_last / part_first and name the bucket in join_b at the
-// chunk of its last run, for k_msm_join.
-// Waves per SIMD k_msm_accum is compiled for (1 = the compiler's choice,
-// 145 VGPRs, 3 waves).  4 (128 VGPRs, 26 spilled) measured slower, 119.4-120.5
-// vs 123.7-124.9 M/s (profiles/r03/ab_register_budget.txt).
-#ifndef TMV_ACCUM_WAVES
-#define TMV_ACCUM_WAVES 1
-#endif
-// How the lane reads its chunk's bucket / point words (A/B, profiles/r04/
-// ab_accum_r04m.txt, per-launch k_msm_accum at the bench's size relative to
-// the unchanged k_msm_wpart of the same run): TMV_ACCUM_REGIDX=1 (default)
-// loads them as four uint4 into register arrays, which the rolled loop
-// indexes by its wave-uniform counter (v_movrels, two VALU per entry, yet
-// the fastest: 2.44x the running sums' time); 0 reads each entry's words
-// from memory one entry ahead (no selects, 2.47x); TMV_ACCUM_PREFETCH=1 also
-// loads the next entry's Niels point during this entry's addition (163
-// VGPRs, still 3 waves / SIMD, 2.60x).  The accumulation is not purely
-// issue-bound: the gathers' latency, not the selects, is what the loop waits on.
-#ifndef TMV_ACCUM_REGIDX
-#define TMV_ACCUM_REGIDX 1
-#endif
-#ifndef TMV_ACCUM_PREFETCH
-#define TMV_ACCUM_PREFETCH 0
-#endif
+// chunk of its last run, for k_msm_join_list.
+// Register budget: the compiler's choice (145 VGPRs, 3 waves per SIMD); 4
+// waves (128 VGPRs, 26 spilled) measured slower (profiles/r03/
+// ab_register_budget.txt).  The chunk's bucket / point words are loaded as
+// uint4 into register arrays that the rolled loop indexes by its wave-uniform
+// counter (v_movrels): faster than reading them entry by entry, or than also
+// prefetching the next Niels point (profiles/r04/ab_accum_r04m.txt) -- the
+// gathers' latency, not the selects, is what the loop waits on.
 template <int L>
-__global__ void __launch_bounds__(256, TMV_ACCUM_WAVES)
+__global__ void __launch_bounds__(256)
 k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   __shared__ ge_p3 first_run[256];  // a lane's first run, joined by its wave neighbour (40 KB)
   // blocks b and b + 8 share an XCD (round-robin dispatch): give each XCD a
@@ -613,7 +508,6 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   if (g >= live_groups) return;
   const uint32_t base = t * L;
   const uint32_t lane = threadIdx.x & 63;
-#if TMV_ACCUM_REGIDX
   // the chunk's words in registers: the loop below is not unrolled (L copies
   // of a 1,400-instruction body), so bk[q] / pt[q] are read with v_movrels
   // under s_set_gpr_idx (q is wave-uniform)
@@ -628,19 +522,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       pt[4 * q] = y.x; pt[4 * q + 1] = y.y; pt[4 * q + 2] = y.z; pt[4 * q + 3] = y.w;
     }
   }
-#define TMV_BK(q) bk[q]
-#define TMV_PT(q) pt[q]
-#else
-  // the chunk's words read entry by entry (L1 / L2 hits after the first):
-  // no register array indexed by the rolled loop's counter
-  const uint32_t *bkp = mw.ent_bk + base, *ptp = mw.ent_pt + base;
-#define TMV_BK(q) bkp[q]
-#define TMV_PT(q) ptp[q]
-#endif
-  if (TMV_BK(0) == kMsmEmpty) {  // padding: nothing to join (the scan form of k_msm_join reads every live chunk's word)
-    if (kMsmJoin && !kMsmJoinList) mw.join_b[t] = kMsmEmpty;
-    return;
-  }
+  if (bk[0] == kMsmEmpty) return;  // padding: nothing to sum or join
   uint32_t join = kMsmEmpty;  // this chunk's join_b
   auto flush = [&](uint32_t b, uint32_t rs, uint32_t re, const ge_p3 &acc) {
     const uint32_t bs = mw.bk_start[b], be = bs + mw.bk_cnt[b];
@@ -648,7 +530,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       mw.bk_sum[b] = acc;
     } else if (re == base + L && re < be) {
       mw.part_last[t] = acc;  // (the open run at the chunk's end: see below)
-    } else if (kMsmJoin && lane != 0 && bs >= base - L) {  // ends here, opened by the previous lane
+    } else if (lane != 0 && bs >= base - L) {  // ends here, opened by the previous lane
       first_run[threadIdx.x] = acc;
     } else {
       mw.part_first[t] = acc;
@@ -658,7 +540,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   // every lane's first run starts at entry 0: take that point as the
   // accumulator (one multiply) instead of adding it to the identity (seven)
   ge_p3 acc;
-  const uint32_t pt0 = TMV_PT(0);
+  const uint32_t pt0 = pt[0];
   if (kNielsPer == 2) {  // the signed point's own slot
     const niels_pt P = mw.pts[pt0];
     niels_to_p3(acc, P.ypx, P.ymx);
@@ -667,41 +549,17 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     const bool neg = pt0 & 1;
     niels_to_p3(acc, neg ? P.ymx : P.ypx, neg ? P.ypx : P.ymx);
   }
-  uint32_t cur = TMV_BK(0), rs = base;
+  uint32_t cur = bk[0], rs = base;
   uint32_t j = 1;
   bool more = true;
-#if TMV_ACCUM_PREFETCH
-  // software pipeline: the next entry's Niels point is loaded while this
-  // entry's addition runs, its bucket / point words two entries ahead (the
-  // point's address needs them); padding entries load nothing
-  auto slot_of = [](uint32_t ptw) { return kNielsPer == 2 ? ptw : ptw >> 1; };
-  uint32_t b1 = TMV_BK(1), p1 = TMV_PT(1);
-  niels_pt P1;
-  if (b1 != kMsmEmpty) P1 = mw.pts[slot_of(p1)];
-  uint32_t b2 = L > 2 ? TMV_BK(2) : kMsmEmpty, p2 = L > 2 ? TMV_PT(2) : 0u;
-#pragma unroll
-  for (int q = 1; q < L; q++) {
-    const uint32_t bq = b1, pq = p1;
-    const niels_pt P = P1;
-    if (q + 1 < L) {
-      b1 = b2;
-      p1 = p2;
-      if (b1 != kMsmEmpty) P1 = mw.pts[slot_of(p1)];
-      if (q + 2 < L) {
-        b2 = TMV_BK(q + 2);
-        p2 = TMV_PT(q + 2);
-      }
-    }
-#else
-  uint32_t bn = TMV_BK(1), pn = TMV_PT(1);  // loaded one entry ahead
+  uint32_t bn = bk[1], pn = pt[1];  // loaded one entry ahead
 #pragma unroll
   for (int q = 1; q < L; q++) {
     const uint32_t bq = bn, pq = pn;
     if (q + 1 < L) {
-      bn = TMV_BK(q + 1);
-      pn = TMV_PT(q + 1);
+      bn = bk[q + 1];
+      pn = pt[q + 1];
     }
-#endif
     more = more && bq != kMsmEmpty;  // padding only follows the last bucket
     if (!more) continue;
     if (bq != cur) {
@@ -711,9 +569,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
       rs = base + q;
     }
     ge_precomp np;
-#if !TMV_ACCUM_PREFETCH
     const niels_pt P = mw.pts[kNielsPer == 2 ? pq : pq >> 1];
-#endif
     if (kNielsPer == 2) {
       np.ypx = P.ypx;
       np.ymx = P.ymx;
@@ -734,7 +590,7 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t bs = mw.bk_start[cur], be = bs + mw.bk_cnt[cur];
   const uint32_t re = base + j;
   const bool open = re == base + L && re < be;
-  const bool join_next = kMsmJoin && open && bs >= base && lane != 63 && be <= base + 2 * L;
+  const bool join_next = open && bs >= base && lane != 63 && be <= base + 2 * L;
   if (!open) flush(cur, rs, re, acc);
   else if (!join_next) mw.part_last[t] = acc;
   // the first runs are in LDS: wave-local exchange, no workgroup barrier
@@ -746,41 +602,26 @@ k_msm_accum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
     p3_add(acc, first_run[threadIdx.x + 1]);
     mw.bk_sum[cur] = acc;
   }
-  if (kMsmJoin && kMsmJoinList) {
-    // append this wave's joins to the launch's list: one atomic per wave, by
-    // its lowest joining lane
-    const uint64_t jm = __ballot(join != kMsmEmpty);
-    if (jm) {  // wave-uniform
-      const int leader = __ffsll((unsigned long long)jm) - 1;
-      uint32_t jb = 0;
-      if ((int)lane == leader) jb = atomicAdd(mw.join_count, (uint32_t)__popcll(jm));
-      jb = __shfl(jb, leader);
-      if (join != kMsmEmpty) mw.join_b[jb + __popcll(jm & ((1ull << lane) - 1))] = join;
-    }
-  } else if (kMsmJoin) {
-    mw.join_b[t] = join;
+  // append this wave's joins to the launch's list: one atomic per wave, by
+  // its lowest joining lane
+  const uint64_t jm = __ballot(join != kMsmEmpty);
+  if (jm) {  // wave-uniform
+    const int leader = __ffsll((unsigned long long)jm) - 1;
+    uint32_t jb = 0;
+    if ((int)lane == leader) jb = atomicAdd(mw.join_count, (uint32_t)__popcll(jm));
+    jb = __shfl(jb, leader);
+    if (join != kMsmEmpty) mw.join_b[jb + __popcll(jm & ((1ull << lane) - 1))] = join;
+#ifdef TMV_CHECKS
+    if ((int)lane == leader) atomicAdd(&g_joins_named, (uint32_t)__popcll(jm));
+#endif
   }
 }
-#undef TMV_BK
-#undef TMV_PT
 
-// The buckets accumulation could not join inside a wave (about 1% of the
-// chunks name one): bucket value from its chunk partials (part_last of every
-// chunk but its last, part_first of the last).  Each wave scans
-// kJoinScan x 64 chunks' join_b words (coalesced), gathers the named
-// buckets into a wave-local LDS list and joins them 64 at a time, so the
-// grid is small and no wave walks the join for one lane.  The join is
-// latency-bound (its waves wait on the partials' loads), so more, shorter
-// waves pay: 8 x 64 chunks per wave, k_msm_join per launch at 1M / 2.56M
-// 150 / 338 us vs 171 / 345 (16), 197 / 357 (32), 245 / 386 (64), 216 /
-// 483 (4) (profiles/r05/ab_join_scan.txt).
-#ifndef TMV_JOIN_SCAN
-#define TMV_JOIN_SCAN 8
-#endif
-constexpr uint32_t kJoinScan = TMV_JOIN_SCAN;
-// List form (TMV_JOIN_LIST=1): k_msm_accum appends the named buckets to a
-// packed list (one atomic per wave), and k_msm_join strides over it with
-// every lane busy, instead of scanning every chunk's word.
+// The buckets k_msm_accum could not join inside a wave (~7% of the chunks at
+// the bench's shape): k_msm_accum appended them to a packed list (one atomic
+// per wave), and this kernel strides over it with every lane busy.  (Rounds
+// 2-5 scanned one join word per chunk instead: 2.56M join 577 -> 381 us per
+// launch with the list, profiles/r05/ab_join_list.txt.)
 __global__ void __launch_bounds__(256)
 k_msm_join_list(MsmWork mw, MsmParams p) {
   const uint32_t cnt = *mw.join_count;
@@ -798,58 +639,16 @@ k_msm_join_list(MsmWork mw, MsmParams p) {
     const ge_p3 q = mw.part_first[t1];
     p3_add(acc, q);
     mw.bk_sum[b] = acc;
-  }
-}
-__global__ void __launch_bounds__(256)
-k_msm_join(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
-  __shared__ uint32_t list[4][kJoinScan * 64];
-  const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
-  const uint32_t chunks = live_groups * p.chunks_per_group();
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t c0 = (blockIdx.x * 4 + wv) * kJoinScan * 64;
-  if (c0 >= chunks) return;  // wave-uniform
-  uint32_t cnt = 0;
-  for (uint32_t k = 0; k < kJoinScan; k++) {
-    const uint32_t t = c0 + k * 64 + lane;
-    const uint32_t b = t < chunks ? mw.join_b[t] : kMsmEmpty;
-    const uint64_t m = __ballot(b != kMsmEmpty);
-    if (b != kMsmEmpty) list[wv][cnt + __popcll(m & ((1ull << lane) - 1))] = b;
-    cnt += __popcll(m);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (uint32_t i = lane; i < cnt; i += 64) {
-    const uint32_t b = list[wv][i];
-    ge_p3 B;
-    bucket_value(mw, p.L, b, B, mw.bk_cnt[b], mw.bk_start[b]);
-    mw.bk_sum[b] = B;
+#ifdef TMV_CHECKS
+    atomicAdd(&g_joins_done, 1u);
+#endif
   }
 }
 
-// Waves per SIMD the running-sum kernel is compiled for (register budget;
-// 1 = the compiler's choice, 178 VGPRs, 2 waves).  3 (168 VGPRs, 2 spilled)
-// measured the same, 123.8-124.9 vs 123.7-124.9 M/s
-// (profiles/r03/ab_register_budget.txt).
-#ifndef TMV_WPART_WAVES
-#define TMV_WPART_WAVES 1
-#endif
-// Running sums with the next bucket's sum loaded one step ahead (219
-// VGPRs, still 2 waves): measured no faster -- running sums / accumulation
-// time 0.419 vs 0.413 without, bench 127.7 / 129.1 vs 129.4 / 129.4 M/s
-// (profiles/r04/ab_wpart_prefetch.txt); the kernel waits on its addition
-// chains, not on the bucket loads.  Off by default.
-#ifndef TMV_WPART_PREFETCH
-#define TMV_WPART_PREFETCH 0
-#endif
-// One-lane running sums with U held in cached form only (P = 1): U += B
-// adds the P3 bucket sum to the cached U and converts the result straight
-// back to cached, T += U takes that cached U -- 17 multiplications a bucket
-// instead of 18 (B's own cached conversion goes away).
-#ifndef TMV_WPART_CACHED_U
-#define TMV_WPART_CACHED_U 1
-#endif
+// Running sums: register budget the compiler's choice (178 VGPRs, 2 waves;
+// 3 waves measured the same, profiles/r03/ab_register_budget.txt); loading
+// the next bucket's sum one step ahead measured no faster (the kernel waits
+// on its addition chains, profiles/r04/ab_wpart_prefetch.txt).
 
 // A window sum as k_msm_horner reads it: the top window (Horner's start) as a
 // P3Q point (X, Y, Z, T), every other window already in CachedQ order
@@ -874,7 +673,11 @@ __device__ __forceinline__ void store_window_sum(ge_p3 *dst, const ge_p3 &S, boo
 
 // Window parts: lane (g, w, q) sums buckets [q s, (q+1) s) of window w with
 // the running-sum trick: T = sum_i (i+1) B_{qs+i}, U = sum_i B_{qs+i}.
-__global__ void __launch_bounds__(256, TMV_WPART_WAVES)
+// Buckets are whole (joined by k_msm_accum or k_msm_join_list).  One lane per
+// window (P = 1) keeps U in cached form only: U += B adds the P3 bucket sum
+// to the cached U and converts the result straight back, T += U takes that
+// cached U -- 17 multiplications a bucket instead of 18.
+__global__ void __launch_bounds__(256)
 k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t per_group = p.W * p.P;
@@ -883,40 +686,10 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   const uint32_t r = t - g * per_group, wdx = r / p.P, part = r % p.P;
   const uint32_t s = p.H / p.P;
   ge_p3 U, T;
-#if TMV_WPART_CACHED_U
-  ge_cached Uc;  // P = 1: U's only form
-#endif
   bool u_set = false, t_set = false;
   const uint32_t gb = g * p.W * p.H, i0 = part * s;
-#if TMV_WPART_PREFETCH
-  if (kMsmJoin) {
-    // whole buckets only: the next bucket's sum is loaded during this
-    // step's two additions, its count one step earlier still
-    uint32_t c_cur = mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 1)];
-    ge_p3 Bn;
-    if (c_cur) Bn = mw.bk_sum[gb + p.bucket(wdx, i0 + s - 1)];
-    uint32_t c_next = s > 1 ? mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 2)] : 0u;
-    for (int i = (int)s - 1; i >= 0; i--) {
-      const ge_p3 B = Bn;
-      const bool nz = c_cur != 0;
-      if (i > 0) {
-        c_cur = c_next;
-        if (c_cur) Bn = mw.bk_sum[gb + p.bucket(wdx, i0 + (uint32_t)i - 1)];
-        if (i > 1) c_next = mw.bk_cnt[gb + p.bucket(wdx, i0 + (uint32_t)i - 2)];
-      }
-      if (nz) {
-        if (u_set) p3_add(U, B);
-        else { U = B; u_set = true; }
-      }
-      if (u_set) {
-        if (t_set) p3_add(T, U);
-        else { T = U; t_set = true; }
-      }
-    }
-  } else
-#endif
-#if TMV_WPART_CACHED_U
-  if (kMsmJoin && p.P == 1) {  // U only as the cached addend; T starts as the first B
+  if (p.P == 1) {  // U only as the cached addend; T starts as the first B
+    ge_cached Uc;
     uint32_t cnt = mw.bk_cnt[gb + p.bucket(wdx, s - 1)];
     for (int i = (int)s - 1; i >= 0; i--) {
       const uint32_t c_i = cnt;
@@ -939,36 +712,23 @@ k_msm_wpart(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
         ge_p1p1_to_p3(T, rr);
       }
     }
-  } else
-#endif
-  {
-  // the next bucket's count and start are loaded one iteration ahead, so
-  // only its point load is exposed
-  uint32_t cnt = mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 1)], bst = mw.bk_start[gb + p.bucket(wdx, i0 + s - 1)];
-  for (int i = (int)s - 1; i >= 0; i--) {
-    ge_p3 B;
-    const uint32_t c_i = cnt, s_i = bst;
-    if (i > 0) {
-      const uint32_t bn = gb + p.bucket(wdx, i0 + (uint32_t)i - 1);
-      cnt = mw.bk_cnt[bn];
-      bst = mw.bk_start[bn];
+  } else {
+    // the next bucket's count is loaded one iteration ahead, so only its
+    // point load is exposed
+    uint32_t cnt = mw.bk_cnt[gb + p.bucket(wdx, i0 + s - 1)];
+    for (int i = (int)s - 1; i >= 0; i--) {
+      const uint32_t c_i = cnt;
+      if (i > 0) cnt = mw.bk_cnt[gb + p.bucket(wdx, i0 + (uint32_t)i - 1)];
+      if (c_i) {
+        const ge_p3 B = mw.bk_sum[gb + p.bucket(wdx, i0 + (uint32_t)i)];
+        if (u_set) p3_add(U, B);
+        else { U = B; u_set = true; }
+      }
+      if (u_set) {
+        if (t_set) p3_add(T, U);
+        else { T = U; t_set = true; }
+      }
     }
-    const uint32_t bb = gb + p.bucket(wdx, i0 + (uint32_t)i);
-    bool nz = c_i != 0;
-    if (kMsmJoin) {
-      if (nz) B = mw.bk_sum[bb];  // whole: joined by k_msm_accum or k_msm_join
-    } else {
-      nz = bucket_value(mw, p.L, bb, B, c_i, s_i);
-    }
-    if (nz) {
-      if (u_set) p3_add(U, B);
-      else { U = B; u_set = true; }
-    }
-    if (u_set) {
-      if (t_set) p3_add(T, U);
-      else { T = U; t_set = true; }
-    }
-  }
   }
   if (!u_set) ge_p3_identity(U);
   if (!t_set) ge_p3_identity(T);
@@ -1003,73 +763,13 @@ k_msm_wsum(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   store_window_sum(&mw.wsum[t], acc, t - g * p.W == p.W - 1);
 }
 
-// Quad form of k_msm_wpart (P = 1, buckets joined): one quad per (group,
-// window), lane c holding coordinate c (quad.h), 64 windows per workgroup.
-// U = sum_{j >= i} B_j is only ever an addend, so it is kept in CachedQ form
-// and the bucket sum B_i is the P3Q operand of its addition: a step costs
-// each lane five multiplications (U's addition, its P3 and cached forms, T's
-// addition and P3 form) where the one-lane form costs one lane 18, so a
-// window's 2 H-addition chain is ~3.5x shorter; empty buckets add the
-// identity (the formulas are complete), so every quad runs the same steps.
-// The next bucket's count and sum are loaded one step ahead.
-__global__ void __launch_bounds__(256)
-k_msm_wpart_quad(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
-  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;  // (group, window) row
-  const uint32_t g = t / p.W;
-  if (g >= p.groups || (g << p.m_log2) >= entry_count(count_ptr, n)) return;  // quad-uniform
-  const uint32_t wdx = t - g * p.W;
-  const int c = quad::lane4();
-  const uint32_t b0 = g * p.W * p.H + p.bucket(wdx, 0);
-  fe T, Uc, U, B, Bn, r;
-  quad::p3_identity(T);
-  quad::cached_identity(Uc);
-  uint32_t cnt = mw.bk_cnt[b0 + p.H - 1];
-  if (cnt) Bn = reinterpret_cast<const fe *>(&mw.bk_sum[b0 + p.H - 1])[c];
-  else quad::p3_identity(Bn);
-  for (int i = (int)p.H - 1; i >= 0; i--) {
-    B = Bn;
-    if (i > 0) {
-      cnt = mw.bk_cnt[b0 + i - 1];
-      if (cnt) Bn = reinterpret_cast<const fe *>(&mw.bk_sum[b0 + i - 1])[c];
-      else quad::p3_identity(Bn);
-    }
-    quad::add(r, B, Uc);  // U += B_i
-    quad::p1p1_to_p3(U, r);
-    quad::to_cached(Uc, U);
-    quad::add(r, T, Uc);  // T += U
-    quad::p1p1_to_p3(T, r);
-  }
-  fe *dst = reinterpret_cast<fe *>(&mw.wpart[2ull * t]);
-  if (wdx == p.W - 1) {  // Horner's start: P3Q
-    dst[c] = T;
-  } else {  // CachedQ, as store_window_sum
-    quad::to_cached(U, T);
-    dst[c] = U;
-  }
-}
-
-// Rows of (group, window) up to which the running sums run in quad form
-// (TMV_WPART_QUAD_ROWS; default 0 = never).  Measured and not kept: 125k
-// launch 222 -> 255 us for the running sums (rocprof), the C2 bench 129.9
-// -> 125.3 M/s (profiles/r04/ab_kernels_r04k.txt) -- the quad form does ~10%
-// more lane work per step, and at these sizes the one-lane kernel is no
-// longer chain-bound.
-static uint32_t wpart_quad_rows() {
-  static const uint32_t v = [] {
-    const char *e = getenv("TMV_WPART_QUAD_ROWS");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-  }();
-  return v;
-}
-
 // Group verdicts: one quad per group (lane c holds coordinate c), 16 groups
 // per wave; T_g = sum_w 2^(c w) S_w by Horner, then
 //   ed25519: [8] T_g == O;  sr25519: T_g is the Ristretto identity.
 // A failing group's T_g goes to mw.fail_T at its place in the failing list.
 // LOC: the same Horner over the locate MSM's slots (count_ptr = loc_count),
-// T'_f to mw.fail_T, no verdict; LOC = 2: the bisection slots' sums to
-// mw.l2_T (count_ptr = l2e_count).
-template <bool SR, bool KM, int LOC>
+// T'_f to mw.fail_T, no verdict.
+template <bool SR, bool KM, bool LOC>
 __device__ __forceinline__ void horner_block(uint32_t bx, const uint32_t *count_ptr, uint32_t n, MsmWork mw,
                                              const MsmParams &p, const uint32_t *__restrict__ group_run0,
                                              uint32_t n_runs) {
@@ -1104,10 +804,7 @@ __device__ __forceinline__ void horner_block(uint32_t bx, const uint32_t *count_
     }
   }
   if (LOC) {
-    if (live) {
-      if (LOC == 2) mw.l2_T[4ull * g + c] = acc;
-      else mw.fail_T[8ull * g + 4 + c] = acc;
-    }
+    if (live) mw.fail_T[8ull * g + 4 + c] = acc;
     return;
   }
   bool ok;
@@ -1131,7 +828,7 @@ __device__ __forceinline__ void horner_block(uint32_t bx, const uint32_t *count_
   if (f >= 0 && mw.fail_T) mw.fail_T[8ull * f + c] = acc;
 }
 
-template <bool SR, bool KM, int LOC = 0>
+template <bool SR, bool KM, bool LOC = false>
 __global__ void __launch_bounds__(64)
 k_msm_horner(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, const uint32_t *__restrict__ group_run0,
              uint32_t n_runs) {
@@ -1151,7 +848,7 @@ k_msm_horner_helped(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams
                     uint32_t hblocks) {
   if (blockIdx.x < hblocks) {  // block-uniform
     __builtin_amdgcn_s_setprio(3);
-    horner_block<SR, false, 0>(blockIdx.x, count_ptr, n, mw, p, nullptr, 0u);
+    horner_block<SR, false, false>(blockIdx.x, count_ptr, n, mw, p, nullptr, 0u);
     return;
   }
   const uint32_t e = (blockIdx.x - hblocks) * 64 + threadIdx.x;
@@ -1168,13 +865,6 @@ k_msm_horner_helped(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams
   hd[2] = make_uint4((fast ? 1u : 0u) | (neg ? 2u : 0u), 0u, 0u, 0u);
 }
 
-// TMV_HORNER_HELP=0: the plain Horner, and the fallback reduces in its quads
-// (read at every launch, for A/B).
-static bool horner_help() {
-  const char *e = getenv("TMV_HORNER_HELP");
-  return !(e && !strcmp(e, "0"));
-}
-
 // Located fallback, search stage: one wave per failing group (slot f).  With
 // M = [8] T_f and M' = [8] T'_f (sr25519: T and T' themselves, compared as
 // Ristretto points), the group holds exactly one entry j whose term is not
@@ -1186,7 +876,7 @@ static bool horner_help() {
 // pre-check status); otherwise every entry of the group is.
 template <bool SR>
 __global__ void __launch_bounds__(64)
-k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, int sub2) {
+k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
   __shared__ int s_cnt, s_j;
   __shared__ uint32_t s_base;
   const uint32_t f = blockIdx.x;
@@ -1243,137 +933,9 @@ k_loc_search(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p, int
     }
     return;
   }
-  if (sub2 == 1) {  // two or more bad entries: its sub-groups are checked next
-    if (threadIdx.x == 0) mw.l2_list[atomicAdd(mw.l2_count, 1u)] = mw.fail_list[f];
-    return;
-  }
-  if (sub2 == 2 && !ovf) {  // two or more bad entries: bisected next (k_loc_search2)
-    if (threadIdx.x == 0) mw.l2_list[atomicAdd(mw.l2_count, 1u)] = f;
-    return;
-  }
   if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < mlive; t += 64) mw.fb_list[s_base + t] = e0 + t;
-}
-
-// Bisection of the groups k_loc_search could not name (two or more bad
-// entries; ~9% of C2's failing groups of 128, each of which cost 128
-// one-by-one verifications): one wave per listed group t.  The bisection
-// MSM gave the first half's sums T1 = sum_{j < m/2} z_j Delta_j (slot 2t)
-// and T1' = sum_{j < m/2} (j+1) z_j Delta_j (slot 2t + 1); the second half's
-// are T - T1 and T' - T1' (the group's own sums from k_msm_horner and the
-// located pass).  Per half: [8] T_h == O (sr25519: the Ristretto identity) --
-// no bad entry, every entry keeps its pre-check status; else the search of
-// k_loc_search on (T_h, T_h') names its one bad entry, or, with two or more,
-// every entry of the half is verified one by one.  Two bad entries in
-// different halves (about half of such groups) cost two verifications
-// instead of 128, in one half 64.
-template <bool SR>
-__global__ void __launch_bounds__(64)
-k_loc_search2(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
-  __shared__ int s_cnt, s_j;
-  __shared__ uint32_t s_base;
-  const uint32_t t = blockIdx.x;
-  const uint32_t nl2 = *mw.l2_count;
-  if (t >= nl2) return;  // block-uniform
-  const uint32_t f = mw.l2_list[t];
-  const uint32_t m = p.m(), half = m >> 1;
-  const uint32_t e0 = mw.fail_list[f] << p.m_log2;
-  const uint32_t mlive = min(m, entry_count(count_ptr, n) - e0);
-  const uint32_t ns = min(2u * nl2, p.groups);
-  const int c = (int)(threadIdx.x & 3), q = (int)(threadIdx.x >> 2);
-  // slots past the workspace's capacity (more listed groups than half the
-  // groups) or an overflowed sort: every entry of the group one by one
-  if (2 * t + 1 >= ns || mw.sort_ovf[p.groups + 2 * t] || mw.sort_ovf[p.groups + 2 * t + 1]) {  // block-uniform
-    if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, mlive);
-    __syncthreads();
-    for (uint32_t u = threadIdx.x; u < mlive; u += 64) mw.fb_list[s_base + u] = e0 + u;
-    return;
-  }
-  const fe T = mw.fail_T[8ull * f + c], Tp = mw.fail_T[8ull * f + 4 + c];
-  const fe A = mw.l2_T[4ull * (2 * t) + c], Ap = mw.l2_T[4ull * (2 * t + 1) + c];
-  fe Bh, Bp, nc, r;
-  quad::to_cached(nc, A);  // second half: T - T1, T' - T1'
-  quad::cached_cneg(nc, true);
-  quad::add(r, T, nc);
-  quad::p1p1_to_p3(Bh, r);
-  quad::to_cached(nc, Ap);
-  quad::cached_cneg(nc, true);
-  quad::add(r, Tp, nc);
-  quad::p1p1_to_p3(Bp, r);
-  for (int h = 0; h < 2; h++) {
-    const uint32_t lo = (uint32_t)h * half, hi = min(lo + half, mlive);
-    if (lo >= hi) break;  // block-uniform (a short last group)
-    fe M = h ? Bh : A, Mp = h ? Bp : Ap;
-    const bool clean = SR ? quad::is_ristretto_identity(M) : quad::is_identity_times8(M);
-    if (clean) continue;  // block-uniform: every quad holds the same sums
-    if (!SR) {
-      for (int i = 0; i < 3; i++) {
-        quad::dbl(r, M);
-        quad::p1p1_to_p3(M, r);
-        quad::dbl(r, Mp);
-        quad::p1p1_to_p3(Mp, r);
-      }
-    }
-    if (threadIdx.x == 0) {
-      s_cnt = 0;
-      s_j = -1;
-    }
-    fe Mc, Dc, P = M, D = M;
-    quad::to_cached(Mc, M);
-    const int k = q + 1;  // <= 16; quad-uniform
-    for (int b = 30 - __builtin_clz((unsigned)k); b >= 0; b--) {
-      quad::dbl(r, P);
-      quad::p1p1_to_p3(P, r);
-      if ((k >> b) & 1) {
-        quad::add(r, P, Mc);
-        quad::p1p1_to_p3(P, r);
-      }
-    }
-    for (int i = 0; i < 4; i++) {
-      quad::dbl(r, D);
-      quad::p1p1_to_p3(D, r);
-    }
-    quad::to_cached(Dc, D);
-    __syncthreads();  // s_cnt / s_j initialised
-    for (uint32_t j = (uint32_t)q; j < m; j += 16) {
-      const bool eq = SR ? quad::ristretto_equal(P, Mp) : quad::p3_equal(P, Mp);
-      if (eq && c == 0) {
-        atomicAdd(&s_cnt, 1);
-        s_j = (int)j;
-      }
-      quad::add(r, P, Dc);
-      quad::p1p1_to_p3(P, r);
-    }
-    __syncthreads();
-    if (s_cnt == 1 && (uint32_t)s_j >= lo && (uint32_t)s_j < hi) {  // block-uniform
-      if (threadIdx.x == 0) {
-        mw.fb_list[atomicAdd(mw.fb_count, 1u)] = e0 + (uint32_t)s_j;
-        atomicAdd(mw.loc_found, 1u);
-      }
-    } else {
-      if (threadIdx.x == 0) s_base = atomicAdd(mw.fb_count, hi - lo);
-      __syncthreads();
-      for (uint32_t u = threadIdx.x; u < hi - lo; u += 64) mw.fb_list[s_base + u] = e0 + lo + u;
-    }
-    __syncthreads();  // s_cnt / s_j / s_base reused by the next half
-  }
-}
-
-// After k_msm_subcheck over the groups the search could not name: the
-// entries of every failing 8-entry sub-group go to the per-entry list (the
-// rest keep their pre-check status).  One lane per (listed group, sub-group).
-__global__ void __launch_bounds__(256)
-k_sub_list(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t sh = p.m_log2 - kSubGroupLog2;
-  if ((t >> sh) >= *mw.l2_count) return;
-  const uint32_t e0 = (mw.l2_list[t >> sh] << p.m_log2) + ((t & ((1u << sh) - 1)) << kSubGroupLog2);
-  const uint32_t cnt = entry_count(count_ptr, n);
-  if (e0 >= cnt || mw.sub_ok[e0 >> kSubGroupLog2]) return;
-  const uint32_t k = min(kSubGroup, cnt - e0);
-  const uint32_t at = atomicAdd(mw.fb_count, k);
-  for (uint32_t j = 0; j < k; j++) mw.fb_list[at + j] = e0 + j;
 }
 
 // Sub-group bisection (row H, before the per-entry fallback): a failing group
@@ -1589,6 +1151,25 @@ static size_t sort_smem(const MsmParams &p, uint32_t bs) {
   return ((size_t)p.W * p.H + bs * 9 + bs + 1 + 2 * (2 * p.m() + 1)) * sizeof(uint32_t);
 }
 
+#ifdef TMV_CHECKS
+// Test build: every bucket with entries must have a sum written by this
+// launch.  The bucket sums are zeroed before the accumulation runs, so a
+// bucket whose join was lost keeps Z == 0 and is counted here.
+__global__ void __launch_bounds__(256)
+k_check_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork mw, MsmParams p) {
+  const uint32_t live_groups = (entry_count(count_ptr, n) + p.m() - 1) >> p.m_log2;
+  const uint64_t nb = (uint64_t)live_groups * p.W * p.H;
+  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    if (!mw.bk_cnt[b]) continue;
+    const fe &z = mw.bk_sum[b].Z;
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < 10; k++) zero = zero && z.v[k] == 0;
+    if (zero) atomicAdd(&g_buckets_unwritten, 1u);
+  }
+}
+#endif
+
 // Bucket sums, window parts and window sums (shared by both forms).
 // timed: bracket the first two kernels with the live kernel timer (the
 // located fallback's second pass over the failing groups is not timed).
@@ -1596,34 +1177,28 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
                                  hipStream_t stream, bool timed = true) {
   const uint64_t chunks = (uint64_t)p.groups * p.chunks_per_group();
   const uint32_t ablocks = (uint32_t)((chunks + 255) / 256), per_xcd = (ablocks + 7) / 8;
+  hipError_t e;
+#ifdef TMV_CHECKS
+  if ((e = hipMemsetAsync(mw.bk_sum, 0, (size_t)p.groups * p.W * p.H * sizeof(ge_p3), stream)) != hipSuccess) return e;
+#endif
   void *tk = timed ? ktimer::begin(ktimer::kAccum, stream) : nullptr;
-  if (p.L == 8)
-    hipLaunchKernelGGL(k_msm_accum<8>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
-  else if (p.L == 16)
+  if (p.L == 16)
     hipLaunchKernelGGL(k_msm_accum<16>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
   else
     hipLaunchKernelGGL(k_msm_accum<32>, dim3(8 * per_xcd), dim3(256), 0, stream, count_ptr, n, mw, p);
-  hipError_t e;
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
-  if (kMsmJoin && kMsmJoinList) {
-    // lanes for ~3% of the chunks (C2 names ~2.5%); more joins stride
-    const uint32_t jblocks = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((chunks / 32 + 255) / 256, 1), 8192);
-    hipLaunchKernelGGL(k_msm_join_list, dim3(jblocks), dim3(256), 0, stream, mw, p);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  } else if (kMsmJoin) {
-    const uint64_t per_block = 4ull * kJoinScan * 64;
-    hipLaunchKernelGGL(k_msm_join, dim3((uint32_t)((chunks + per_block - 1) / per_block)), dim3(256), 0, stream,
-                       count_ptr, n, mw, p);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
+  // lanes for ~3% of the chunks (C2 names ~2.5%); more joins stride
+  const uint32_t jblocks = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((chunks / 32 + 255) / 256, 1), 8192);
+  hipLaunchKernelGGL(k_msm_join_list, dim3(jblocks), dim3(256), 0, stream, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+#ifdef TMV_CHECKS
+  hipLaunchKernelGGL(k_check_buckets, dim3(1024), dim3(256), 0, stream, count_ptr, n, mw, p);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+#endif
   const uint64_t parts = (uint64_t)p.groups * p.W * p.P;
   tk = timed ? ktimer::begin(ktimer::kWpart, stream) : nullptr;
-  if (kMsmJoin && p.P == 1 && parts <= wpart_quad_rows())
-    hipLaunchKernelGGL(k_msm_wpart_quad, dim3((uint32_t)((4 * parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n,
-                       mw, p);
-  else
-    hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
+  hipLaunchKernelGGL(k_msm_wpart, dim3((uint32_t)((parts + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   ktimer::end(tk, stream);
   if (p.P == 1) return hipSuccess;  // the parts are the window sums
@@ -1637,39 +1212,32 @@ static hipError_t launch_buckets(const uint32_t *count_ptr, uint32_t n, MsmWork 
 // with; m = 256 20.2 ms without, 19.4 ms with; the C2 bench (m = 64, 4
 // launches in flight) 76.3 vs 69.7 M/s -- the check is a ~1.1k-addition
 // chain per quad that lengthens every launch's critical path by ~1.4 ms.
-// Default: groups of >= 256 entries.  TMV_SUBCHECK=0 never, =1 always.
-static int subcheck_mode() {
-  static const int mode = [] {
-    const char *e = getenv("TMV_SUBCHECK");
-    if (!e) return -1;
-    return strcmp(e, "0") ? 1 : 0;
-  }();
-  return mode;
-}
-// k_msm_sort workgroup size for groups <= 256 entries: 64 by default
-// (TMV_SORT_BLOCK=256: the old 256).  A 64-entry group in a 256-thread
-// workgroup left 3 of 4 waves idle but resident through the sort's LDS
-// phases; C2 bench (3,072 steps, round 1, one GPU call): 80.4 / 80.7 ->
-// 84.8 / 84.7 M/s.
-// TMV_SORT_BLOCK=128: two waves per group of <= 256 (A/B).
-static int sort_block() {
-  static const int bs = [] {
-    const char *e = getenv("TMV_SORT_BLOCK");
-    return (e && !strcmp(e, "256")) ? 256 : (e && !strcmp(e, "128")) ? 128 : 64;
-  }();
-  return bs;
-}
+// Default: groups of >= 256 entries (tmv_set_batch_options can force it on
+// or off per context).
+bool subcheck_enabled(uint32_t m_log2) { return m_log2 >= 8; }
 
-// Per-entry fallback over the failing groups only (k_msm_horner's list; the
-// pre-check statuses of every entry written by k_msm_sort) instead of a grid
-// over all entries whose passing blocks exit early.  TMV_FALLBACK_COMPACT=0:
-// off.  C2 bench, one GPU call: 85.3 / 85.3 vs 84.6 / 84.4 M/s off.
-static bool fallback_compact() {
-  static const bool on = [] {
-    const char *e = getenv("TMV_FALLBACK_COMPACT");
-    return !(e && !strcmp(e, "0"));
-  }();
-  return on;
+// Test build counters (TMV_CHECKS), summed over every launch since the last
+// reset; false in a product build.
+bool read_checks(uint32_t out[3], bool reset) {
+#ifdef TMV_CHECKS
+  uint32_t v[3] = {0, 0, 0};
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&v[0], HIP_SYMBOL(g_joins_named), 4) != hipSuccess ||
+      hipMemcpyFromSymbol(&v[1], HIP_SYMBOL(g_joins_done), 4) != hipSuccess ||
+      hipMemcpyFromSymbol(&v[2], HIP_SYMBOL(g_buckets_unwritten), 4) != hipSuccess)
+    return false;
+  for (int k = 0; k < 3; k++) out[k] = v[k];
+  if (reset) {
+    const uint32_t z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_joins_named), &z, 4);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_joins_done), &z, 4);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_buckets_unwritten), &z, 4);
+  }
+  return true;
+#else
+  (void)out;
+  (void)reset;
+  return false;
+#endif
 }
 
 // Located fallback (k_msm_sort<LOC> .. k_loc_search): for launches of at
@@ -1681,9 +1249,12 @@ static bool fallback_compact() {
 // a longer chain (a second Horner), so it pays where throughput, not the
 // launch's latency, sets the rate.  C2 launches alone (profiles/r05/
 // ab_locate_min.txt), located vs not: 250k 2.99 vs 2.65-2.70 ms, 500k 4.80 vs
-// 4.73-4.81, 1M 8.67-8.92 vs 9.40 -- with the half-size scalars the
-// per-entry fallback got cheaper, so the crossover moved up from 150k.
-// (Read at every launch: tests cover the located path below the default.)
+// 4.73-4.81, 1M 8.67-8.92 vs 9.40.  Round 5 measured and removed two
+// refinements for the groups the search cannot name (two or more bad
+// entries): sub-group checks (profiles/r03/ab_loc_subcheck.txt) and a
+// bisection MSM (profiles/r05/ab_loc_bisect.txt) -- both fewer one-by-one
+// entries, both slower launches.  (Read at every launch: tests cover the
+// located path below the default.)
 static uint32_t locate_min() {
   const char *e = getenv("TMV_LOCATE_MIN");
   return e ? (uint32_t)strtoul(e, nullptr, 10) : 400000u;
@@ -1691,51 +1262,9 @@ static uint32_t locate_min() {
 
 uint32_t locate_min_entries() { return locate_min(); }
 
-// TMV_LOC_PARTS=1: the located pass's running sums on one lane per window
-// (as the primary pass of a wide launch), for A/B
-static bool loc_parts_env() {
-  static const bool one = [] {
-    const char *e = getenv("TMV_LOC_PARTS");
-    return e && !strcmp(e, "1");
-  }();
-  return one;
-}
-
-// TMV_LOC_SUBCHECK=1: groups the located search cannot name (two or more
-// bad entries, ~2% of C2's groups of 128) get sub-group checks before the
-// per-entry fallback instead of all their entries verified one by one.  Less
-// work, a longer tail (the Straus sub-group chain, then the fallback's): C2
-// bench 126.2-126.9 with vs 127.9-128.8 M/s without (profiles/r03/
-// ab_loc_subcheck.txt), so off by default.
-static bool loc_subcheck() {
-  static const bool on = [] {
-    const char *e = getenv("TMV_LOC_SUBCHECK");
-    return e && !strcmp(e, "1");
-  }();
-  return on;
-}
-
-// Bisection of the groups the located search cannot name (k_loc_search2)
-// for launches of at least this many entries (TMV_LOC_BISECT_MIN; default 0
-// = never).  Measured and not kept (profiles/r05/ab_loc_bisect.txt, one box):
-// it cuts the one-by-one entries of a 2.56M C2 launch from 46,416 to 13,040,
-// but its second MSM, Horner and search lengthen the chain -- launch alone
-// 19.42 -> 19.88 ms at 2.56M, 8.21 -> 8.87 ms at 1M -- and with 4 launches in
-// flight the bench does not gain either (135.9 / 136.6 off vs 135.4 / 136.1
-// M/s on).  (Read at every launch: the tests switch it on.)
-static uint32_t loc_bisect_min() {
-  const char *e = getenv("TMV_LOC_BISECT_MIN");
-  return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-}
-
 bool locate_enabled(uint32_t n, const MsmParams &p) {
   const uint32_t lmin = locate_min();
-  return fallback_compact() && lmin && n >= lmin && !p.sub && p.WL() <= p.W;
-}
-
-bool subcheck_enabled(uint32_t m_log2) {
-  const int mode = subcheck_mode();
-  return mode < 0 ? m_log2 >= 8 : mode == 1;
+  return lmin && n >= lmin && !p.sub && p.WL() <= p.W;
 }
 
 // Views of a launch's work arrays for the entries of groups [g0, ...): the
@@ -1773,57 +1302,55 @@ static MsmWork msm_view(MsmWork mw, const MsmParams &p, uint32_t n, uint64_t g0)
   return mw;
 }
 
+// k_msm_sort over every group (LOC: every failing group's slot).  Groups of
+// <= 256 entries take 64-thread workgroups (4 entries per thread at most):
+// a 64-entry group in a 256-thread workgroup left 3 of 4 waves idle but
+// resident through the sort's LDS phases (C2 bench, round 1: 80.4 / 80.7 ->
+// 84.8 / 84.7 M/s).
+template <bool SR, bool LOC>
+static hipError_t launch_sort(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
+                              uint32_t e_base, const fe *btab_q, Ed25519Work w, MsmWork mw, const MsmParams &p,
+                              const MsmSeed &seed, uint8_t *out, int aligned, hipStream_t stream) {
+  if (p.m_log2 <= 8)
+    hipLaunchKernelGGL((k_msm_sort<SR, false, 64, LOC>), dim3(p.groups), dim3(64), sort_smem(p, 64), stream, sig, idx,
+                       count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, out, e_base);
+  else
+    hipLaunchKernelGGL((k_msm_sort<SR, false, kMsmSortBlock, LOC>), dim3(p.groups), dim3(kMsmSortBlock),
+                       sort_smem(p, kMsmSortBlock), stream, sig, idx, count_ptr, n, w, mw, p, seed, btab_q, aligned,
+                       nullptr, nullptr, out, e_base);
+  return hipGetLastError();
+}
+
 // Throughput stages (prep, sort, bucket sums, window sums) of entries
 // [e_base, e_base + n) of a launch; w / mw / out / pk / sig / msg_off are
 // already offset to the part.
 template <bool SR>
-static hipError_t launch_sort_buckets(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
-                                      uint32_t e_base, const fe *btab_q, Ed25519Work w, MsmWork mw,
-                                      const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned,
-                                      bool compact, hipStream_t stream) {
-  hipError_t e;
-  // groups of <= 256 entries: 64-thread workgroups (4 entries per thread at
-  // most), so a 64-entry group no longer parks 192 idle lanes
-  if (p.m_log2 <= 8 && sort_block() == 64) {
-    const size_t smem = sort_smem(p, 64);
-    hipLaunchKernelGGL((k_msm_sort<SR, false, 64>), dim3(p.groups), dim3(64), smem, stream, sig, idx, count_ptr, n,
-                       w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr, e_base);
-  } else if (p.m_log2 <= 8 && sort_block() == 128) {
-    const size_t smem = sort_smem(p, 128);
-    hipLaunchKernelGGL((k_msm_sort<SR, false, 128>), dim3(p.groups), dim3(128), smem, stream, sig, idx, count_ptr,
-                       n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr, e_base);
-  } else {
-    const size_t smem = sort_smem(p, kMsmSortBlock);
-    hipLaunchKernelGGL((k_msm_sort<SR, false>), dim3(p.groups), dim3(kMsmSortBlock), smem, stream, sig, idx,
-                       count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, compact ? out : nullptr,
-                       e_base);
-  }
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_buckets(count_ptr, n, mw, p, stream);
-}
-
-template <bool SR>
 static hipError_t launch_part(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                               const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, uint32_t e_base,
                               const fe *btab_q, const strobe_t *prefix, Ed25519Work w, MsmWork mw,
-                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned, bool compact,
+                              const MsmParams &p, const MsmSeed &seed, uint8_t *out, int aligned,
                               hipStream_t stream) {
   w.niels = mw.pts;
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
-  return launch_sort_buckets<SR>(sig, idx, count_ptr, n, e_base, btab_q, w, mw, p, seed, out, aligned, compact,
-                                 stream);
+  if ((e = launch_sort<SR, false>(sig, idx, count_ptr, n, e_base, btab_q, w, mw, p, seed, out, aligned, stream)) !=
+      hipSuccess)
+    return e;
+  return launch_buckets(count_ptr, n, mw, p, stream);
 }
 
 // Latency stages of a whole launch: Horner over every group, then the
 // located fallback (large launches) or the per-entry fallback of the failing
-// groups.
+// groups.  Below the located size Horner runs beside helper workgroups that
+// reduce every entry's k for the fallback (k_msm_horner_helped; 125k
+// fallback 273 -> 238 us, profiles/r05/ab_horner_help.txt).
 template <bool SR>
 static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uint32_t *count_ptr, uint32_t n,
                               const fe *btab_q, Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
-                              uint8_t *out, int aligned, bool compact, hipStream_t stream) {
+                              uint8_t *out, int aligned, hipStream_t stream) {
   hipError_t e;
-  const bool helped = compact && !locate_enabled(n, p) && horner_help() && w.hs_buf;
+  const bool located = locate_enabled(n, p);
+  const bool helped = !located && w.hs_buf;
   const uint32_t hblocks = (p.groups + 15) / 16;
   if (helped) {
     hipLaunchKernelGGL(k_msm_horner_helped<SR>, dim3(hblocks + (n + 63) / 64), dim3(64), 0, stream, count_ptr, n, mw,
@@ -1834,63 +1361,21 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
                        0u);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (compact && locate_enabled(n, p)) {
+  if (located) {
     // second MSM over the failing groups (slot f = f-th failing group), then
     // the search, then one-by-one verification of the listed entries only
-    if (p.m_log2 <= 8 && sort_block() == 64) {
-      const size_t smem = sort_smem(p, 64);
-      hipLaunchKernelGGL((k_msm_sort<SR, false, 64, true>), dim3(p.groups), dim3(64), smem, stream, sig, idx,
-                         count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
-    } else if (p.m_log2 <= 8 && sort_block() == 128) {
-      const size_t smem = sort_smem(p, 128);
-      hipLaunchKernelGGL((k_msm_sort<SR, false, 128, true>), dim3(p.groups), dim3(128), smem, stream, sig, idx,
-                         count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
-    } else {
-      const size_t smem = sort_smem(p, kMsmSortBlock);
-      hipLaunchKernelGGL((k_msm_sort<SR, false, kMsmSortBlock, true>), dim3(p.groups), dim3(kMsmSortBlock), smem,
-                         stream, sig, idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr,
-                         0u);
-    }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_sort<SR, true>(sig, idx, count_ptr, n, 0u, btab_q, w, mw, p, seed, nullptr, aligned, stream)) !=
+        hipSuccess)
+      return e;
     const uint32_t n_slots = p.groups << p.m_log2;
-    MsmParams pl = p;  // running sums split over loc_parts() lanes per window (TMV_LOC_PARTS=1: one)
-    pl.P = loc_parts_env() ? p.P : p.loc_parts();
+    MsmParams pl = p;  // running sums split over loc_parts() lanes per window (few live slots: the chain sets the time)
+    pl.P = p.loc_parts();
     if ((e = launch_buckets(mw.loc_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_msm_horner<SR, false, 1>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
+    hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
                        mw.loc_count, n_slots, mw, pl, nullptr, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t bmin = loc_bisect_min();
-    const int sub2 = loc_subcheck() ? 1 : (bmin && n >= bmin ? 2 : 0);
-    hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p, sub2);
+    hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (sub2 == 2) {  // bisection MSM over the first halves of the unnamed groups, then its search
-      if (p.m_log2 <= 8 && sort_block() == 64) {
-        hipLaunchKernelGGL((k_msm_sort<SR, false, 64, 2>), dim3(p.groups), dim3(64), sort_smem(p, 64), stream, sig,
-                           idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
-      } else if (p.m_log2 <= 8 && sort_block() == 128) {
-        hipLaunchKernelGGL((k_msm_sort<SR, false, 128, 2>), dim3(p.groups), dim3(128), sort_smem(p, 128), stream,
-                           sig, idx, count_ptr, n, w, mw, p, seed, btab_q, aligned, nullptr, nullptr, nullptr, 0u);
-      } else {
-        hipLaunchKernelGGL((k_msm_sort<SR, false, kMsmSortBlock, 2>), dim3(p.groups), dim3(kMsmSortBlock),
-                           sort_smem(p, kMsmSortBlock), stream, sig, idx, count_ptr, n, w, mw, p, seed, btab_q,
-                           aligned, nullptr, nullptr, nullptr, 0u);
-      }
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      if ((e = launch_buckets(mw.l2e_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
-      hipLaunchKernelGGL((k_msm_horner<SR, false, 2>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
-                         mw.l2e_count, n_slots, mw, pl, nullptr, 0u);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_loc_search2<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if (sub2) {  // groups the search could not name: sub-group checks, then their failing sub-groups' entries
-      const uint64_t subs = (uint64_t)p.groups << (p.m_log2 - kSubGroupLog2);
-      hipLaunchKernelGGL(k_msm_subcheck<SR>, dim3((uint32_t)((subs + 15) / 16)), dim3(64), 0, stream, sig, idx,
-                         count_ptr, n, w, mw, p, seed, btab_q, aligned, (const uint32_t *)mw.l2_list,
-                         (const uint32_t *)mw.l2_count);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_sub_list, dim3((uint32_t)((subs + 255) / 256)), dim3(256), 0, stream, count_ptr, n, mw, p);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream,
                                     nullptr, nullptr, nullptr, mw.fb_list, mw.fb_count);
   }
@@ -1904,8 +1389,10 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     if ((e = hipGetLastError()) != hipSuccess) return e;
     sub_ok = mw.sub_ok;
   }
+  // the failing groups' entries only (k_msm_horner's list; every entry's
+  // pre-check status was written by k_msm_sort)
   return launch_quad_fallback<SR>(sig, idx, count_ptr, n, btab_q, w, mw.group_ok, p.m_log2, out, aligned, stream,
-                                  sub_ok, compact ? mw.fail_list : nullptr, compact ? mw.fail_count : nullptr);
+                                  sub_ok, mw.fail_list, mw.fail_count);
 }
 
 template <bool SR>
@@ -1915,18 +1402,17 @@ static hipError_t launch_check(const uint8_t *pk, const uint8_t *sig, const uint
                                const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
-  const bool compact = fallback_compact();
   w.niels = mw.pts;
   hipError_t e = launch_part<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, 0u, btab_q, prefix, w, mw, p, seed, out,
-                                 aligned, compact, stream);
+                                 aligned, stream);
   if (e != hipSuccess) return e;
-  return launch_tail<SR>(sig, idx, count_ptr, n, btab_q, w, mw, p, seed, out, aligned, compact, stream);
+  return launch_tail<SR>(sig, idx, count_ptr, n, btab_q, w, mw, p, seed, out, aligned, stream);
 }
 
 hipError_t launch_batch_check_part(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                    const uint32_t *msg_off, uint32_t n, uint32_t e0, uint32_t e1, const fe *btab_q,
                                    const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
-                                   const MsmSeed &seed, uint8_t *out, hipStream_t stream, bool prep_only) {
+                                   const MsmSeed &seed, uint8_t *out, hipStream_t stream) {
   // a part is whole groups: it starts on a group edge and ends on one or at n
   if (e0 >= e1 || e1 > n || (e0 & (p.m() - 1)) || (e1 != n && (e1 & (p.m() - 1)))) return hipErrorInvalidValue;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
@@ -1935,40 +1421,23 @@ hipError_t launch_batch_check_part(bool sr, const uint8_t *pk, const uint8_t *si
   pp.groups = ((e1 - e0) + p.m() - 1) >> p.m_log2;
   w.niels = mw.pts;
   const uint64_t E = e0;
-  if (prep_only) {  // the sort and bucket stages run later over the whole launch
-    Ed25519Work v = work_view(w, E);
-    v.niels = mw.pts + 2 * E * kNielsPer;
-    if (sr) return launch_prep<true>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, prefix,
-                                     v, aligned, stream);
-    return launch_prep<false>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, prefix, v,
-                              aligned, stream);
-  }
   if (sr)
     return launch_part<true>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, e0, btab_q,
                              prefix, work_view(w, E), msm_view(mw, p, n, g0), pp, seed, out ? out + E : nullptr,
-                             aligned, fallback_compact(), stream);
+                             aligned, stream);
   return launch_part<false>(pk + 32 * E, sig + 64 * E, msg, msg_off + E, nullptr, nullptr, e1 - e0, e0, btab_q,
                             prefix, work_view(w, E), msm_view(mw, p, n, g0), pp, seed, out ? out + E : nullptr,
-                            aligned, fallback_compact(), stream);
+                            aligned, stream);
 }
 
 hipError_t launch_batch_check_tail(bool sr, const uint8_t *pk, const uint8_t *sig, uint32_t n, const fe *btab_q,
                                    Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
-                                   uint8_t *out, hipStream_t stream, bool after_prep) {
+                                   uint8_t *out, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
   w.niels = mw.pts;
-  if (after_prep) {  // parts ran their prep only: sort and bucket stages over the whole launch first
-    hipError_t e = sr ? launch_sort_buckets<true>(sig, nullptr, nullptr, n, 0u, btab_q, w, mw, p, seed, out, aligned,
-                                                  fallback_compact(), stream)
-                      : launch_sort_buckets<false>(sig, nullptr, nullptr, n, 0u, btab_q, w, mw, p, seed, out, aligned,
-                                                   fallback_compact(), stream);
-    if (e != hipSuccess) return e;
-  }
-  if (sr) return launch_tail<true>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(),
-                                   stream);
-  return launch_tail<false>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(),
-                            stream);
+  if (sr) return launch_tail<true>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, stream);
+  return launch_tail<false>(sig, nullptr, nullptr, n, btab_q, w, mw, p, seed, out, aligned, stream);
 }
 
 hipError_t launch_batch_check_part_idx(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
@@ -1985,9 +1454,9 @@ hipError_t launch_batch_check_part_idx(bool sr, const uint8_t *pk, const uint8_t
   // indexed by them); the work arrays are views at slot e0
   if (sr)
     return launch_part<true>(pk, sig, msg, msg_off, idx + e0, nullptr, e1 - e0, e0, btab_q, prefix, work_view(w, e0),
-                             msm_view(mw, p, nb, g0), pp, seed, out, aligned, fallback_compact(), stream);
+                             msm_view(mw, p, nb, g0), pp, seed, out, aligned, stream);
   return launch_part<false>(pk, sig, msg, msg_off, idx + e0, nullptr, e1 - e0, e0, btab_q, prefix, work_view(w, e0),
-                            msm_view(mw, p, nb, g0), pp, seed, out, aligned, fallback_compact(), stream);
+                            msm_view(mw, p, nb, g0), pp, seed, out, aligned, stream);
 }
 
 hipError_t launch_batch_check_tail_idx(bool sr, const uint8_t *pk, const uint8_t *sig, const uint32_t *idx, uint32_t n,
@@ -1996,8 +1465,8 @@ hipError_t launch_batch_check_tail_idx(bool sr, const uint8_t *pk, const uint8_t
   if (n == 0) return hipSuccess;
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
   w.niels = mw.pts;
-  if (sr) return launch_tail<true>(sig, idx, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(), stream);
-  return launch_tail<false>(sig, idx, nullptr, n, btab_q, w, mw, p, seed, out, aligned, fallback_compact(), stream);
+  if (sr) return launch_tail<true>(sig, idx, nullptr, n, btab_q, w, mw, p, seed, out, aligned, stream);
+  return launch_tail<false>(sig, idx, nullptr, n, btab_q, w, mw, p, seed, out, aligned, stream);
 }
 
 // Key-merged form: one quad per item.  Items [0, n_runs) are runs of one key

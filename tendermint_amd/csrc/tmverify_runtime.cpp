@@ -35,6 +35,7 @@
 #include "host/shard_plan.h"
 #include "host/shard_run.h"
 #include "host/wait.h"
+#include "knobs.h"
 #include "ktimer.h"
 #include "verify_kernels.h"
 #include "votes.h"
@@ -174,7 +175,7 @@ struct Workspace {
   DeviceBuf work, work2, idx, msm, msm2, gather;
   hipEvent_t done = nullptr;
   // mixed batch-equation launches: the sr25519 pipeline's stream and its
-  // fork / join events (created on first use; TMV_MIXED_TWO=0: one stream)
+  // fork / join events (created on first use)
   tmv::KindStreams kinds{nullptr, nullptr, nullptr};
   // last batch-equation launch on this stream (for tmv_batch_stats)
   const uint8_t *group_ok[2] = {nullptr, nullptr};
@@ -315,9 +316,8 @@ size_t leaked_pin_count() {
 // Kernel choice: the quad (4 lanes / signature) path wins while the batch is
 // too small to fill the chip one lane per signature; the single-lane kernel
 // has less glue per signature and wins on large batches.
-// TMV_KERNEL=quad|single overrides (A/B measurement).
-uint32_t g_quad_max = 0;
-int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
+constexpr uint32_t kQuadMax = 49152;
+int g_kernel_override = -1;  // A/B (TMV_KERNEL=quad|single): -1 auto, 0 single, 1 quad
 // Batch equation (msm.h) by default from this many entries up (TMV_MSM_MIN,
 // 0 = never): below it a batch is latency-bound and the per-entry pipeline
 // beats the batch check's longer chain; above it the batch check does 2-3x
@@ -329,48 +329,40 @@ int g_kernel_override = -1;  // -1 auto, 0 single, 1 quad
 // both.  Flags override per call.
 uint32_t g_msm_min = 32768;
 uint32_t g_km_min = 16384;
-uint32_t g_msm_chunk = 0;  // TMV_MSM_CHUNK: 8, 16 or 32 overrides the chunk length (A/B measurement)
-uint32_t g_msm_parts = 0;  // TMV_MSM_PARTS: running-sum lanes per window (power of two <= H; A/B measurement)
+uint32_t g_msm_chunk = 0;  // A/B (TMV_MSM_CHUNK): 16 or 32 overrides the chunk length
+uint32_t g_msm_parts = 0;  // A/B (TMV_MSM_PARTS): running-sum lanes per window (power of two <= H)
 // Key-cached batches up to this size run as one fused latency kernel
 // (TMV_CACHED_FUSED_MAX; commit-sized calls such as VerifyCommit).
 uint32_t g_cached_fused_max = 4096;
 // Fused-path batches read their inputs and write their statuses in pinned
-// host memory instead of copying (TMV_ZERO_COPY=0 turns it off).
+// host memory instead of copying (A/B: TMV_ZERO_COPY=0 turns it off).
 int g_zero_copy = 1;
 // Host-buffer batches of at least this many entries per device are
 // pipelined in chunks (of half to one of these) over two lanes
 // (TMV_HOST_CHUNK).
 uint32_t g_host_chunk = 262144;
-// Mixed ed25519 + sr25519 host batches on the batch equation are not
-// streamed (one-kind batches only): each chunk is a whole pipeline with its
-// two kinds' latency tails, so they are cut into fewer, larger chunks than
-// other host batches -- 1M entries in two 500k chunks, the second's copy
-// beside the first's kernels (TMV_MIXED_CHUNK).
+// Mixed ed25519 + sr25519 host batches on the batch equation are streamed
+// (mixed_check_streamed, round 5: C5 1M end to end 16.0 -> 11.0-11.3 ms);
+// A/B (TMV_MIXED_STREAM=0): unstreamed, in chunks of g_mixed_chunk, the
+// second's copy beside the first's kernels.
+int g_mixed_stream = 1;
 uint32_t g_mixed_chunk = 786432;
-// Mixed batches on the batch equation are streamed like one-kind ones
-// (mixed_check_streamed): TMV_MIXED_STREAM=0 turns it off (then g_mixed_chunk
-// applies).  Read at every call (A/B and tests).
-static bool mixed_stream_on() {
-  const char *e = getenv("TMV_MIXED_STREAM");
-  return !(e && !strcmp(e, "0"));
-}
-// Lanes the chunks rotate over (TMV_HOST_LANES, 1..kLanes).
+// Lanes the chunks rotate over (A/B: TMV_HOST_LANES, 1..kLanes).
 uint32_t g_host_lanes = 2;
 // Bound on every wait for device work (TMV_DEVICE_TIMEOUT_MS, 0 = none).
 int64_t g_timeout_ms = 60000;
-// Streamed host batches (uncached batch equation, one key kind): a chunk's
-// inputs are staged and copied in parts -- the first of g_stream_first
-// entries, then g_stream_part each (rounded to whole groups) -- and each
-// part's throughput kernels start as soon as its copy lands, so one
-// pipeline covers the chunk (one latency tail) while the rest is still
-// being staged (TMV_STREAM_FIRST, TMV_STREAM_PART; TMV_STREAM=0 turns it
-// off).  Such batches are cut into chunks of up to g_stream_chunk entries
-// per device (TMV_STREAM_CHUNK).
+// Streamed host batches (uncached batch equation): a chunk's inputs are
+// staged and copied in parts -- the first of g_stream_first entries, then
+// g_stream_part each (rounded to whole groups) -- and each part's throughput
+// kernels start as soon as its copy lands, so one pipeline covers the chunk
+// (one latency tail) while the rest is still being staged
+// (TMV_STREAM_FIRST, TMV_STREAM_PART).  Such batches are cut into chunks of
+// up to g_stream_chunk entries per device (TMV_STREAM_CHUNK).  A/B:
+// TMV_STREAM=0 (no streaming), TMV_STREAM_TWO=0 (every part on the lane's
+// stream), TMV_SR_GROUP_LOG2 (group size of uncached sr25519 launches).
 int g_stream = 1;
-bool g_stream_prep_only = false;  // TMV_STREAM_MODE=prep: parts run their prep only
-int g_stream_two = 1;              // TMV_STREAM_TWO=0: every part on the lane's stream
-int g_mixed_two = 1;               // TMV_MIXED_TWO=0: a mixed launch's two kind pipelines on one stream
-uint32_t g_sr_group_log2 = 0;      // TMV_SR_GROUP_LOG2: group size of uncached sr25519 launches (A/B; 0 = default)
+int g_stream_two = 1;
+uint32_t g_sr_group_log2 = 0;
 // Round 2, 320k C2 entries end to end (parts on two streams): 5.7 ms with
 // parts of 32k / 64k, 5.85-6.0 with 32k / 128k; one stream 6.05-6.3;
 // unstreamed (two lanes of 80k chunks) 6.9 ms.  Round 3 (faster kernels,
@@ -385,54 +377,52 @@ constexpr uint32_t kMaxStreamParts = 512;  // bound on a streamed mixed chunk's 
 // whole pages of its pk / sig / msg spans (hipHostRegister, disjoint page
 // ranges part to part) while earlier parts run, and only the bytes outside
 // them (< 4 KiB per span and part) go through the lane's pinned staging
-// (TMV_REGISTER=0: stage everything).  A span whose pages cannot be pinned
-// (already pinned, read-only mapping, ...) is staged.
+// (A/B: TMV_REGISTER=0 stages everything).  A span whose pages cannot be
+// pinned (already pinned, read-only mapping, ...) is staged.
 int g_register = 1;
 
 void read_env() {
   static std::once_flag once;
   std::call_once(once, [] {
-    const char *k = getenv("TMV_KERNEL");
-    if (k && !strcmp(k, "quad")) g_kernel_override = 1;
-    if (k && !strcmp(k, "single")) g_kernel_override = 0;
-    const char *t = getenv("TMV_QUAD_MAX");
-    g_quad_max = t ? (uint32_t)strtoul(t, nullptr, 10) : 49152u;
+    // production knobs
     const char *mm = getenv("TMV_MSM_MIN");
     if (mm) g_msm_min = g_km_min = (uint32_t)strtoul(mm, nullptr, 10);
     const char *cf = getenv("TMV_CACHED_FUSED_MAX");
     if (cf) g_cached_fused_max = (uint32_t)strtoul(cf, nullptr, 10);
-    const char *zc = getenv("TMV_ZERO_COPY");
-    if (zc) g_zero_copy = atoi(zc);
     const char *hc = getenv("TMV_HOST_CHUNK");
-    if (hc) g_host_chunk = (uint32_t)strtoul(hc, nullptr, 10);
-    const char *mxc = getenv("TMV_MIXED_CHUNK");
-    if (mxc) g_mixed_chunk = (uint32_t)strtoul(mxc, nullptr, 10);
-    const char *hl = getenv("TMV_HOST_LANES");
-    if (hl) g_host_lanes = std::min<uint32_t>(kLanes, std::max<uint32_t>(1, (uint32_t)strtoul(hl, nullptr, 10)));
-    const char *mp = getenv("TMV_MSM_PARTS");
-    if (mp) g_msm_parts = (uint32_t)strtoul(mp, nullptr, 10);
-    const char *mc = getenv("TMV_MSM_CHUNK");
-    if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
+    if (hc) g_host_chunk = std::max<uint32_t>(1, (uint32_t)strtoul(hc, nullptr, 10));
     const char *to = getenv("TMV_DEVICE_TIMEOUT_MS");
     if (to) g_timeout_ms = strtoll(to, nullptr, 10);
-    const char *st = getenv("TMV_STREAM");
-    if (st) g_stream = atoi(st);
-    const char *sg = getenv("TMV_SR_GROUP_LOG2");
-    if (sg) g_sr_group_log2 = (uint32_t)strtoul(sg, nullptr, 10);
-    const char *m2 = getenv("TMV_MIXED_TWO");
-    if (m2) g_mixed_two = atoi(m2);
-    const char *s2 = getenv("TMV_STREAM_TWO");
-    if (s2) g_stream_two = atoi(s2);
-    const char *smd = getenv("TMV_STREAM_MODE");
-    if (smd) g_stream_prep_only = !strcmp(smd, "prep");
     const char *sf = getenv("TMV_STREAM_FIRST");
     if (sf) g_stream_first = std::max<uint32_t>(1, (uint32_t)strtoul(sf, nullptr, 10));
     const char *sp = getenv("TMV_STREAM_PART");
     if (sp) g_stream_part = std::max<uint32_t>(1, (uint32_t)strtoul(sp, nullptr, 10));
-    const char *rg = getenv("TMV_REGISTER");
-    if (rg) g_register = atoi(rg);
     const char *sc = getenv("TMV_STREAM_CHUNK");
     if (sc) g_stream_chunk = std::max<uint32_t>(2048, (uint32_t)strtoul(sc, nullptr, 10));
+    // A/B switches: read only by a -DTMV_AB build (knobs.h)
+    const char *k = tmv::ab_knob("TMV_KERNEL");
+    if (k && !strcmp(k, "quad")) g_kernel_override = 1;
+    if (k && !strcmp(k, "single")) g_kernel_override = 0;
+    const char *zc = tmv::ab_knob("TMV_ZERO_COPY");
+    if (zc) g_zero_copy = atoi(zc);
+    const char *ms = tmv::ab_knob("TMV_MIXED_STREAM");
+    if (ms) g_mixed_stream = atoi(ms);
+    const char *mxc = tmv::ab_knob("TMV_MIXED_CHUNK");
+    if (mxc) g_mixed_chunk = std::max<uint32_t>(1, (uint32_t)strtoul(mxc, nullptr, 10));
+    const char *hl = tmv::ab_knob("TMV_HOST_LANES");
+    if (hl) g_host_lanes = std::min<uint32_t>(kLanes, std::max<uint32_t>(1, (uint32_t)strtoul(hl, nullptr, 10)));
+    const char *mp = tmv::ab_knob("TMV_MSM_PARTS");
+    if (mp) g_msm_parts = (uint32_t)strtoul(mp, nullptr, 10);
+    const char *mc = tmv::ab_knob("TMV_MSM_CHUNK");
+    if (mc) g_msm_chunk = (uint32_t)strtoul(mc, nullptr, 10);
+    const char *st = tmv::ab_knob("TMV_STREAM");
+    if (st) g_stream = atoi(st);
+    const char *sg = tmv::ab_knob("TMV_SR_GROUP_LOG2");
+    if (sg) g_sr_group_log2 = (uint32_t)strtoul(sg, nullptr, 10);
+    const char *s2 = tmv::ab_knob("TMV_STREAM_TWO");
+    if (s2) g_stream_two = atoi(s2);
+    const char *rg = tmv::ab_knob("TMV_REGISTER");
+    if (rg) g_register = atoi(rg);
   });
 }
 
@@ -503,8 +493,8 @@ int faulted_rc(Device &d) {
 // and join less, and the 2H-addition running-sum chain halves.  3.0 keeps
 // c = 5 for groups of 64 and 128.
 constexpr double kRunningSumWeight = 3.0;
-static double running_sum_weight() {  // TMV_RS_WEIGHT: A/B of the weight (read per launch)
-  const char *e = getenv("TMV_RS_WEIGHT");
+static double running_sum_weight() {  // A/B of the weight (TMV_RS_WEIGHT, read per launch)
+  const char *e = tmv::ab_knob("TMV_RS_WEIGHT");
   return e ? atof(e) : kRunningSumWeight;
 }
 tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false, bool ed_only = false,
@@ -530,7 +520,7 @@ tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged =
   }
   c = std::max<uint32_t>(4, std::min<uint32_t>(9, c));
   tmv::MsmParams p = tmv::MsmParams::make(n, m_log2, c, merged);
-  if (g_msm_chunk == 8 || g_msm_chunk == 16 || g_msm_chunk == 32) p.L = g_msm_chunk;
+  if (g_msm_chunk == 16 || g_msm_chunk == 32) p.L = g_msm_chunk;
   if (g_msm_parts && g_msm_parts <= p.H && !(g_msm_parts & (g_msm_parts - 1))) p.P = g_msm_parts;
   // sub-group bisection: the context's choice, else the default policy
   // (the key-merged form's fallback is the key-cached comb: never)
@@ -541,7 +531,7 @@ tmv::MsmParams msm_params(uint32_t n, uint32_t m_log2, uint32_t c, bool merged =
 // Phase timing of the host-buffer path, printed to stderr when
 // TMV_HOST_TIMING is set (profiling aid; the host layer prints its own).
 struct EngineTimer {
-  bool on = getenv("TMV_HOST_TIMING") != nullptr;
+  bool on = tmh::host_timing();
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   void mark(const char *what, uint32_t n) {
     if (!on) return;
@@ -1137,15 +1127,14 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
       const hipStream_t t = two && (j & 1) ? s2 : s;
       if ((e = hipStreamWaitEvent(t, ready, 0)) != hipSuccess) { set_error("part wait", e); return TMV_ERR_LAUNCH; }
       e = tmv::launch_batch_check_part(sr, pk, sig, msg, off, n, b[j], b[j + 1], d.d_btab_q, d.d_prefix, w, mw, o.p,
-                                       o.seed[sr ? 1 : 0], out, t, g_stream_prep_only);
+                                       o.seed[sr ? 1 : 0], out, t);
       if (e != hipSuccess) { set_error("batch check part launch", e); return TMV_ERR_LAUNCH; }
     }
     if (two && ((e = hipEventRecord(join, s2)) != hipSuccess || (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess)) {
       set_error("part join", e);
       return TMV_ERR_LAUNCH;
     }
-    e = tmv::launch_batch_check_tail(sr, pk, sig, n, d.d_btab_q, w, mw, o.p, o.seed[sr ? 1 : 0], out, s,
-                                     g_stream_prep_only);
+    e = tmv::launch_batch_check_tail(sr, pk, sig, n, d.d_btab_q, w, mw, o.p, o.seed[sr ? 1 : 0], out, s);
   } else {
     e = tmv::launch_batch_check(sr, pk, sig, msg, off, nullptr, nullptr, n, d.d_btab_q, d.d_prefix, w, mw, o.p,
                                 o.seed[sr ? 1 : 0], out, s);
@@ -1305,14 +1294,14 @@ static int launch_mixed(Device &d, const LaunchOpts &o, const uint8_t *kind, con
     tmv::MsmWork m2 = tmv::MsmWork::carve(ws->msm2.ptr, n, o.p);
     read_env();
     tmv::KindStreams &ks = ws->kinds;
-    if (g_mixed_two && !ks.helper) {
+    if (!ks.helper) {
       if (hipStreamCreateWithFlags(&ks.helper, hipStreamNonBlocking) != hipSuccess) ks.helper = nullptr;
       if (hipEventCreateWithFlags(&ks.fork, hipEventDisableTiming) != hipSuccess) ks.fork = nullptr;
       if (hipEventCreateWithFlags(&ks.join, hipEventDisableTiming) != hipSuccess) ks.join = nullptr;
     }
     e = tmv::launch_mixed_batch_check(kind, pk, sig, msg, off, n, d.d_btab_q, d.d_prefix, w1, w2, m1, m2, o.p_ed,
                                       o.p, o.seed[0], o.seed[1], counts, idx_ed, idx_sr, status, s,
-                                      g_mixed_two ? &ks : nullptr);
+                                      &ks);
     ws->group_ok[0] = m1.group_ok;
     ws->group_ok[1] = m2.group_ok;
     ws->sub_ok[0] = o.p_ed.sub ? m1.sub_ok : nullptr;
@@ -1377,7 +1366,7 @@ static int launch_ed25519(Device &d, const LaunchOpts &o, const uint8_t *pk, con
                           const uint32_t *off, uint32_t n, uint8_t *valid, hipStream_t s) {
   if (o.batch_eq) return batch_check(d, o, false, pk, sig, msg, off, n, valid, s);
   read_env();
-  const bool quad = g_kernel_override == 1 || (g_kernel_override == -1 && n <= g_quad_max);
+  const bool quad = g_kernel_override == 1 || (g_kernel_override == -1 && n <= kQuadMax);
   hipError_t e;
   if (!quad) {
     e = tmv::launch_ed25519_verify(pk, sig, msg, off, n, d.d_btable, valid, s);
@@ -1426,6 +1415,30 @@ void tmv_internal_set_error(const char *msg) { g_last_error = msg ? msg : ""; }
 void tmv_internal_random_fault(int err, int count) {
   g_rand_fault_err = err;
   g_rand_fault_count = count;
+}
+// Test aid: switches the engine's tests set on paths that random inputs
+// almost never reach.  "half_scalars" = 1 (the product), 0 (every entry's
+// per-entry check on the full-k chain) or 2 (every third entry).  Returns 0,
+// or TMV_ERR_ARG for an unknown name.  Never called by the Go shim.
+int tmv_internal_option(const char *name, int64_t value) {
+  if (name && !strcmp(name, "half_scalars")) {
+    tmv::set_half_scalar_mode((int)value);
+    return 0;
+  }
+  set_error("unknown internal option");
+  return TMV_ERR_ARG;
+}
+// Test build counters (-DTMV_CHECKS, tools/build_checks.sh): out[0] joins
+// k_msm_accum named, out[1] joins k_msm_join_list did, out[2] buckets with
+// entries whose sum was never written; reset != 0 zeroes them.  Returns 0,
+// or TMV_ERR_ARG in a product build (no counters compiled in).
+int tmv_internal_checks(uint32_t *out3, int reset) {
+  if (!out3) { set_error("null argument"); return TMV_ERR_ARG; }
+  if (!tmv::read_checks(out3, reset != 0)) {
+    set_error("not a TMV_CHECKS build, or the device read failed");
+    return TMV_ERR_ARG;
+  }
+  return 0;
 }
 int64_t tmv_internal_mixed_stream_chunk(uint64_t free_bytes) {
   read_env();
@@ -1610,7 +1623,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
   }
   if (cached && !merged) o.batch_eq = false;  // key-cached per-entry path
   read_env();
-  const bool mixed_stream = sch == Scheme::Mixed && mixed_stream_on();
+  const bool mixed_stream = sch == Scheme::Mixed && g_mixed_stream;
   if (g_stream && !cached && !vs && (sch == Scheme::Ed25519 || sch == Scheme::Sr25519 || mixed_stream) &&
       o.batch_eq && n > g_stream_first) {
     // streamed: stage and copy part by part, each part's kernels behind its
@@ -1629,7 +1642,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     uint32_t *off = reinterpret_cast<uint32_t *>(h + L.off);
     const uint32_t base = msg_off[lo];
     size_t part = 0;
-    if ((g_stream_two || (mixed_stream && g_mixed_two)) && !ln.helper) {
+    if ((g_stream_two || mixed_stream) && !ln.helper) {
       if (hipStreamCreateWithFlags(&ln.helper, hipStreamNonBlocking) != hipSuccess) ln.helper = nullptr;
       else if (hipEventCreateWithFlags(&ln.join, hipEventDisableTiming) != hipSuccess) ln.join = nullptr;
     }
@@ -1718,7 +1731,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
         mixed_stream
             ? mixed_check_streamed(d, o, kind + lo, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg,
                                    reinterpret_cast<const uint32_t *>(dd + L.off), n,
-                                   static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, g_mixed_two ? ln.helper : nullptr,
+                                   static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, ln.helper,
                                    ln.join, ln.part_split, feed)
             : batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off), n,
                           static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed, g_stream_two ? ln.helper : nullptr,
@@ -1918,7 +1931,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
                           ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
   const bool mixed_batch_eq = sch == Scheme::Mixed && !vs && !(flags & TMV_FLAG_PER_ENTRY) &&
                               ((flags & TMV_FLAG_BATCH_EQUATION) || (g_msm_min > 0 && per_dev >= g_msm_min));
-  const bool mixed_streamed = mixed_batch_eq && g_stream && mixed_stream_on();
+  const bool mixed_streamed = mixed_batch_eq && g_stream && g_mixed_stream;
   uint32_t chunk = streamable ? g_stream_chunk : (mixed_batch_eq ? g_mixed_chunk : g_host_chunk);
   if (mixed_streamed) {
     size_t free_b = 0, total_b = 0;

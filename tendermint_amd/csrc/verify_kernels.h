@@ -89,16 +89,14 @@ hipError_t launch_batch_check(bool sr, const uint8_t *pk, const uint8_t *sig, co
 // group size, e1 too unless e1 = n -- once those entries are in device
 // memory, then, after every part, the latency stages of the whole launch
 // (Horner, located / per-entry fallback).  Parts may be enqueued on the
-// stream one by one, each behind its own copy.  prep_only: a part runs its
-// prep only, and the tail (after_prep) runs the sort and bucket stages over
-// the whole launch before Horner.
+// stream one by one, each behind its own copy.
 hipError_t launch_batch_check_part(bool sr, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg,
                                    const uint32_t *msg_off, uint32_t n, uint32_t e0, uint32_t e1, const fe *btab_q,
                                    const strobe_t *prefix, Ed25519Work w, MsmWork mw, const MsmParams &p,
-                                   const MsmSeed &seed, uint8_t *out, hipStream_t stream, bool prep_only = false);
+                                   const MsmSeed &seed, uint8_t *out, hipStream_t stream);
 hipError_t launch_batch_check_tail(bool sr, const uint8_t *pk, const uint8_t *sig, uint32_t n, const fe *btab_q,
                                    Ed25519Work w, MsmWork mw, const MsmParams &p, const MsmSeed &seed,
-                                   uint8_t *out, hipStream_t stream, bool after_prep = false);
+                                   uint8_t *out, hipStream_t stream);
 // Mixed batch through the batch equation: partition, then one pipeline per
 // kind (p: the ed25519 half's parameters, p_sr: the sr25519 half's); with
 // ks, the sr25519 pipeline runs on ks->helper (forked after the
@@ -126,9 +124,16 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
                                 const uint32_t *fail_list = nullptr, const uint32_t *fail_count = nullptr,
                                 const uint32_t *fb_list = nullptr, const uint32_t *fb_count = nullptr);
 // Default for MsmParams::sub: k_msm_subcheck runs before the per-entry
-// fallback for groups of 2^m_log2 (m >= 256; TMV_SUBCHECK=0 never, =1 always;
-// tmv_set_batch_options can override it per context).
+// fallback for groups of 2^m_log2 (m >= 256; tmv_set_batch_options can
+// override it per context).
 bool subcheck_enabled(uint32_t m_log2);
+// Test build (-DTMV_CHECKS) counters since the last reset: joins named by
+// k_msm_accum, joins done by k_msm_join_list, buckets with entries left
+// unwritten.  false in a product build.
+bool read_checks(uint32_t out[3], bool reset);
+// Test aid (tmv_internal_option "half_scalars"): 1 = the product's half-size
+// scalars, 0 = every entry on the full-k chain, 2 = every third entry.
+void set_half_scalar_mode(int mode);
 // Launches of at least this many entries use the located fallback
 // (TMV_LOCATE_MIN, 0 = never).
 uint32_t locate_min_entries();

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include "ed25519_core.h"
 #include "quad.h"
 #include "sr25519_core.h"
@@ -19,10 +20,6 @@
 #include "ktimer.h"
 
 namespace tmv {
-
-#ifndef TMV_DECODE_WAVES
-#define TMV_DECODE_WAVES 2  // 3 fits ed25519 decode in 168 VGPRs but spills 76 B/lane: measured slower
-#endif
 
 __global__ void __launch_bounds__(kVerifyBlock)
 k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
@@ -56,10 +53,8 @@ k_ed25519_verify(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig
 // k_prep stores -A in P3Q layout, R (ed25519: CachedQ; sr25519: P3Q) and k;
 // decode failures go to flags (4 bytes per entry: A ok, R ok, s ok, -).
 
-// Two kernels, so each gets its own register budget: k_prep_decode (lanes
-// [0, m) decode A, [m, 2m) decode R; 3 waves/SIMD for ed25519) and
-// k_prep_hash (one lane per entry: SHA-512 + Barrett, or the merlin
-// transcript).
+// Decode blocks (lanes [0, m) decode A, [m, 2m) decode R) and hash blocks
+// (one lane per entry: SHA-512 + Barrett, or the merlin transcript).
 template <bool SR>
 __device__ __forceinline__ void prep_decode_block(uint32_t bx, const uint8_t *__restrict__ pk,
                                                   const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
@@ -151,24 +146,10 @@ __device__ __forceinline__ void prep_hash_block(uint32_t bx, const uint8_t *__re
   }
 }
 
-template <bool SR>
-__global__ void __launch_bounds__(kVerifyBlock, SR ? 2 : TMV_DECODE_WAVES)
-k_prep_decode(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx,
-              const uint32_t *count_ptr, uint32_t n, Ed25519Work w, int aligned) {
-  prep_decode_block<SR>(blockIdx.x, pk, sig, idx, count_ptr, n, w, aligned);
-}
-
-template <bool SR>
-__global__ void __launch_bounds__(kVerifyBlock)
-k_prep_hash(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
-            const uint32_t *__restrict__ msg_off, const uint32_t *__restrict__ idx, const uint32_t *count_ptr,
-            uint32_t n, Ed25519Work w, const strobe_t *__restrict__ prefix, int aligned) {
-  prep_hash_block<SR>(blockIdx.x, pk, sig, msg, msg_off, idx, count_ptr, n, w, prefix, aligned);
-}
-
 // Both halves of the prep in one launch: blocks [0, dblocks) decode, the
-// rest hash, so the hash no longer waits behind the decode's sqrt chains
-// (the two kernels' register budgets are alike, 182 / 192 VGPRs).
+// rest hash, so the hash does not wait behind the decode's sqrt chains
+// (round 2, against two kernels: one 10k batch 1.047 -> 0.987 ms through the
+// batch equation, 0.546 -> 0.491 ms per entry).
 template <bool SR>
 __global__ void __launch_bounds__(kVerifyBlock)
 k_prep_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msg,
@@ -778,133 +759,10 @@ k_verify_comb(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ key_
 }
 
 // Latency form of the key-cached path (small batches: VerifyCommit).  The
-// comb sum needs k but not R, so one workgroup of two waves covers 16
-// signatures: wave 0 hashes (lane 4q for signature q), recodes and runs the
-// 96 comb additions per quad while lanes 0..15 of wave 1 decode the R's; the
-// waves meet once, for the final check (R through LDS).  The critical path
-// is max(hash + comb, R decode) instead of their sum.
-template <bool SR>
-__global__ void __launch_bounds__(2 * kQuadBlock)
-k_verify_cached_fused(const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
-                      const uint8_t *__restrict__ msg, const uint32_t *__restrict__ msg_off,
-                      const uint32_t *__restrict__ key_slot, uint32_t n, KeyTable kt, const fe *__restrict__ bcomb,
-                      const strobe_t *__restrict__ prefix, uint8_t *__restrict__ out, int aligned) {
-  __shared__ int8_t dig[kQuadSigs][2][64];
-  __shared__ fe Rs[kQuadSigs][4];
-  __shared__ uint8_t rok[kQuadSigs];
-  const uint32_t base = blockIdx.x * kQuadSigs;
-  if (base >= n) return;  // block-uniform
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave == 1) {
-    if (lane < kQuadSigs) {
-      const uint32_t i = min(base + lane, n - 1);
-      uint32_t r_w[8];
-      if (aligned) load_words_aligned(r_w, sig + 64ull * i);
-      else load_words_unaligned(r_w, sig + 64ull * i);
-      ge_p3 P;
-      const bool ok = SR ? ristretto_decode(P, r_w) : ge_decode_zip215(P, r_w);
-      if (!ok) ge_p3_identity(P);
-      rok[lane] = ok ? 1 : 0;
-      if (SR) {
-        Rs[lane][0] = P.X; Rs[lane][1] = P.Y;
-        fe t; fe_one(t); Rs[lane][2] = t;
-        Rs[lane][3] = P.T;
-      } else {  // CachedQ of R, negated by the final check
-        ge_cached cc;
-        ge_p3_to_cached(cc, P);
-        fe t;
-        fe_carry(t, cc.YmX); Rs[lane][0] = t;
-        fe_carry(t, cc.YpX); Rs[lane][1] = t;
-        Rs[lane][2] = cc.T2d;
-        Rs[lane][3] = cc.Z;
-      }
-    }
-    __syncthreads();
-    return;
-  }
-  const int c = lane & 3;
-  const int q = lane >> 2;
-  const uint32_t raw = base + q;
-  const bool live = raw < n;
-  const uint32_t i = live ? raw : n - 1;
-  uint32_t k_w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (c == 0) {
-    uint32_t a_w[8], r_w[8];
-    if (aligned) {
-      load_words_aligned(a_w, pk + 32ull * i);
-      load_words_aligned(r_w, sig + 64ull * i);
-    } else {
-      load_words_unaligned(a_w, pk + 32ull * i);
-      load_words_unaligned(r_w, sig + 64ull * i);
-    }
-    const uint32_t o0 = msg_off[i], o1 = msg_off[i + 1];
-    if constexpr (SR) {  // transcript state in LDS, one slot per quad
-      __shared__ uint64_t strobe_lanes[25][kQuadSigs];
-      sr25519_challenge_lds<kQuadSigs>(k_w, *prefix, &strobe_lanes[0][q], a_w, r_w, msg + o0, o1 - o0);
-    } else {
-      uint32_t h[16];
-      sha512_pq_msg(h, r_w, a_w, msg + o0, o1 - o0);
-      sc_reduce512(k_w, h);
-    }
-  }
-  uint32_t s_raw[8], s_w[8];
-  if (aligned) load_words_aligned(s_raw, sig + 64ull * i + 32);
-  else load_words_unaligned(s_raw, sig + 64ull * i + 32);
-  bool s_ok;
-  if (SR) {
-    s_ok = sr25519_decode_s(s_w, s_raw);
-  } else {
-#pragma unroll
-    for (int t = 0; t < 8; t++) s_w[t] = s_raw[t];
-    s_ok = sc_is_canonical(s_w);
-  }
-  if (!s_ok) s_w[7] &= 0x0fffffffu;
-  if (c == 1) recode256_store(&dig[q][1][0], s_w);
-  else if (c == 0) recode16_store(&dig[q][0][0], k_w, true);
-  // the digits were written by other lanes of this wave: order the LDS
-  // stores before the loads without waiting for the decoding wave
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const uint32_t slot = key_slot[i];
-  const bool a_ok = kt.ok[slot] != 0;
-  const fe *krow = kt.tab + (size_t)slot * kKeyRowsEntries * 4;
-  fe acc, r, idq;
-  quad::p3_identity(acc);
-  quad::cached_identity(idq);
-  auto entry_at = [&](int t, int &dsg) -> const fe * {
-    if (t < 64) {
-      dsg = dig[q][0][t];
-      const int a = dsg < 0 ? -dsg : dsg;
-      return krow + ((t * 8) + (a ? a - 1 : 0)) * 4 + c;
-    }
-    dsg = dig[q][1][t - 64];
-    const int a = dsg < 0 ? -dsg : dsg;
-    return bcomb + (((t - 64) * kBaseQuadEntries) + (a ? a - 1 : 0)) * 4 + c;
-  };
-  comb_accumulate<96>(acc, idq, entry_at);
-  __syncthreads();  // R decoded by wave 1
-  const bool r_ok = rok[q] != 0;
-  int status;
-  if (SR) {
-    const fe Rq = Rs[q][c];
-    const bool eq = quad::ristretto_equal(acc, Rq);
-    status = !a_ok ? -1 : (!s_ok ? -2 : (!r_ok ? 0 : (eq ? 1 : 0)));
-  } else {
-    fe Rq = Rs[q][c];
-    quad::cached_cneg(Rq, true);
-    quad::add(r, acc, Rq);
-    quad::p1p1_to_p3(acc, r);
-    status = (quad::is_identity_times8(acc) && s_ok && a_ok && r_ok) ? 1 : 0;
-  }
-  if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
-}
-
-// Four-wave latency form (TMV_FUSED_WAVES=4, default): the 96 comb additions
-// were one quad chain on wave 0 after the hash (the kernel's critical path,
-// ~40% longer than the R decode).  Now a workgroup of four waves covers 16
-// signatures: wave 1 decodes the R's as before; wave 2 runs the 32 base-comb
+// comb sum needs k but not R, so the work of 16 signatures is spread over a
+// workgroup of four waves (round 3's two-wave form ran the 96 comb additions
+// as one quad chain after the hash, ~40% longer than the R decode): wave 1
+// decodes the R's; wave 2 runs the 32 base-comb
 // additions (s is known at once); waves 0 and 3 each hash (the same SHA-512 /
 // transcript, computed twice so neither waits for the other) and run half of
 // the 64 key-comb additions; wave 0 then adds the other partial sums (LDS)
@@ -1064,16 +922,6 @@ k_verify_cached_fused4(const uint8_t *__restrict__ pk, const uint8_t *__restrict
   if (live && c == 0) out[i] = (uint8_t)(int8_t)status;
 }
 
-// Waves per fused latency workgroup (TMV_FUSED_WAVES: 4 = k_verify_cached_fused4,
-// 2 = k_verify_cached_fused).
-static int fused_waves() {
-  static const int v = [] {
-    const char *e = getenv("TMV_FUSED_WAVES");
-    return (e && atoi(e) == 2) ? 2 : 4;
-  }();
-  return v;
-}
-
 hipError_t launch_key_build(bool sr, const uint8_t *keys, const uint32_t *slots, uint32_t m, KeyTable kt,
                             fe *bases, hipStream_t stream) {
   if (m == 0) return hipSuccess;
@@ -1095,17 +943,10 @@ hipError_t launch_verify_cached(bool sr, const uint8_t *pk, const uint8_t *sig, 
   const int aligned = ((((uintptr_t)pk) | ((uintptr_t)sig)) & 15) == 0;
   if (n <= fused_max) {  // latency-bound: one fused kernel
     const uint32_t blocks = (n + kQuadSigs - 1) / kQuadSigs;
-    if (fused_waves() == 4) {
-      if (sr) hipLaunchKernelGGL(k_verify_cached_fused4<true>, dim3(blocks), dim3(4 * kQuadBlock), 0, stream, pk, sig,
-                                 msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
-      else hipLaunchKernelGGL(k_verify_cached_fused4<false>, dim3(blocks), dim3(4 * kQuadBlock), 0, stream, pk, sig,
-                              msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
-    } else {
-      if (sr) hipLaunchKernelGGL(k_verify_cached_fused<true>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig,
-                                 msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
-      else hipLaunchKernelGGL(k_verify_cached_fused<false>, dim3(blocks), dim3(2 * kQuadBlock), 0, stream, pk, sig,
-                              msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
-    }
+    if (sr) hipLaunchKernelGGL(k_verify_cached_fused4<true>, dim3(blocks), dim3(4 * kQuadBlock), 0, stream, pk, sig,
+                               msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
+    else hipLaunchKernelGGL(k_verify_cached_fused4<false>, dim3(blocks), dim3(4 * kQuadBlock), 0, stream, pk, sig,
+                            msg, msg_off, key_slot, n, kt, bcomb, prefix, out, aligned);
     return hipGetLastError();
   }
   w.niels = nullptr;
@@ -1162,31 +1003,17 @@ template hipError_t launch_comb_fallback<true>(const uint8_t *, const uint32_t *
 // every block exits at once, and the 22.5 KB of LDS a block holds only caps
 // how fast the grid drains: global there (C2 bench, profiles/r02_close/
 // ab_quad_fallback.txt: 101.5 / 101.8 -> 102.8 / 102.5 M/s), LDS for the
-// per-entry pipeline.  TMV_QUAD_TABLE=global|lds forces one.
-static int quad_table_env() {
-  static const int g = [] {
-    const char *e = getenv("TMV_QUAD_TABLE");
-    return !e ? 0 : !strcmp(e, "global") ? 1 : !strcmp(e, "lds") ? 2 : 0;
-  }();
-  return g;
-}
-
-// Half-size scalars in the per-entry checks (halfscalar.h); TMV_HALF_SCALARS=0
-// verifies with the full k, =2 (tests) puts every third entry on the full-k
-// path beside half-size quads of the same wave (read at every launch, so
-// tests can compare the modes in one process).
-static int half_scalars_on() {
-  const char *e = getenv("TMV_HALF_SCALARS");
-  return !e ? 1 : !strcmp(e, "0") ? 0 : !strcmp(e, "2") ? 2 : 1;
-}
-
-// Per-entry pipeline: the half-size scalars reduced once per entry by the
-// prep's hash lane (default) or by every lane of the entry's quad
-// (TMV_HALF_PREP=0; read at every launch, for A/B).
-static bool half_prep_on() {
-  const char *e = getenv("TMV_HALF_PREP");
-  return !(e && !strcmp(e, "0"));
-}
+// per-entry pipeline while its grid fits that residency.
+//
+// Half-size scalars in the per-entry checks (halfscalar.h): mode 1 (the
+// product).  Test aid (tmv_internal_option "half_scalars", never set by a
+// deployment): 0 verifies every entry with the full k, 2 puts every third
+// entry on the full-k path beside half-size quads of the same wave -- the
+// path an entry whose reduction does not finish (~2^-24 of hash outputs)
+// takes, which random tests would otherwise never reach.
+static std::atomic<int> g_half_mode{1};
+void set_half_scalar_mode(int mode) { g_half_mode = mode == 0 || mode == 2 ? mode : 1; }
+static int half_scalars_on() { return g_half_mode.load(std::memory_order_relaxed); }
 
 template <bool SR>
 static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig, const uint32_t *idx,
@@ -1195,11 +1022,10 @@ static void launch_quad(uint32_t qblocks, hipStream_t stream, const uint8_t *sig
                         const uint8_t *sub_ok = nullptr, const uint32_t *fail_list = nullptr,
                         const uint32_t *fail_count = nullptr, const uint32_t *fb_list = nullptr,
                         const uint32_t *fb_count = nullptr, bool fallback = false) {
-  const int forced = quad_table_env();
   const int half = half_scalars_on();
   // LDS tables hold 40 KB per wave (3 waves per CU): only while the grid fits
   // that residency, else global
-  const bool global = forced == 1 || (forced == 0 && (fallback || qblocks > 3u * 256u));
+  const bool global = fallback || qblocks > 3u * 256u;
   if (global)
     hipLaunchKernelGGL((k_verify_quad<SR, true>), dim3(qblocks), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n,
                        w, btab_q, out, aligned, group_ok, group_log2, sub_ok, fail_list, fail_count, fb_list,
@@ -1221,7 +1047,7 @@ static hipError_t launch_pipeline(const uint8_t *pk, const uint8_t *sig, const u
                                   uint8_t *out, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const int aligned = is_aligned(pk, sig);
-  w.hs = half_prep_on() ? w.hs_buf : nullptr;
+  w.hs = w.hs_buf;  // the prep's hash lane reduces k once per entry (10k launch 0.331 -> 0.299 ms, round 5)
   hipError_t e = launch_prep<SR>(pk, sig, msg, msg_off, idx, count_ptr, n, prefix, w, aligned, stream);
   if (e != hipSuccess) return e;
   const uint32_t qblocks = (n + kQuadSigs - 1) / kQuadSigs;
@@ -1242,7 +1068,7 @@ hipError_t launch_quad_fallback(const uint8_t *sig, const uint32_t *idx, const u
   const uint32_t qblocks = fb_list ? (n + kQuadSigs - 1) / kQuadSigs
                            : fail_list ? ((((n + (1u << group_log2) - 1) >> group_log2)) << (group_log2 - 4))
                                        : (n + kQuadSigs - 1) / kQuadSigs;
-  if (fb_list && quad_table_env() != 2) {
+  if (fb_list) {
     // at most 16 waves per CU (the kernel fits 5 per SIMD); blocks stride over the list
     const uint32_t grid = qblocks < 256u * 16u ? qblocks : 256u * 16u;
     hipLaunchKernelGGL(k_verify_quad_list<SR>, dim3(grid), dim3(kQuadBlock), 0, stream, sig, idx, count_ptr, n, w,
@@ -1262,39 +1088,18 @@ template hipError_t launch_quad_fallback<true>(const uint8_t *, const uint32_t *
                                                hipStream_t, const uint8_t *, const uint32_t *, const uint32_t *,
                                                const uint32_t *, const uint32_t *);
 
-// Decode and hash blocks in one launch (default; TMV_PREP_FUSED=0: two
-// kernels).  Measured in one GPU call (round 2): one 10k batch
-// 1.047 -> 0.987 ms through the batch equation, 0.546 -> 0.491 ms per entry;
-// the 32-batch bench unchanged (77.1-77.8 M/s either way).
-static bool prep_fused() {
-  static const bool on = [] {
-    const char *e = getenv("TMV_PREP_FUSED");
-    return !(e && !strcmp(e, "0"));
-  }();
-  return on;
-}
-
 template <bool SR>
 hipError_t launch_prep(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
                        const uint32_t *idx, const uint32_t *count_ptr, uint32_t n, const strobe_t *prefix,
                        Ed25519Work w, int aligned, hipStream_t stream) {
   const uint32_t dblocks = (uint32_t)((2ull * n + kVerifyBlock - 1) / kVerifyBlock);
   const uint32_t hblocks = (n + kVerifyBlock - 1) / kVerifyBlock;
-  if (prep_fused()) {
-    void *tk = ktimer::begin(ktimer::kPrep, stream);
-    hipLaunchKernelGGL(k_prep_fused<SR>, dim3(dblocks + hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off,
-                       idx, count_ptr, n, w, prefix, aligned, dblocks);
-    const hipError_t e = hipGetLastError();
-    ktimer::end(tk, stream);
-    return e;
-  }
-  hipLaunchKernelGGL(k_prep_decode<SR>, dim3(dblocks), dim3(kVerifyBlock), 0, stream, pk, sig, idx, count_ptr, n, w,
-                     aligned);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_prep_hash<SR>, dim3(hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off, idx,
-                     count_ptr, n, w, prefix, aligned);
-  return hipGetLastError();
+  void *tk = ktimer::begin(ktimer::kPrep, stream);
+  hipLaunchKernelGGL(k_prep_fused<SR>, dim3(dblocks + hblocks), dim3(kVerifyBlock), 0, stream, pk, sig, msg, msg_off,
+                     idx, count_ptr, n, w, prefix, aligned, dblocks);
+  const hipError_t e = hipGetLastError();
+  ktimer::end(tk, stream);
+  return e;
 }
 template hipError_t launch_prep<false>(const uint8_t *, const uint8_t *, const uint8_t *, const uint32_t *,
                                        const uint32_t *, const uint32_t *, uint32_t, const strobe_t *, Ed25519Work,

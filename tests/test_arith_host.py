@@ -200,7 +200,7 @@ def test_sr25519_transcript_fast_path(H):
 
 
 def test_p1p1_to_cached_matches_two_step(H):
-    """ge_p1p1_to_cached (k_msm_wpart's U, TMV_WPART_CACHED_U) equals
+    """ge_p1p1_to_cached (k_msm_wpart's cached U, one lane per window) equals
     p1p1_to_p3 followed by p3_to_cached, coordinate by coordinate."""
     import random
     rng = random.Random(1717)

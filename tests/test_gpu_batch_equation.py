@@ -472,10 +472,11 @@ def _bisect_case(kind, m, n=150_000 + 91):
     return b, sig, bad
 
 
-def _bisect_expect(bad, n, m):
-    """(located, one-by-one) the bisection gives: a group with one bad entry
-    names it; with more, each half names its one bad entry, or is verified
-    whole when it holds two or more (a clean half costs nothing)."""
+def _located_expect(bad, n, m):
+    """(located, one-by-one) the located fallback gives: a failing group with
+    one bad entry names it (one verification); a group with two or more is
+    verified whole (its live entries).  (Round 5's bisection of such groups
+    and the sub-group checks were measured slower and removed.)"""
     groups = {}
     for i in bad:
         groups.setdefault(i // m, []).append(i)
@@ -484,30 +485,18 @@ def _bisect_expect(bad, n, m):
         if len(es) == 1:
             located += 1
             fallback += 1
-            continue
-        lo_g, h = g * m, m // 2
-        for lo in (lo_g, lo_g + h):
-            hi = min(lo + h, n)
-            k = sum(lo <= i < hi for i in es)
-            if k == 1:
-                located += 1
-                fallback += 1
-            elif k >= 2:
-                fallback += hi - lo
+        else:
+            fallback += min(m, n - g * m)
     return located, fallback
 
 
 @pytest.mark.parametrize("kind,m_log2", [(ED, 7), (ED, 8), (SR, 6)], ids=["ed-128", "ed-256", "sr-64"])
-def test_located_bisection(bctx, kind, m_log2, monkeypatch):
-    """TMV_LOC_BISECT_MIN (off by default: measured slower; 150k here, read at
-    every launch):
-    the groups the located search cannot name are bisected -- the first
-    half's sums T1, T1' by a second MSM, the second half's as differences --
-    and each half names its one bad entry or, with two or more, is verified
-    one by one.  tmv_metrics counts exactly the entries the rule implies, and
-    the vector equals the oracle's."""
+def test_located_two_bad_groups(bctx, kind, m_log2, monkeypatch):
+    """The located fallback (TMV_LOCATE_MIN, 150k here, read at every launch)
+    on groups holding one, two or more bad entries: tmv_metrics counts
+    exactly the entries the rule implies (_located_expect), and the vector
+    equals the oracle's."""
     monkeypatch.setenv("TMV_LOCATE_MIN", "150000")
-    monkeypatch.setenv("TMV_LOC_BISECT_MIN", "150000")
     m = 1 << m_log2
     b, sig, bad = _bisect_case(kind, m)
     n = b.n
@@ -526,58 +515,18 @@ def test_located_bisection(bctx, kind, m_log2, monkeypatch):
         ref = C.sr25519_status_packed(b.pk, sig, b.msg, b.off, threads=16)
         assert np.array_equal(st, ref)
         assert int((ref != 1).sum()) == len(bad)
-    located, fallback = _bisect_expect(bad, n, m)
+    located, fallback = _located_expect(bad, n, m)
     assert met["groups_failed"] == len({i // m for i in bad})
     assert (met["located_groups"], met["fallback_signatures"]) == (located, fallback), met
 
 
-LOC_SUB = r"""
-import sys, numpy as np
-sys.path.insert(0, '.'); sys.path.insert(0, 'oracle'); sys.path.insert(0, 'tests')
-import oracle_c as C
-from tendermint_amd import _native as N
-from test_gpu_batch_equation import _located_case
-ctx = N.Context(1)
-b, sig, singles, pairs = _located_case(m=128)
-ctx.set_batch_options(group_log2=7, window_bits=6, seed=bytes(range(32)), stats=True)
-ctx.metrics_reset()
-ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, b.pk, sig, b.msg, b.off)
-met = ctx.metrics()
-ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)
-assert ok == ok_o and np.array_equal(st.astype(np.uint8), ref)
-assert met["located_groups"] == len(singles)
-subs = {i // 8 for p in pairs for i in p}  # failing 8-entry sub-groups of the two-bad groups
-assert met["fallback_signatures"] == len(singles) + sum(min(8, b.n - 8 * s) for s in subs), met
-print("ok")
-"""
-
-
-def test_located_then_subgroups_option():
-    """TMV_LOC_SUBCHECK=1 (measured slower, off by default): the groups the
-    located search cannot name are checked by 8-entry sub-groups, and only
-    the entries of their failing sub-groups are verified one by one; the
-    vector equals the oracle's."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, TMV_LOC_SUBCHECK="1", TMV_LOCATE_MIN="150000")
-    out = subprocess.run([sys.executable, "-c", LOC_SUB], cwd=root, env=env, capture_output=True, text=True,
-                         timeout=600)
-    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
-    assert "ok" in out.stdout
-
-
-@pytest.mark.parametrize("help_on,prep_on", [("0", "1"), ("1", "0"), ("0", "0")])
 @pytest.mark.parametrize("kind", [ED, SR])
-def test_chain_knobs(bctx, kind, help_on, prep_on, monkeypatch):
-    """The round-5 paths beside their switched-off forms (defaults: both on;
-    both read at every launch): TMV_HORNER_HELP (helper workgroups reduce
-    every entry's k during the batch equation's Horner, below the located
-    size) and TMV_HALF_PREP (the per-entry pipeline's k reduced once by the
-    prep's hash lane).  Each setting gives the oracle's vector through the
-    batch equation (failing groups re-verified one by one) and per entry."""
-    monkeypatch.setenv("TMV_HORNER_HELP", help_on)
-    monkeypatch.setenv("TMV_HALF_PREP", prep_on)
+def test_chain_paths(bctx, kind):
+    """One case through both chains of round 5: the batch equation (its
+    Horner beside the helper workgroups that reduce every entry's k, then the
+    failing groups re-verified one by one) and the per-entry pipeline (k
+    reduced once by the prep's hash lane) -- each gives the oracle's vector.
+    (Their switched-off forms were A/B knobs, now in -DTMV_AB builds only.)"""
     b, sig, bad = _bisect_case(kind, 64, n=20_000 + 37)
     if kind == ED:
         ok_o, ref = C.ed25519_verify_packed(b.pk, sig, b.msg, b.off, threads=16)

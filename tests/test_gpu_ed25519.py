@@ -106,21 +106,18 @@ def test_unaligned_device_path(ctx):
     assert np.array_equal(out.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("kernel", ["single", "quad"])
-def test_both_kernels_c2_subprocess(kernel, golden):
-    """Each kernel (TMV_KERNEL override) reproduces the C2 vector bit for bit."""
-    import os
-    import subprocess
-    import sys
-    code = (
-        "import numpy as np, sys; sys.path.insert(0, '.');"
-        "from tendermint_amd import _native as N;"
-        "from tendermint_amd.testing.factory import make_c2_batch;"
-        "b = make_c2_batch(); ok, v = N.Context(1).ed25519_verify_batch(b.pk, b.sig, b.msg, b.off);"
-        "print(np.packbits(v.astype(np.uint8), bitorder='little').tobytes().hex())")
-    env = dict(os.environ, TMV_KERNEL=kernel)
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
-                         timeout=300)
-    assert out.returncode == 0, out.stderr
-    assert out.stdout.strip().splitlines()[-1] == golden("c2_expected.json")["valid_bits_hex"]
+@pytest.mark.parametrize("tiles", [1, 6], ids=["quad", "single"])
+def test_both_kernels_c2(ctx, golden, tiles):
+    """Per-entry verification picks its kernel by size: up to 49,152 entries
+    the quad kernel (4 lanes per signature), above it the single-lane one.
+    The C2 batch once (quad) and tiled 6x = 60k entries (single lane): every
+    tile reproduces the committed C2 vector bit for bit."""
+    from tendermint_amd import _native as N
+    from tendermint_amd.testing.factory import Batch
+    b1 = make_c2_batch()
+    b = Batch.concat([b1] * tiles)
+    _, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_PER_ENTRY, b.pk, b.sig, b.msg, b.off)
+    want = golden("c2_expected.json")["valid_bits_hex"]
+    for t in range(tiles):
+        v = (st[t * b1.n:(t + 1) * b1.n] == 1).astype(np.uint8)
+        assert np.packbits(v, bitorder="little").tobytes().hex() == want, t

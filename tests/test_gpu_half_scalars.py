@@ -5,9 +5,11 @@ validity bit for every input.  Every path that runs the per-entry kernels --
 the per-entry pipeline with LDS tables (<= 12,288 entries) and with global
 tables, the batch equation's compacted fallback of failing groups, the
 located fallback's entry list (launches >= TMV_LOCATE_MIN entries) -- is compared with
-the C oracle in three modes: TMV_HALF_SCALARS=1 (the default), 0 (the full
-253-bit k, the rounds 1-4 check) and 2 (every third entry on the full-k path
-beside half-size quads of the same wave)."""
+the C oracle in three modes, set through the library's test hook
+(tmv_internal_option "half_scalars"): 1 (the product), 0 (the full 253-bit
+k, the rounds 1-4 check, which an entry whose reduction does not finish
+takes) and 2 (every third entry on the full-k path beside half-size quads of
+the same wave)."""
 import numpy as np
 import pytest
 
@@ -29,6 +31,22 @@ def _edge_batch(golden):
     return C.pack(ents)
 
 
+@pytest.fixture
+def half_mode():
+    """The half-size scalar mode through the library's test hook
+    (tmv_internal_option "half_scalars": 1 = the product, 0 = every entry on
+    the full-k chain, 2 = every third entry); reset to 1 afterwards."""
+    import ctypes
+    L = N.lib()
+    L.tmv_internal_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+
+    def set_mode(mode):
+        assert L.tmv_internal_option(b"half_scalars", int(mode)) == 0
+
+    yield set_mode
+    set_mode(1)
+
+
 @pytest.fixture(scope="module")
 def c2_mix():
     """The edge vectors ahead of 3 C2 batches' worth of entries (3,300)."""
@@ -36,8 +54,8 @@ def c2_mix():
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_ed25519_per_entry_and_fallback(ctx, golden, c2_mix, mode, monkeypatch):
-    monkeypatch.setenv("TMV_HALF_SCALARS", mode)
+def test_ed25519_per_entry_and_fallback(ctx, golden, c2_mix, mode, half_mode, monkeypatch):
+    half_mode(mode)
     pk, sig, msg, off = _edge_batch(golden)
     _, want = C.ed25519_verify_packed(pk, sig, msg, off)
     for flags in (N.TMV_FLAG_PER_ENTRY, N.TMV_FLAG_BATCH_EQUATION):
@@ -53,10 +71,10 @@ def test_ed25519_per_entry_and_fallback(ctx, golden, c2_mix, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ("1", "2"))
-def test_ed25519_per_entry_global_tables(ctx, mode, monkeypatch):
+def test_ed25519_per_entry_global_tables(ctx, mode, half_mode, monkeypatch):
     """20k entries per entry: more than 768 quad blocks, so the -A / -R tables
     live in global memory (GT) outside the fallback too."""
-    monkeypatch.setenv("TMV_HALF_SCALARS", mode)
+    half_mode(mode)
     b = Batch.concat([make_c2_batch(10_000, seed=0xB0 + j) for j in range(2)])
     _, want = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=16)
     _, got = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_PER_ENTRY, b.pk, b.sig, b.msg, b.off)
@@ -64,10 +82,10 @@ def test_ed25519_per_entry_global_tables(ctx, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_sr25519_statuses(ctx, mode, monkeypatch):
+def test_sr25519_statuses(ctx, mode, half_mode, monkeypatch):
     """sr25519 (and mixed) statuses 1 / 0 / -1 / -2 per entry and through the
     batch equation's fallback, against the C oracle."""
-    monkeypatch.setenv("TMV_HALF_SCALARS", mode)
+    half_mode(mode)
     kind, mb = make_mixed_batch(4000, seed=0x77)
     ed, sr = np.flatnonzero(kind == 0), np.flatnonzero(kind == 1)
     want = np.zeros(mb.n, np.int8)
@@ -84,10 +102,10 @@ def test_sr25519_statuses(ctx, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ("1", "2"))
-def test_located_fallback_list(ctx, mode, monkeypatch):
+def test_located_fallback_list(ctx, mode, half_mode, monkeypatch):
     """A 160k-entry C2-shaped launch runs the located fallback: its entry
     list goes through k_verify_quad_list (global tables, grid-stride)."""
-    monkeypatch.setenv("TMV_HALF_SCALARS", mode)
+    half_mode(mode)
     monkeypatch.setenv("TMV_LOCATE_MIN", "150000")  # 160k entries: the located pass
     base = [make_c2_batch(10_000, seed=0xC0 + j) for j in range(4)]
     want1 = [C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=16)[1] for b in base]

@@ -154,32 +154,3 @@ print("ok", s)
         assert out.returncode == 0, (cap, out.stderr[-2000:])
         assert "ok" in out.stdout
 
-
-def test_fused_two_wave_form_matches_oracle():
-    """TMV_FUSED_WAVES=2 keeps the round-3 two-wave fused latency kernel
-    (hash + 96 comb additions on one wave beside the R decode); it must give
-    the oracle's vectors as the four-wave default does."""
-    code = r"""
-import sys, numpy as np
-sys.path.insert(0, '.'); sys.path.insert(0, 'oracle')
-import oracle_c as C
-from tendermint_amd import _native as N
-from tendermint_amd.testing.factory import make_c2_batch, make_sr25519_batch
-ctx = N.Context(1)
-b = make_c2_batch(700, seed=38, edge_scale=6.0)
-_, ref = C.ed25519_verify_packed(b.pk, b.sig, b.msg, b.off, threads=4)
-for _ in range(2):
-    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_KEY_CACHE, b.pk, b.sig, b.msg, b.off)
-    assert np.array_equal(st.astype(np.uint8), ref)
-s = make_sr25519_batch(300, seed=39, bad_frac=0.05)
-ref = C.sr25519_status_packed(s.pk, s.sig, s.msg, s.off, threads=4)
-ok, st = ctx.verify_batch_ex(N.TMV_KIND_SR25519, N.TMV_FLAG_KEY_CACHE, s.pk, s.sig, s.msg, s.off)
-assert np.array_equal(st, ref)
-print("ok")
-"""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, TMV_FUSED_WAVES="2")
-    out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
-                         timeout=300)
-    assert out.returncode == 0, out.stderr[-2000:]
-    assert "ok" in out.stdout

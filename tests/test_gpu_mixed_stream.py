@@ -2,9 +2,10 @@
 mixed_check_streamed): the caller's pages DMA'd part by part, each part split
 by key kind on the device into the two kinds' work-slot lists at bases the
 host counted, each kind's pipeline running the groups the parts complete,
-one tail per kind.  The statuses must equal the C oracle's and the
-unstreamed path's (TMV_MIXED_STREAM=0) for every layout of kinds over the
-parts: runs of one kind longer than a part (a kind absent from whole parts,
+one tail per kind.  The statuses must equal the C oracle's for every
+layout of kinds over the parts (the unstreamed host path is an A/B variant
+now, -DTMV_AB builds only; the device-resident mixed path is tested in
+test_gpu_configs.py): runs of one kind longer than a part (a kind absent from whole parts,
 groups spanning parts), alternating kinds, unknown kinds (status 0) and a
 kind absent altogether (crypto/batch/batch.go:11-21 mixed batches)."""
 import numpy as np
@@ -58,35 +59,28 @@ def test_mixed_streamed_vs_oracle(ctx, base, layout, monkeypatch):
         want[::997] = 0
     for lmin in ("150000", "400000"):  # each kind's half with and without the located fallback
         monkeypatch.setenv("TMV_LOCATE_MIN", lmin)
-        for mode in ("1", "0"):
-            monkeypatch.setenv("TMV_MIXED_STREAM", mode)
-            _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
-            got = np.asarray(st, np.int8)
-            bad = np.flatnonzero(got != want)
-            assert not len(bad), (f"{layout}, TMV_MIXED_STREAM={mode} TMV_LOCATE_MIN={lmin}: entries {bad[:8]}: "
-                                  f"{got[bad[:8]]} vs {want[bad[:8]]}")
+        _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
+        got = np.asarray(st, np.int8)
+        bad = np.flatnonzero(got != want)
+        assert not len(bad), (f"{layout}, TMV_LOCATE_MIN={lmin}: entries {bad[:8]}: "
+                              f"{got[bad[:8]]} vs {want[bad[:8]]}")
 
 
 def test_mixed_streamed_stats(ctx, base, monkeypatch):
     """The batch statistics see both kinds' groups on the streamed path (the
-    partition's device counts), as on the unstreamed one: ed25519 in groups
-    of 64 streamed (tmverify_runtime.cpp make_opts: p_ed_streamed), of 128
-    unstreamed (>= TMV_LOCATE_MIN entries, 150k here), sr25519 in groups of
-    64."""
+    partition's device counts): ed25519 in groups of 64 streamed
+    (tmverify_runtime.cpp make_opts: p_ed_streamed, even at >= TMV_LOCATE_MIN
+    entries, 150k here), sr25519 in groups of 64."""
     monkeypatch.setenv("TMV_LOCATE_MIN", "150000")
     kind, mb, _ = base
     idx = np.arange(300_000) % mb.n
     hb = mb.take(idx)
     kinds = np.ascontiguousarray(kind[idx])
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("TMV_MIXED_STREAM", mode)
-        ctx.set_batch_options(stats=True)
-        g0 = ctx.batch_stats()["groups"]
-        ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
-        out[mode] = ctx.batch_stats()["groups"] - g0
-        ctx.set_batch_options()
+    ctx.set_batch_options(stats=True)
+    g0 = ctx.batch_stats()["groups"]
+    ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
+    groups = ctx.batch_stats()["groups"] - g0
+    ctx.set_batch_options()
     n_ed, n_sr = int(np.sum(kinds == 0)), int(np.sum(kinds == 1))
     g = lambda k, m: (k + m - 1) // m  # noqa: E731
-    assert out["1"] == g(n_ed, 64) + g(n_sr, 64), out
-    assert out["0"] == g(n_ed, 128) + g(n_sr, 64), out
+    assert groups == g(n_ed, 64) + g(n_sr, 64), groups

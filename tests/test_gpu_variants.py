@@ -1,8 +1,11 @@
-"""Kernel-variant overrides (A/B knobs) must keep the oracle's vector: the
-single-lane kernel, global-memory quad tables, accumulation chunk lengths,
-and a large host batch (4M signatures, chunked over both lanes) whose
-honest entries must all pass.  Each variant runs in its own process (the
-knobs are read once)."""
+"""The production knobs' thresholds move entries between
+paths; every setting must keep the oracle's vector: the batch equation never
+(TMV_MSM_MIN=0), the key-cached batches never on the fused latency kernel
+(TMV_CACHED_FUSED_MAX=0), the located fallback for every launch
+(TMV_LOCATE_MIN=1); and a large host batch (4M signatures, chunked over both
+lanes) whose honest entries must all pass.  Each setting runs in its own
+process (the knobs are read once).  The A/B switches (knobs.h) exist only in
+-DTMV_AB builds; tools/gpu_ab_so.sh runs the GPU tests on such builds."""
 import os
 import subprocess
 import sys
@@ -33,9 +36,8 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"TMV_KERNEL": "single"}, {"TMV_QUAD_TABLE": "global"}, {"TMV_QUAD_TABLE": "lds"},
-                                 {"TMV_MSM_CHUNK": "8"},
-                                 {"TMV_MSM_CHUNK": "32"}, {"TMV_KERNEL": "quad", "TMV_MSM_MIN": "0"}])
+@pytest.mark.parametrize("env", [{}, {"TMV_MSM_MIN": "0"}, {"TMV_CACHED_FUSED_MAX": "0"}, {"TMV_LOCATE_MIN": "1"}],
+                         ids=["default", "msm-min-0", "fused-max-0", "locate-min-1"])
 def test_variant_matches_oracle(env):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", CODE], env=dict(os.environ, **env), cwd=root, capture_output=True,
