@@ -442,7 +442,18 @@ def _kernel_fracs():
         return {}
 
 
-def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method, n_launch=0, ms_per_step=0.0):
+def _profile_build(d, build_digest):
+    """(same_build, note) for a committed profile d: its executed counts
+    describe this run's kernels only when it was taken on a library with
+    this run's compiled source digest."""
+    src = (d.get("source") or {}).get("src_digest") if isinstance(d.get("source"), dict) else d.get("src_digest")
+    if src and build_digest and src == build_digest:
+        return True, f"profile of this build (src={src})"
+    return False, (f"ESTIMATE: the committed profile was taken on build src={src or 'unrecorded'}, this run's "
+                   f"library is src={build_digest or 'unknown'}; the counts may not describe these kernels")
+
+
+def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method, n_launch=0, ms_per_step=0.0, build_digest=None):
     """The whole pipeline.  executed_mad_frac: the v_mad_i64_i32 lane-ops one
     launch of this size executes (PMC SQ_INSTS_VALU_INT64 per kernel x its
     static v_mad_i64_i32 share, tools/isa_mix.py; committed pass at this
@@ -473,11 +484,13 @@ def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method, n_launch=0, ms_pe
         mads = sum(k["int64_lane_ops"] * k["mad_share_static"] for k in L["kernels"].values()
                    if "int64_lane_ops" in k)
         if mads and ms_per_step:
-            out["executed_mad_frac"] = round(mads / (ms_per_step * 1e-3) / peak, 4)
+            same, prov = _profile_build(kf, build_digest)
+            key = "executed_mad_frac" if same else "executed_mad_frac_estimate"
+            out[key] = round(mads / (ms_per_step * 1e-3) / peak, 4)
             out["executed_mad_note"] = (f"{mads:.4g} v_mad_i64_i32 lane-ops per launch of {n_launch} signatures (PMC "
                                         "SQ_INSTS_VALU_INT64 x 64 lanes x each kernel's static v_mad_i64_i32 share, "
                                         f"{KFRACS_FILE}) / this run's ms_per_step / peak; the same launch alone: "
-                                        f"{L.get('pipeline_executed_mad_frac')}")
+                                        f"{L.get('pipeline_executed_mad_frac')}; {prov}")
     if kf:
         out["kernel_fracs"] = {
             str(L["n"]): {"launch_span_us": L["launch_span_us"], "verifies_per_s": L["verifies_per_s"],
@@ -526,7 +539,7 @@ def _isa_mix():
     return None
 
 
-def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, ms_per_step):
+def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, ms_per_step, build_digest=None):
     """roofline for the dominant kernel, k_msm_accum<16> (bucket sums; the
     largest share of the pipeline's VALU work): its algorithmic products per
     launch (SURVEY 8(d)'s per-unit work: one mixed addition = 7 field
@@ -584,11 +597,12 @@ def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, 
         # against the v_mad_i64_i32 peak (the carry adds / shifts are other
         # instructions): PMC INT64 lane-ops x the kernel's static mad share
         mads = ex * mix["mad_share_of_int64"]
-        r["executed_mad_frac"] = round(mads / (own_ms * 1e-3) / peak, 4)
+        same, prov = _profile_build(dfile, build_digest)
+        r["executed_mad_frac" if same else "executed_mad_frac_estimate"] = round(mads / (own_ms * 1e-3) / peak, 4)
         r["executed_note"] = (f"PMC SQ_INSTS_VALU_INT64 lane-ops per launch (profiled at {prof_k} batches per launch) "
                               f"x the kernel's static v_mad_i64_i32 share of its 64-bit VALU instructions "
                               f"({mix['mad_share_of_int64']}, {mix['source']}) / own duration / peak "
-                              "v_mad_i64_i32 rate")
+                              f"v_mad_i64_i32 rate; {prov}")
     return r
 
 
@@ -775,6 +789,8 @@ def main():
             if world > 1:  # the gathered vector holds every rank's copy of this launch
                 assert gathered[f].numel() == world * kk * n
         first += kk
+    build_digest = None if stub else (N.build_info() or {}).get("src_digest_compiled")
+
     def max_over_ranks(x):
         if world == 1:
             return x
@@ -1079,11 +1095,12 @@ def main():
                                    "batches, context / workspaces, warmup); device memory = total - free on the "
                                    "rank's GPU after the timed region (every process on that GPU)"},
             **extras,
-            "roofline": _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, args.method, K * n, elapsed / steps * 1e3),
+            "roofline": _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, args.method, K * n, elapsed / steps * 1e3,
+                                           build_digest),
         }
         if ktimes.get("k_msm_accum", (0, 0))[1] and args.method == "batch":
             result["roofline"] = _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps,
-                                                    result["roofline"], elapsed / steps * 1e3)
+                                                    result["roofline"], elapsed / steps * 1e3, build_digest)
         if "end_to_end_verifies_per_s" in result:
             result["end_to_end_vs_headline"] = round(result["end_to_end_verifies_per_s"] / value, 4)
         if not stub:

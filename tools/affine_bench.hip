@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   fe u[K], v[K], c[K];
 #pragma unroll
   for (int j = 0; j < K; j++) {
-    const uint32_t i = mix(t * 31u + j) & (kTable - 1);
+    const uint32_t i = mix(t * 31u + (uint32_t)j + 0x9e3779b9u) & (kTable - 1);
     u[j] = tab[2 * i];
     v[j] = tab[2 * i + 1];
   }
@@ -188,7 +188,7 @@ int host_check(const std::vector<fe> &tab, const std::vector<fe> &dev_u0) {
   int bad = 0;
   for (uint32_t t = 0; t < 64; t++) {
     for (int j = 0; j < 4; j++) {
-      const uint32_t i0 = mix(t * 31u + j) & (kTable - 1), i1 = mix(t * 977u + (uint32_t)j) & (kTable - 1);
+      const uint32_t i0 = mix(t * 31u + (uint32_t)j + 0x9e3779b9u) & (kTable - 1), i1 = mix(t * 977u + (uint32_t)j) & (kTable - 1);
       fe u = tab[2 * i0], v = tab[2 * i0 + 1], du, inv;
       fe_sub(du, tab[2 * i1], u);
       fe_carry(du, du);
@@ -216,7 +216,7 @@ __global__ void k_affine_check(const fe *__restrict__ tab, fe *out_u, fe *out_v)
   fe u[K], v[K], c[K], one;
   fe_one(one);
   for (int j = 0; j < K; j++) {
-    const uint32_t i = mix((uint32_t)lane * 31u + j) & (kTable - 1);
+    const uint32_t i = mix((uint32_t)lane * 31u + (uint32_t)j + 0x9e3779b9u) & (kTable - 1);
     u[j] = tab[2 * i];
     v[j] = tab[2 * i + 1];
   }
@@ -298,7 +298,7 @@ int main() {
   int mism = 0;
   for (uint32_t lane = 0; lane < 64; lane++)
     for (int j = 0; j < 4; j++) {
-      const uint32_t i0 = mix(lane * 31u + j) & (kTable - 1), i1 = mix(lane * 977u + (uint32_t)j) & (kTable - 1);
+      const uint32_t i0 = mix(lane * 31u + (uint32_t)j + 0x9e3779b9u) & (kTable - 1), i1 = mix(lane * 977u + (uint32_t)j) & (kTable - 1);
       fe u = tab[2 * i0], v = tab[2 * i0 + 1], du, inv;
       fe_sub(du, tab[2 * i1], u);
       fe_carry(du, du);

@@ -14,6 +14,7 @@
 #   tracepy:SCRIPT ARGS rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS -> tracepy_K/
 #   configs[:ARGS]      tools/bench_configs.py ARGS       -> configs_K.log
 #   py[:ARGS]           python -u ARGS                    -> py_K.log
+#   bin:PATH [ARGS]     a built tool binary (e.g. tools/affine_bench) -> bin_K.log
 # Optional per-step limit: STEP@SECONDS (default 600).  Optional per-step
 # environment: [K=V,K2=V2]STEP (e.g. [TMV_MSM_PARTS=2]alone:--n 125000, or
 # [TMV_LIB_PATH=tendermint_amd/_build/ab_x.so]alone:... for an A/B build).
@@ -67,6 +68,8 @@ for step in "$@"; do
       cat "$out/configs_$k.log" | grep '^{';;
     py)
       timeout -k 10 "$lim" python -u $args > "$out/py_$k.log" 2>&1; rc=$?; tail -20 "$out/py_$k.log";;
+    bin)
+      timeout -k 10 "$lim" $args > "$out/bin_$k.log" 2>&1; rc=$?; tail -20 "$out/bin_$k.log";;
     *)
       echo "unknown step $kind"; exit 2;;
   esac

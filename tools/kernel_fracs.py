@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--pmc", default="")
     ap.add_argument("--isa", default=os.path.join(REPO, "profiles", "r05", "isa_mix.json"))
     ap.add_argument("--skip", type=int, default=3)
+    ap.add_argument("--src-digest", default="",
+                    help="the profiled library's compiled source digest (tmv_version src=...); bench.py labels "
+                         "executed fractions from a profile of another build as estimates")
     ap.add_argument("--locate-min", type=int, default=400_000,
                     help="the profiled build's TMV_LOCATE_MIN (groups of 128 and the located pass from it)")
     a = ap.parse_args()
@@ -94,7 +97,8 @@ def main():
     shapes = [json.loads(x) for x in open(a.alone) if x.startswith("{")]
     # prep grid = ceil(2n / 256) + ceil(n / 256) blocks x 256 threads
     grid_of = lambda n: (-(-2 * n // 256) + -(-n // 256)) * 256  # noqa: E731
-    res = {"peak_mul_per_s": peak, "source": {"trace": a.trace, "pmc": a.pmc or None, "isa": a.isa}, "launches": []}
+    res = {"peak_mul_per_s": peak, "source": {"trace": a.trace, "pmc": a.pmc or None, "isa": a.isa,
+                                               "src_digest": a.src_digest or None}, "launches": []}
     for sh in shapes:
         n = sh["n"]
         Ls = tl.get(grid_of(n), [])[a.skip:]
