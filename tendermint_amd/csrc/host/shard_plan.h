@@ -17,13 +17,9 @@ struct ShardPlan {
   std::vector<uint32_t> bounds;   // shard s covers [bounds[s], bounds[s + 1])
   std::vector<uint32_t> nchunks;  // chunks of shard s
   uint32_t max_chunks = 0;
-  // staggered plan (plan_staggered): every shard is two chunks, the second
-  // the shard's last `tail` entries
-  uint32_t tail = 0;
 
   // chunk k of shard s covers [chunk_lo(s, k), chunk_lo(s, k + 1))
   uint32_t chunk_lo(uint32_t s, uint32_t k) const {
-    if (tail) return k == 0 ? bounds[s] : k == 1 ? bounds[s + 1] - tail : bounds[s + 1];
     const uint32_t len = bounds[s + 1] - bounds[s];
     return bounds[s] + (uint32_t)((uint64_t)len * k / nchunks[s]);
   }
@@ -47,27 +43,6 @@ inline ShardPlan plan_shards(uint32_t n, uint32_t ndev, uint32_t host_chunk) {
     p.nchunks[s] = std::max<uint32_t>(1, std::min<uint32_t>(len / (chunk / 2), std::max<uint32_t>(4, len / chunk)));
     p.max_chunks = std::max(p.max_chunks, p.nchunks[s]);
   }
-  return p;
-}
-
-// Streamed batch-equation shards of one pipeline each (up to the stream
-// chunk) are cut into a main chunk and a short last chunk of `tail` entries
-// on the other lane, whose kernels wait for the main chunk's throughput
-// stages (tmverify_runtime.cpp: HostLane::thr_done): the main chunk's latency
-// tail -- Horner, the located pass, the one-by-one fallback at about one wave
-// per SIMD -- then runs beside the last chunk's throughput stages instead of
-// after them, and only the short chunk's tail is left at the end.  A shard
-// shorter than 4 x tail keeps one chunk (plan_shards).
-inline ShardPlan plan_staggered(uint32_t n, uint32_t ndev, uint32_t tail) {
-  ShardPlan p;
-  p.shards = std::max<uint32_t>(1, std::min<uint32_t>(ndev, n / 1024));
-  p.bounds.resize(p.shards + 1);
-  for (uint32_t s = 0; s <= p.shards; s++) p.bounds[s] = (uint32_t)((uint64_t)n * s / p.shards);
-  p.nchunks.assign(p.shards, 2);
-  p.max_chunks = 2;
-  p.tail = tail;
-  for (uint32_t s = 0; s < p.shards; s++)
-    if (p.bounds[s + 1] - p.bounds[s] < 4ull * tail) return plan_shards(n, ndev, ~0u);
   return p;
 }
 

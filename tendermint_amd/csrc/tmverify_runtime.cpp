@@ -203,10 +203,6 @@ struct HostLane {
   // `join` orders the launch's tail after them
   hipStream_t helper = nullptr;
   hipEvent_t join = nullptr;
-  // staggered plan (tmh::plan_staggered): recorded after this lane's chunk
-  // enqueued its throughput stages ([0] on the lane's stream, [1] on the
-  // helper), waited for by the shard's short last chunk on the other lane
-  hipEvent_t thr_done[2] = {nullptr, nullptr};
   // streamed mixed chunks: one event per part after its kind partition
   std::vector<hipEvent_t> part_split;
   // caller pages pinned for the chunk in flight (streamed path, direct DMA);
@@ -384,11 +380,6 @@ constexpr uint32_t kMaxStreamParts = 512;  // bound on a streamed mixed chunk's 
 // (A/B: TMV_REGISTER=0 stages everything).  A span whose pages cannot be
 // pinned (already pinned, read-only mapping, ...) is staged.
 int g_register = 1;
-// Streamed shards of one pipeline are split into a main chunk and a last
-// chunk of this many entries on the other lane, whose kernels wait for the
-// main chunk's throughput stages, so the main chunk's latency tail runs
-// beside them (tmh::plan_staggered; A/B: TMV_STAGGER_TAIL, 0 = off).
-uint32_t g_stagger_tail = 262144;
 
 void read_env() {
   static std::once_flag once;
@@ -432,8 +423,6 @@ void read_env() {
     if (s2) g_stream_two = atoi(s2);
     const char *rg = tmv::ab_knob("TMV_REGISTER");
     if (rg) g_register = atoi(rg);
-    const char *stg = tmv::ab_knob("TMV_STAGGER_TAIL");
-    if (stg) g_stagger_tail = (uint32_t)strtoul(stg, nullptr, 10);
   });
 }
 
@@ -1120,33 +1109,9 @@ static std::vector<uint32_t> stream_parts(uint32_t n, uint32_t m) {
 
 // feed: streamed launch, parts alternating between s and s2 (if given,
 // joined back into s by `join` before the tail).
-// Staggered plans (tmh::plan_staggered): the main chunk records `rec` after
-// its throughput stages, the short last chunk's kernels wait for `wait`.
-struct Stagger {
-  const hipEvent_t *wait = nullptr;  // 2 events, or null
-  hipEvent_t *rec = nullptr;         // 2 events, or null
-};
-
-// Make both streams wait for the events of st.wait (a staggered plan's last
-// chunk); 0 or TMV_ERR_LAUNCH.
-static int stagger_wait(const Stagger &st, hipStream_t s, hipStream_t s2) {
-  if (!st.wait) return 0;
-  for (int k = 0; k < 2; k++) {
-    if (!st.wait[k]) continue;
-    hipError_t e;
-    if ((e = hipStreamWaitEvent(s, st.wait[k], 0)) != hipSuccess ||
-        (s2 && s2 != s && (e = hipStreamWaitEvent(s2, st.wait[k], 0)) != hipSuccess)) {
-      set_error("stagger wait", e);
-      return TMV_ERR_LAUNCH;
-    }
-  }
-  return 0;
-}
-
 static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *pk, const uint8_t *sig,
                        const uint8_t *msg, const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s,
-                       const PartFeeder *feed = nullptr, hipStream_t s2 = nullptr, hipEvent_t join = nullptr,
-                       const Stagger &st = Stagger{}) {
+                       const PartFeeder *feed = nullptr, hipStream_t s2 = nullptr, hipEvent_t join = nullptr) {
   int rc;
   Workspace *ws = reserve_work(d, n, false, s, &rc, &o.p);
   if (!ws) return rc;
@@ -1156,7 +1121,6 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
   if (feed) {  // parts as their inputs land, then one tail
     const std::vector<uint32_t> b = stream_parts(n, o.p.m());
     const bool two = s2 && join && b.size() > 2;
-    if ((rc = stagger_wait(st, s, two ? s2 : s)) != 0) return rc;
     for (size_t j = 0; j + 1 < b.size(); j++) {
       hipEvent_t ready = nullptr;
       if ((rc = (*feed)(b[j], b[j + 1], &ready)) != 0) return rc;
@@ -1168,10 +1132,6 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
     }
     if (two && ((e = hipEventRecord(join, s2)) != hipSuccess || (e = hipStreamWaitEvent(s, join, 0)) != hipSuccess)) {
       set_error("part join", e);
-      return TMV_ERR_LAUNCH;
-    }
-    if (st.rec && st.rec[0] && (e = hipEventRecord(st.rec[0], s)) != hipSuccess) {  // s now covers both streams' parts
-      set_error("stagger record", e);
       return TMV_ERR_LAUNCH;
     }
     e = tmv::launch_batch_check_tail(sr, pk, sig, n, d.d_btab_q, w, mw, o.p, o.seed[sr ? 1 : 0], out, s);
@@ -1206,8 +1166,7 @@ static int batch_check(Device &d, const LaunchOpts &o, bool sr, const uint8_t *p
 static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t *kind_h, const uint8_t *kind_d,
                                 const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *off,
                                 uint32_t n, uint8_t *out, hipStream_t s, hipStream_t s2, hipEvent_t join,
-                                std::vector<hipEvent_t> &split_ev, const PartFeeder &feed,
-                                const Stagger &st = Stagger{}) {
+                                std::vector<hipEvent_t> &split_ev, const PartFeeder &feed) {
   LaunchOpts o = o_in;
   o.p_ed = o_in.p_ed_streamed;
   int rc;
@@ -1244,7 +1203,6 @@ static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t
   }
   const uint32_t g_ed = o.p_ed.m(), g_sr = o.p.m();  // group sizes
   uint32_t base_ed = 0, base_sr = 0, done_ed = 0, done_sr = 0;  // slots assigned / slots launched
-  if ((rc = stagger_wait(st, s, s2)) != 0) return rc;
   for (size_t j = 0; j < parts; j++) {
     const uint32_t a = b[j], z = b[j + 1];
     hipEvent_t ready = nullptr;
@@ -1282,11 +1240,6 @@ static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t
   }
   // the tails: ed25519 on s, sr25519 on s2 (after its last partition), joined into s
   if ((e = hipStreamWaitEvent(s2, split_ev[parts - 1], 0)) != hipSuccess) { set_error("part wait", e); return TMV_ERR_LAUNCH; }
-  if (st.rec && ((st.rec[0] && (e = hipEventRecord(st.rec[0], s)) != hipSuccess) ||
-                 (st.rec[1] && s2 != s && (e = hipEventRecord(st.rec[1], s2)) != hipSuccess))) {
-    set_error("stagger record", e);
-    return TMV_ERR_LAUNCH;
-  }
   if ((e = tmv::launch_batch_check_tail_idx(true, pk, sig, idx_sr, base_sr, d.d_btab_q, w_sr, m_sr, o.p, o.seed[1], out,
                                             s2)) != hipSuccess ||
       (e = tmv::launch_batch_check_tail_idx(false, pk, sig, idx_ed, base_ed, d.d_btab_q, w_ed, m_ed, o.p_ed, o.seed[0],
@@ -1564,10 +1517,6 @@ void tmv_close(tmv_ctx *ctx) {
       if (l.join) (void)hipEventDestroy(l.join);
       l.helper = nullptr;
       l.join = nullptr;
-      for (hipEvent_t &ev : l.thr_done) {
-        if (ev) (void)hipEventDestroy(ev);
-        ev = nullptr;
-      }
       l.d_in.release();
       l.d_out.release();
       l.h_in.release();
@@ -1628,12 +1577,9 @@ struct VoteSrc {
 // slots first; the key-merged batch equation gets the key order of the
 // entries (a counting sort by slot) and the runs of one key inside a group,
 // and its kernels read the entries through that order.
-// stagger: 1 = the main chunk of a staggered plan (records ln.thr_done after
-// its throughput stages), 2 = its last chunk (waits for wait_lane's).
 static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &ln, Scheme sch, const uint8_t *kind,
                             const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, const uint32_t *msg_off,
-                            uint32_t lo, uint32_t hi, const VoteSrc *vs, int stagger = 0,
-                            HostLane *wait_lane = nullptr) {
+                            uint32_t lo, uint32_t hi, const VoteSrc *vs) {
   const uint32_t n = hi - lo;
   const size_t mbytes = (size_t)msg_off[hi] - msg_off[lo];
   Layout L(n, mbytes);
@@ -1781,23 +1727,15 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
       return 0;
     };
     tm.mark("stage", n);
-    Stagger st;
-    if (stagger == 1) {
-      for (hipEvent_t &ev : ln.thr_done)
-        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
-      st.rec = ln.thr_done;
-    } else if (stagger == 2 && wait_lane) {
-      st.wait = wait_lane->thr_done;
-    }
     const int rc =
         mixed_stream
             ? mixed_check_streamed(d, o, kind + lo, dd + kind_at, dd + L.pk, dd + L.sig, dd + L.msg,
                                    reinterpret_cast<const uint32_t *>(dd + L.off), n,
                                    static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, ln.helper,
-                                   ln.join, ln.part_split, feed, st)
+                                   ln.join, ln.part_split, feed)
             : batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off), n,
                           static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed, g_stream_two ? ln.helper : nullptr,
-                          g_stream_two ? ln.join : nullptr, st);
+                          g_stream_two ? ln.join : nullptr);
     if (rc != 0) {  // parts already enqueued still use the lane's buffers: drain before returning
       const bool drained = wait_stream(d, ln.copy) == hipSuccess;
       if (ln.helper) (void)wait_stream(d, ln.helper);
@@ -2003,12 +1941,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
     }
     chunk = free_b ? mixed_stream_chunk(free_b) : g_mixed_chunk;
   }
-  // streamed shards of one pipeline: a main chunk and a short last chunk
-  // whose throughput stages hide the main chunk's latency tail
-  const bool stagger = (streamable || mixed_streamed) && g_stagger_tail && g_host_lanes >= 2 &&
-                       per_dev >= 4ull * g_stagger_tail && per_dev <= chunk;
-  const tmh::ShardPlan plan = stagger ? tmh::plan_staggered(n, (uint32_t)ctx->devs.size(), g_stagger_tail)
-                                      : tmh::plan_shards(n, (uint32_t)ctx->devs.size(), chunk);
+  const tmh::ShardPlan plan = tmh::plan_shards(n, (uint32_t)ctx->devs.size(), chunk);
   const uint32_t shards = plan.shards;
   // claim g_host_lanes lanes per device (devices in order, so concurrent
   // calls cannot deadlock); released on every return
@@ -2080,10 +2013,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
         (void)hipSetDevice(d.id);
         std::lock_guard<std::mutex> lk(d.mu);  // key cache, device scratch, workspaces
         if (d.faulted) return faulted_rc(d);
-        // staggered plan: chunk 0 (lane slot 0) records, chunk 1 (slot 1) waits
-        const int role = plan.tail ? (c0 == plan.bounds[s] ? 1 : 2) : 0;
-        const int r = stage_and_launch(ctx, flags, d, ln, sch, kind, pk, sig, msg, msg_off, c0, c1, vs, role,
-                                       role == 2 ? &d.lane[claims.lane[s][0]] : nullptr);
+        const int r = stage_and_launch(ctx, flags, d, ln, sch, kind, pk, sig, msg, msg_off, c0, c1, vs);
         if (r == 0) {
           ln.lo = c0;
           ln.n = c1 - c0;

@@ -310,18 +310,9 @@ size_t commitcheck_canonical_time(int64_t secs, int32_t nanos, char *out, size_t
 // The runtime's shard / chunk plan of a host-buffer batch (host/shard_plan.h,
 // used by run_batch), in launch order: (device, lo, hi, chunk k) per chunk.
 // Returns the number of chunks written (or needed, if cap is short).
-static uint32_t write_plan(const tmh::ShardPlan &p, uint32_t *out, uint32_t cap);
 extern "C" uint32_t commitcheck_shard_plan(uint32_t n, uint32_t ndev, uint32_t host_chunk, uint32_t *out,
                                            uint32_t cap) {
-  return write_plan(tmh::plan_shards(n, ndev, host_chunk), out, cap);
-}
-// The staggered plan of streamed shards (a main chunk, then the shard's last
-// `tail` entries on the other lane).
-extern "C" uint32_t commitcheck_shard_plan_staggered(uint32_t n, uint32_t ndev, uint32_t tail, uint32_t *out,
-                                                     uint32_t cap) {
-  return write_plan(tmh::plan_staggered(n, ndev, tail), out, cap);
-}
-static uint32_t write_plan(const tmh::ShardPlan &p, uint32_t *out, uint32_t cap) {
+  const tmh::ShardPlan p = tmh::plan_shards(n, ndev, host_chunk);
   uint32_t w = 0;
   for (uint32_t k = 0; k < p.max_chunks; k++)
     for (uint32_t s = 0; s < p.shards; s++) {

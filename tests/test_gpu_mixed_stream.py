@@ -84,18 +84,3 @@ def test_mixed_streamed_stats(ctx, base, monkeypatch):
     n_ed, n_sr = int(np.sum(kinds == 0)), int(np.sum(kinds == 1))
     g = lambda k, m: (k + m - 1) // m  # noqa: E731
     assert groups == g(n_ed, 64) + g(n_sr, 64), groups
-
-
-def test_mixed_staggered_plan(ctx, base):
-    """1.1M mixed entries: a staggered plan (tmh::plan_staggered) -- a main
-    chunk, then the last 262,144 entries on the other lane, whose part
-    pipelines wait for the main chunk's throughput stages on both kinds'
-    streams -- gives the oracle's statuses."""
-    kind, mb, want1 = base
-    idx = np.arange(1_100_000) % mb.n
-    hb = mb.take(idx)
-    kinds = np.ascontiguousarray(kind[idx])
-    _, st = ctx.verify_mixed_batch_ex(N.TMV_FLAG_BATCH_EQUATION, kinds, hb.pk, hb.sig, hb.msg, hb.off)
-    got = np.asarray(st, np.int8)
-    bad = np.flatnonzero(got != want1[idx])
-    assert not len(bad), f"entries {bad[:8]}: {got[bad[:8]]} vs {want1[idx][bad[:8]]}"

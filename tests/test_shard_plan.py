@@ -65,35 +65,3 @@ def test_placement_roundtrip(plan):
         for d, lo, hi, k in plan(n, ndev, 131072):
             out[lo:hi] = want[lo:hi]
         assert np.array_equal(out, want)
-
-
-@pytest.mark.parametrize("n,ndev,tail", [(2_560_000, 1, 262144), (1_000_000, 1, 262144), (1_048_576, 1, 262144),
-                                         (1_048_575, 1, 262144), (8_000_000, 8, 262144), (500_000, 1, 262144),
-                                         (4_194_304, 3, 262144)])
-def test_staggered_plan(n, ndev, tail):
-    """Streamed shards of one pipeline: a main chunk, then the shard's last
-    `tail` entries as chunk 1 (the runtime puts it on the other lane, its
-    kernels behind the main chunk's throughput stages); a shard shorter than
-    4 x tail stays one chunk.  Every entry lands in exactly one chunk."""
-    L = F.FakeBackend().L
-    L.commitcheck_shard_plan_staggered.restype = ctypes.c_uint32
-    L.commitcheck_shard_plan_staggered.argtypes = [ctypes.c_uint32] * 3 + [ctypes.POINTER(ctypes.c_uint32),
-                                                                           ctypes.c_uint32]
-    k = L.commitcheck_shard_plan_staggered(n, ndev, tail, None, 0)
-    buf = np.zeros(4 * k, np.uint32)
-    L.commitcheck_shard_plan_staggered(n, ndev, tail, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), k)
-    p = buf.reshape(-1, 4)
-    shards = max(1, min(ndev, n // 1024))
-    out = np.zeros(n, np.uint8)
-    for d, lo, hi, kk in p:
-        out[lo:hi] += 1
-    assert (out == 1).all()
-    shard_len = [n * (s + 1) // shards - n * s // shards for s in range(shards)]
-    if min(shard_len) >= 4 * tail:
-        assert len(p) == 2 * shards
-        for d, lo, hi, kk in p:
-            end = n * (d + 1) // shards
-            assert (kk == 1) == (hi == end and hi - lo == tail)
-        assert (np.diff(p[:, 3].astype(np.int64)) >= 0).all()  # every main chunk before any last chunk
-    else:
-        assert len(p) == shards
