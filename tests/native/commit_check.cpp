@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <atomic>
 #include <functional>
 #include <string>
@@ -76,8 +77,8 @@ struct tmv_ctx {
 };
 
 extern "C" {
-int commitcheck_backend_calls = 0;
-int commitcheck_entries_verified = 0;
+std::atomic<int> commitcheck_backend_calls{0};  // read as a plain int through ctypes (same layout)
+std::atomic<int> commitcheck_entries_verified{0};
 int g_skip_hash = 0;  // timing of the host layer alone (tools only)
 // the next device call returns this infrastructure error (e.g.
 // TMV_ERR_TIMEOUT), on whichever thread makes it, and leaves a message
@@ -122,16 +123,22 @@ static int take_failure() {
 // the CPU.
 static uint32_t g_devices = 1, g_chunk = 262144, g_lanes = 2;
 static std::vector<uint32_t> g_steps;  // (kind 0 launch / 1 harvest, device, lane, lo, hi) per step
+// sliced host-layer calls (TMV_HOST_SLICE) reach the double from two threads
+// at once: the step log is appended under this lock (it was not, and the
+// concurrent appends corrupted the heap under CPU load)
+static std::mutex g_steps_mu;
 
 void commitcheck_set_devices(uint32_t devices, uint32_t host_chunk, uint32_t lanes) {
   g_devices = devices ? devices : 1;
   g_chunk = host_chunk;
   g_lanes = lanes ? lanes : 1;
+  std::lock_guard<std::mutex> lk(g_steps_mu);
   g_steps.clear();
 }
 
 // Copies up to cap steps (5 words each) and clears the log; returns the count.
 uint32_t commitcheck_steps(uint32_t *out, uint32_t cap) {
+  std::lock_guard<std::mutex> lk(g_steps_mu);
   const uint32_t n = (uint32_t)(g_steps.size() / 5);
   for (uint32_t i = 0; i < std::min(n, cap) * 5; i++) out[i] = g_steps[i];
   g_steps.clear();
@@ -153,7 +160,10 @@ static void run_devices(uint32_t n, int8_t *status_out, F status_of) {
         Lane &ln = lanes[s][l];
         if (!ln.n) return 0;
         if (ok) std::memcpy(status_out + ln.lo, ln.buf.data(), ln.n);
-        g_steps.insert(g_steps.end(), {1u, s, l, ln.lo, ln.lo + ln.n});
+        {
+          std::lock_guard<std::mutex> lk(g_steps_mu);
+          g_steps.insert(g_steps.end(), {1u, s, l, ln.lo, ln.lo + ln.n});
+        }
         ln.n = 0;
         return 0;
       },
@@ -163,7 +173,10 @@ static void run_devices(uint32_t n, int8_t *status_out, F status_of) {
         for (uint32_t i = lo; i < hi; i++) ln.buf[i - lo] = status_of(i);
         ln.lo = lo;
         ln.n = hi - lo;
-        g_steps.insert(g_steps.end(), {0u, s, l, lo, hi});
+        {
+          std::lock_guard<std::mutex> lk(g_steps_mu);
+          g_steps.insert(g_steps.end(), {0u, s, l, lo, hi});
+        }
         return 0;
       });
 }
