@@ -79,7 +79,7 @@ def _load_peak() -> float:
     return best or PEAK_MUL_PER_S
 
 
-PMC_DIRS = ("r05", "r04", "r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
+PMC_DIRS = ("r06", "r05", "r04", "r03", "r02_final", "r02_close", "r02", "r01_close")  # newest first
 
 
 def _load_pmc(method: str, batches_per_step: int = 32):
@@ -429,7 +429,7 @@ class _HostEvent:
         return (other.t - self.t) * 1e3
 
 
-KFRACS_FILE = os.path.join("profiles", "r05", "kernel_fracs.json")
+KFRACS_FILE = os.path.join("profiles", "r06", "kernel_fracs.json")
 
 
 def _kernel_fracs():
@@ -507,7 +507,7 @@ def _pipeline_roofline(gpu_rate, peak, pmc, launch_ms, method, n_launch=0, ms_pe
     return out
 
 
-DOMINANT_FILE = os.path.join("profiles", "r05", "dominant_kernel.json")
+DOMINANT_FILE = os.path.join("profiles", "r06", "dominant_kernel.json")
 
 
 def _dominant_file():
@@ -521,13 +521,14 @@ def _dominant_file():
 def _isa_mix():
     """Static instruction mix of k_msm_accum<16> (tools/isa_mix.py), newest
     committed profile first."""
-    path = os.path.join(REPO, "profiles", "r05", "isa_mix.json")
-    if os.path.exists(path):
-        with open(path) as f:
-            m = json.load(f).get("kernels", {}).get("k_msm_accum<16>")
-        if m and m.get("mad_share_of_int64"):
-            m["source"] = "profiles/r05/isa_mix.json"
-            return m
+    for d in ("r06", "r05"):
+        path = os.path.join(REPO, "profiles", d, "isa_mix.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                m = json.load(f).get("kernels", {}).get("k_msm_accum<16>")
+            if m and m.get("mad_share_of_int64"):
+                m["source"] = f"profiles/{d}/isa_mix.json"
+                return m
     for d in ("r04", "r03", "r02_close"):
         path = os.path.join(REPO, "profiles", d, "isa_mix_accum.json")
         if os.path.exists(path):
@@ -550,7 +551,7 @@ def _dominant_roofline(ktimes, ktimes_alone, K, n, args, peak, steps, pipeline, 
     shares the chip -- against the measured v_mad_i64_i32 peak.  The
     committed rocprofv3 --kernel-trace --stats of bench.py --inflight 1 (one
     launch at a time) gives the same kernel's average dispatch
-    (profiles/r05/dominant_kernel.json); traffic = its HBM bytes per launch
+    (profiles/r06/dominant_kernel.json); traffic = its HBM bytes per launch
     from PMC passes at this launch size (256 x 10k)."""
     m_grp, c_win = msm_shape(K * n, args.group_log2, args.window)
     per_launch = K * n * accum_entries_per_sig(m=m_grp, c=c_win) * ACCUM_PRODUCTS_PER_ENTRY
@@ -887,7 +888,9 @@ def main():
                "exact_vector_on_every_rank": True,
                "note": (f"one {n_total}-signature batch split over {world} rank(s) (contiguous shards), every rank "
                         "verifies its shard and the vectors are all-gathered"
-                        + (" (RCCL)" if world > 1 and not stub else "") + "; every rank's full vector equals the "
+                        + (f" ({'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()})"
+                           if world > 1 and not stub and dist.is_initialized() else "")
+                        + "; every rank's full vector equals the "
                         "known one; wall time = max over ranks, median of the repetitions; kernel_only: inputs "
                         "resident in HBM, vector left on the device; end_to_end: host buffers through the C-ABI, "
                         "vector back on the host")}

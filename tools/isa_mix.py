@@ -9,7 +9,7 @@ the code, not executed): exact for a kernel whose time is one loop body
 (k_msm_accum), an estimate for kernels with several loops (k_prep_fused's
 square-root chains and SHA-512 rounds).
 
-  python tools/isa_mix.py > profiles/r05/isa_mix.json          # every kernel
+  python tools/isa_mix.py > profiles/r06/isa_mix.json          # every kernel
   python tools/isa_mix.py accum > profiles/r05/isa_mix_accum.json  # one (old format)
 """
 import collections
@@ -28,14 +28,13 @@ KERNELS = {
     "k_msm_accum<16>": ("msm_kernels.hip", "_ZN3tmv11k_msm_accumILi16E"),
     "k_msm_wpart": ("msm_kernels.hip", "_ZN3tmv11k_msm_wpartE"),
     "k_msm_wsum": ("msm_kernels.hip", "_ZN3tmv10k_msm_wsumE"),
-    "k_msm_join": ("msm_kernels.hip", "_ZN3tmv10k_msm_joinE"),
     "k_msm_join_list": ("msm_kernels.hip", "_ZN3tmv15k_msm_join_listE"),
-    "k_msm_horner<false, false, 0>": ("msm_kernels.hip", "_ZN3tmv12k_msm_hornerILb0ELb0ELi0E"),
-    "k_msm_horner<false, false, 1>": ("msm_kernels.hip", "_ZN3tmv12k_msm_hornerILb0ELb0ELi1E"),
+    "k_msm_horner<false, false, false>": ("msm_kernels.hip", "_ZN3tmv12k_msm_hornerILb0ELb0ELb0E"),
+    "k_msm_horner<false, false, true>": ("msm_kernels.hip", "_ZN3tmv12k_msm_hornerILb0ELb0ELb1E"),
     "k_msm_horner_helped<false>": ("msm_kernels.hip", "_ZN3tmv19k_msm_horner_helpedILb0E"),
-    "k_msm_sort<false, false, 64, 0>": ("msm_kernels.hip", "_ZN3tmv10k_msm_sortILb0ELb0ELi64ELi0E"),
-    "k_msm_sort<false, false, 64, 1>": ("msm_kernels.hip", "_ZN3tmv10k_msm_sortILb0ELb0ELi64ELi1E"),
-    "k_msm_sort<false, false, 256, 0>": ("msm_kernels.hip", "_ZN3tmv10k_msm_sortILb0ELb0ELi256ELi0E"),
+    "k_msm_sort<false, false, 64, false>": ("msm_kernels.hip", "_ZN3tmv10k_msm_sortILb0ELb0ELi64ELb0E"),
+    "k_msm_sort<false, false, 64, true>": ("msm_kernels.hip", "_ZN3tmv10k_msm_sortILb0ELb0ELi64ELb1E"),
+    "k_msm_sort<false, false, 256, false>": ("msm_kernels.hip", "_ZN3tmv10k_msm_sortILb0ELb0ELi256ELb0E"),
     "k_loc_search<false>": ("msm_kernels.hip", "_ZN3tmv12k_loc_searchILb0E"),
     "k_prep_fused<false>": ("verify_kernels.hip", "_ZN3tmv12k_prep_fusedILb0E"),
     "k_prep_fused<true>": ("verify_kernels.hip", "_ZN3tmv12k_prep_fusedILb1E"),
