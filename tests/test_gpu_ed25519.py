@@ -121,3 +121,30 @@ def test_both_kernels_c2(ctx, golden, tiles):
     for t in range(tiles):
         v = (st[t * b1.n:(t + 1) * b1.n] == 1).astype(np.uint8)
         assert np.packbits(v, bitorder="little").tobytes().hex() == want, t
+
+
+def test_random_failure_fails_the_call_not_the_vector(ctx, golden):
+    """A batch-equation call whose weights key cannot be drawn (getrandom
+    failing, injected through tmv_internal_random_fault) returns
+    TMV_ERR_RANDOM before anything is launched, so the caller sees an error,
+    never a vector; per-entry calls draw nothing and are unaffected; the
+    next batch-equation call after the fault clears verifies normally
+    (crypto/ed25519/ed25519.go:232: rand.Reader errors reach the caller)."""
+    import ctypes
+    import errno
+    from tendermint_amd import _native as N
+    L = N.lib()
+    L.tmv_internal_random_fault.argtypes = [ctypes.c_int, ctypes.c_int]
+    b = make_c2_batch()
+    want = golden("c2_expected.json")["valid_bits_hex"]
+    bits = lambda st: np.packbits((st == 1).astype(np.uint8), bitorder="little").tobytes().hex()  # noqa: E731
+    try:
+        L.tmv_internal_random_fault(errno.ENOSYS, -1)
+        with pytest.raises(N.NativeError, match=r"\(-6\).*getrandom"):
+            ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, b.pk, b.sig, b.msg, b.off)
+        _, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_PER_ENTRY, b.pk, b.sig, b.msg, b.off)
+        assert bits(st) == want
+    finally:
+        L.tmv_internal_random_fault(0, 0)
+    _, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, b.pk, b.sig, b.msg, b.off)
+    assert bits(st) == want
