@@ -40,17 +40,18 @@ def main():
     ctx = N.Context(1)
     flags = N.TMV_FLAG_BATCH_EQUATION
     n = len(off) - 1
-    ts = []
+    ts, calls_ns = [], []
     for i in range(9):
-        t = time.perf_counter()
+        t, t_ns = time.perf_counter(), time.monotonic_ns()
         ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, flags, pk, sig, msg, off)
         ts.append(time.perf_counter() - t)
+        calls_ns.append([t_ns, time.monotonic_ns()])
         assert int((st == 1).sum()) == (len(off) - 1) // 10_000 * 9950
     m = statistics.median(ts[2:])
     env = {k: v for k, v in os.environ.items() if k.startswith("TMV_")}
     h2d = pk.nbytes + sig.nbytes + msg.nbytes + off.nbytes
     line = {"env": env, "n": n, "median_ms": round(m * 1e3, 3), "e2e_verifies_per_s": round(n / m),
-            "h2d_GBps": round(h2d / m / 1e9, 2)}
+            "h2d_GBps": round(h2d / m / 1e9, 2), "calls_monotonic_ns": calls_ns}
     # TMV_E2E_CALLERS=C: C threads, each calling 4 times on its own copy of
     # the batch (each call claims its own lanes)
     callers = int(os.environ.get("TMV_E2E_CALLERS", "1"))

@@ -12,6 +12,7 @@
 #   trace[:ARGS]        rocprofv3 --kernel-trace --stats of tools/launch_alone.py ARGS -> trace_K/
 #   tracebench[:ARGS]   rocprofv3 --kernel-trace --stats of bench.py ARGS     -> tracebench_K/
 #   tracepy:SCRIPT ARGS rocprofv3 --kernel-trace --stats of python3 SCRIPT ARGS -> tracepy_K/
+#   tracecp:SCRIPT ARGS the same with --memory-copy-trace (host-buffer timelines) -> tracecp_K/
 #   configs[:ARGS]      tools/bench_configs.py ARGS       -> configs_K.log
 #   py[:ARGS]           python -u ARGS                    -> py_K.log
 #   bin:PATH [ARGS]     a built tool binary (e.g. tools/affine_bench) -> bin_K.log
@@ -63,6 +64,10 @@ for step in "$@"; do
       timeout -k 10 "$lim" rocprofv3 --kernel-trace --stats --output-format csv -d "$out/tracepy_$k" -o run -- \
         python3 -u $args > "$out/tracepy_$k.log" 2>&1; rc=$?
       grep '^{' "$out/tracepy_$k.log" | tail -c 600;;
+    tracecp)
+      timeout -k 10 "$lim" rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+        -d "$out/tracecp_$k" -o run -- python3 -u $args > "$out/tracecp_$k.log" 2>&1; rc=$?
+      grep '^{' "$out/tracecp_$k.log" | tail -c 600;;
     configs)
       timeout -k 10 "$lim" python -u tools/bench_configs.py $args > "$out/configs_$k.log" 2>&1; rc=$?
       cat "$out/configs_$k.log" | grep '^{';;

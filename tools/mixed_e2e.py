@@ -48,11 +48,12 @@ def main():
     if a.group_log2 or a.window_bits:
         ctx.set_batch_options(group_log2=a.group_log2, window_bits=a.window_bits)
     flags = N.TMV_FLAG_BATCH_EQUATION
-    e2e = []
+    e2e, calls_ns = [], []
     for r in range(a.reps + 2):
-        t0 = time.perf_counter()
+        t0, t0_ns = time.perf_counter(), time.monotonic_ns()
         _, st = ctx.verify_mixed_batch_ex(flags, kinds, hb.pk, hb.sig, hb.msg, hb.off)
         t1 = time.perf_counter()
+        calls_ns.append([t0_ns, time.monotonic_ns()])
         if r == 0:
             bad = np.flatnonzero(np.asarray(st, np.int8) != want)
             assert not len(bad), f"end to end: entries {bad[:8]} differ from the oracle"
@@ -79,7 +80,8 @@ def main():
                       "group_log2": a.group_log2, "window_bits": a.window_bits,
                       "end_to_end_ms": round(em, 3), "end_to_end_verifies_per_s": round(a.n / em * 1e3, 1),
                       "kernel_only_ms": round(km, 3), "kernel_only_verifies_per_s": round(a.n / km * 1e3, 1),
-                      "e2e_reps_ms": [round(x, 3) for x in e2e], "exact_vs_oracle": True}), flush=True)
+                      "e2e_reps_ms": [round(x, 3) for x in e2e], "exact_vs_oracle": True,
+                      "calls_monotonic_ns": calls_ns}), flush=True)
 
 
 if __name__ == "__main__":
