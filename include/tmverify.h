@@ -42,8 +42,8 @@ extern "C" {
  * forever).  The context's device work is then in an unknown state: the
  * context refuses further work (every call returns TMV_ERR_TIMEOUT); the
  * caller verifies on the CPU and may tmv_close / tmv_open a new context.
- * Pages of the caller's input buffers that a streamed call had registered
- * for direct DMA (TMV_REGISTER) stay page-locked after a failed call: the
+ * Pages of the caller's buffers (inputs and status array) that a streamed
+ * call had registered for direct DMA stay page-locked after a failed call: the
  * device may still read them, so they are never unregistered under it (and
  * the library keeps no record that could unregister them once reused). */
 #define TMV_ERR_TIMEOUT (-5)

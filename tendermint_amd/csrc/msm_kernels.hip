@@ -15,6 +15,7 @@
 #include "ktimer.h"
 #include "verify_kernels.h"
 #include "halfscalar.h"
+#include "knobs.h"
 
 #include <atomic>
 #include <mutex>
@@ -279,7 +280,7 @@ k_msm_sort(const uint8_t *__restrict__ sig, const uint32_t *__restrict__ idx, co
     k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w;
     k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
     sc_mul_mod(wv[r], z[r], 4, k);
-    if (LOC) {  // weights times (j + 1): z (j + 1) exactly, z k (j + 1) mod l
+    if constexpr (LOC) {  // weights times (j + 1): z (j + 1) exactly, z k (j + 1) mod l
       const uint32_t jj = j + 1;
       uint64_t cy = 0;
 #pragma unroll
@@ -1370,6 +1371,11 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
     const uint32_t n_slots = p.groups << p.m_log2;
     MsmParams pl = p;  // running sums split over loc_parts() lanes per window (few live slots: the chain sets the time)
     pl.P = p.loc_parts();
+    static const uint32_t lp_ab = [] {  // A/B (knobs.h): TMV_LOC_PARTS, a power of two <= loc_parts()
+      const char *v = ab_knob("TMV_LOC_PARTS");
+      return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+    }();
+    if (lp_ab && lp_ab <= pl.P && !(lp_ab & (lp_ab - 1))) pl.P = lp_ab;
     if ((e = launch_buckets(mw.loc_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
                        mw.loc_count, n_slots, mw, pl, nullptr, 0u);

@@ -372,6 +372,12 @@ uint32_t g_sr_group_log2 = 0;
 // call: chunks of up to 4 M (one pipeline) 106 M/s, 2 M (two pipelines of
 // 1.28 M on two lanes) 98 M/s, 1 M 87 M/s (profiles/r03/e2e_chunk.txt)
 uint32_t g_stream_first = 32768, g_stream_part = 131072, g_stream_chunk = 1u << 22;
+// Part sizes double from g_stream_first up to g_stream_part (32k, 64k,
+// 128k, ...), so the second part lands while the first one's kernels run
+// instead of the device idling for a whole 128k part's copy (round 6, same
+// box, A/B TMV_STREAM_RAMP=0: 2.56M C2 call 22.29 / 22.12 -> 21.83 / 21.65
+// ms, C5 1M mixed 11.48 -> 11.19 ms; profiles/r06/ab_e2e_ramp.txt)
+int g_stream_ramp = 1;
 constexpr uint32_t kMaxStreamParts = 512;  // bound on a streamed mixed chunk's parts (4 M / 128k + 1 = 33 by default)
 // Streamed parts DMA straight from the caller's buffers: each part pins the
 // whole pages of its pk / sig / msg spans (hipHostRegister, disjoint page
@@ -421,6 +427,8 @@ void read_env() {
     if (sg) g_sr_group_log2 = (uint32_t)strtoul(sg, nullptr, 10);
     const char *s2 = tmv::ab_knob("TMV_STREAM_TWO");
     if (s2) g_stream_two = atoi(s2);
+    const char *rp = tmv::ab_knob("TMV_STREAM_RAMP");
+    if (rp) g_stream_ramp = atoi(rp);
     const char *rg = tmv::ab_knob("TMV_REGISTER");
     if (rg) g_register = atoi(rg);
   });
@@ -1102,7 +1110,7 @@ static std::vector<uint32_t> stream_parts(uint32_t n, uint32_t m) {
   while (b.back() < n) {
     const uint64_t e1 = std::min<uint64_t>(n, ((uint64_t)b.back() + want + m - 1) / m * m);
     b.push_back((uint32_t)e1);
-    want = g_stream_part;
+    want = g_stream_ramp ? std::min<uint32_t>(g_stream_part, 2 * want) : g_stream_part;
   }
   return b;
 }
@@ -1183,9 +1191,11 @@ static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t
   uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n, *cursor = ib + 16 + 2ull * n;
   // parts: the one-kind schedule (a short first part), at most kMaxStreamParts
   uint32_t part_len = g_stream_part;
-  while ((n - std::min(n, g_stream_first) + part_len - 1) / part_len + 1 > kMaxStreamParts) part_len *= 2;
+  while ((n - std::min(n, g_stream_first) + part_len - 1) / part_len + 1 + (g_stream_ramp ? 32 : 0) > kMaxStreamParts)
+    part_len *= 2;
   std::vector<uint32_t> b{0};
-  for (uint32_t want = g_stream_first; b.back() < n; want = part_len) b.push_back(std::min<uint64_t>(n, (uint64_t)b.back() + want));
+  for (uint32_t want = g_stream_first; b.back() < n; want = g_stream_ramp ? std::min(part_len, 2 * want) : part_len)
+    b.push_back(std::min<uint64_t>(n, (uint64_t)b.back() + want));
   const size_t parts = b.size() - 1;
   hipError_t e;
   if ((e = hipMemsetAsync(ib, 0, 64, s)) != hipSuccess ||
@@ -1649,38 +1659,67 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     bool pin_ok = g_register != 0;
     double pin_ms = 0;
     ln.unpin();
+    // Caller pages pinned for direct DMA, per span (pk, sig, msg, kind): the
+    // whole pages inside part 0's bytes, then at part 1 every whole page
+    // inside the rest of the chunk's span, in one range (registering costs
+    // ~2 us a range and unregistering ~4.5 us: a 2.56M call used to unpin 63
+    // per-part ranges in 0.28 ms, and stage a sub-page tail per part and
+    // span).  Only pages wholly inside the caller's span are registered, so
+    // a neighbouring buffer's registration never collides; the bytes outside
+    // the registered pages (part 0's head and tail, the chunk's last tail)
+    // go through the lane's pinned staging, and so does a span whose range
+    // cannot be registered (read-only, already registered), for the rest of
+    // the chunk.
+    constexpr uintptr_t kPage = 4096;
+    struct Reg {
+      uintptr_t lo = 0, mid = 0, hi = 0;  // registered [lo, mid) and [mid, hi) (mid == hi: one range)
+      bool failed = false;
+    } reg[4];
+    const uintptr_t span_end[4] = {(uintptr_t)(pk + 32ull * (lo + n)), (uintptr_t)(sig + 64ull * (lo + n)),
+                                   mbytes ? (uintptr_t)(msg + msg_off[lo + n]) : 0,
+                                   mixed_stream ? (uintptr_t)(kind + lo + n) : 0};
     const PartFeeder feed = [&](uint32_t a, uint32_t b, hipEvent_t *ready) -> int {
       for (uint32_t i = a; i <= b; i++) off[i] = msg_off[lo + i] - base;
       const size_t m0 = off[a], m1 = off[b];
-      // per span: [dst offset, caller bytes, length]; then the pinned middle
+      // per span: [dst offset, caller bytes, length]; [d0, d1) of it is
+      // DMA'd from registered pages, the rest staged
       struct Span {
         size_t at;
         const uint8_t *src;
         size_t len;
-        size_t d0, d1;  // [d0, d1): DMA'd from the caller's pinned pages
+        size_t d0, d1;
       } sp[4] = {{L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a), 0, 0},
                  {L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a), 0, 0},
                  {L.msg + m0, msg + base + m0, m1 - m0, 0, 0},
                  {kind_at + a, mixed_stream ? kind + lo + a : nullptr, mixed_stream ? (size_t)(b - a) : 0, 0, 0}};
-      constexpr uintptr_t kPage = 4096;
       const auto t0 = std::chrono::steady_clock::now();
-      for (Span &x : sp) {
-        if (!pin_ok || x.len < 4 * kPage) continue;
-        // pages [floor(start), floor(end)) -- part 0 from ceil(start), so no
-        // page outside the caller's span is pinned; consecutive parts' page
-        // ranges are disjoint
+      for (int k = 0; k < 4; k++) {
+        Span &x = sp[k];
+        Reg &r = reg[k];
+        if (!pin_ok || r.failed || x.len < 4 * kPage) continue;
         const uintptr_t s0 = (uintptr_t)x.src, s1 = s0 + x.len;
-        const uintptr_t r0 = a == 0 ? (s0 + kPage - 1) & ~(kPage - 1) : s0 & ~(kPage - 1);
-        const uintptr_t r1 = s1 & ~(kPage - 1);
-        if (r1 <= r0 + kPage) continue;
-        if (hipHostRegister(reinterpret_cast<void *>(r0), r1 - r0, hipHostRegisterDefault) != hipSuccess) {
-          (void)hipGetLastError();
-          pin_ok = false;  // stage the rest of the chunk
-          continue;
+        if (s1 > r.hi && (r.hi == 0 || r.hi < (span_end[k] & ~(kPage - 1)))) {
+          const uintptr_t r0 = r.hi ? r.hi : (s0 + kPage - 1) & ~(kPage - 1);
+          const uintptr_t r1 = (r.hi ? span_end[k] : s1) & ~(kPage - 1);
+          if (r1 >= r0 + kPage) {
+            if (hipHostRegister(reinterpret_cast<void *>(r0), r1 - r0, hipHostRegisterDefault) != hipSuccess) {
+              (void)hipGetLastError();
+              r.failed = true;  // stage this span for the rest of the chunk
+              continue;
+            }
+            ln.pinned.push_back(reinterpret_cast<void *>(r0));
+            if (!r.hi) r.lo = r0;
+            r.mid = r.hi ? r.hi : r1;
+            r.hi = r1;
+          }
         }
-        ln.pinned.push_back(reinterpret_cast<void *>(r0));
-        x.d0 = std::max(s0, r0) - s0;
-        x.d1 = r1 - s0;
+        if (r.hi) {
+          const uintptr_t c0 = std::max(s0, r.lo), c1 = std::min(s1, r.hi);
+          if (c1 > c0) {
+            x.d0 = c0 - s0;
+            x.d1 = c1 - s0;
+          }
+        }
       }
       pin_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       CopySpan cs[8];
@@ -1713,10 +1752,17 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
         return true;
       };
       if (!h2d(L.off + 4ull * a, h + L.off + 4ull * a, 4ull * (b - a + 1))) return TMV_ERR_LAUNCH;
-      for (const Span &x : sp) {
-        const bool ok = x.d1 == 0 ? h2d(x.at, h + x.at, x.len)
-                                  : h2d(x.at, h + x.at, x.d0) && h2d(x.at + x.d0, x.src + x.d0, x.d1 - x.d0) &&
-                                        h2d(x.at + x.d1, h + x.at + x.d1, x.len - x.d1);
+      for (int k = 0; k < 4; k++) {
+        const Span &x = sp[k];
+        bool ok;
+        if (x.d1 == 0) {
+          ok = h2d(x.at, h + x.at, x.len);
+        } else {  // staged head, the registered middle (one DMA per registered range), staged tail
+          const uintptr_t s0 = (uintptr_t)x.src, mid = reg[k].mid;
+          const size_t cut = mid > s0 + x.d0 && mid < s0 + x.d1 ? mid - s0 : x.d1;
+          ok = h2d(x.at, h + x.at, x.d0) && h2d(x.at + x.d0, x.src + x.d0, cut - x.d0) &&
+               h2d(x.at + cut, x.src + cut, x.d1 - cut) && h2d(x.at + x.d1, h + x.at + x.d1, x.len - x.d1);
+        }
         if (!ok) return TMV_ERR_LAUNCH;
       }
       if ((ce = hipEventRecord(ev, ln.copy)) != hipSuccess) {
@@ -1736,18 +1782,23 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
             : batch_check(d, o, sr, dd + L.pk, dd + L.sig, dd + L.msg, reinterpret_cast<const uint32_t *>(dd + L.off), n,
                           static_cast<uint8_t *>(ln.d_out.ptr), ln.stream, &feed, g_stream_two ? ln.helper : nullptr,
                           g_stream_two ? ln.join : nullptr);
-    if (rc != 0) {  // parts already enqueued still use the lane's buffers: drain before returning
+    // an error after parts were enqueued: they still use the lane's buffers
+    // and the caller's registered pages, so drain before returning
+    auto drain = [&](int r) {
       const bool drained = wait_stream(d, ln.copy) == hipSuccess;
       if (ln.helper) (void)wait_stream(d, ln.helper);
       if (wait_stream(d, ln.stream) == hipSuccess && drained) ln.unpin();
       else ln.pinned.clear();  // copies may be in flight: leave the pages registered (see run_batch)
-      return rc;
-    }
+      return r;
+    };
+    if (rc != 0) return drain(rc);
     if (tm.on) fprintf(stderr, "[tmv_engine] pinning %9.3f ms (%zu ranges)\n", pin_ms, ln.pinned.size());
     tm.mark("parts staged + launched", n);
+    // statuses through the lane's staging (a late DMA after a device
+    // timeout must not land in caller memory the call no longer owns)
     if ((e = hipMemcpyAsync(ln.h_out.ptr, ln.d_out.ptr, n, hipMemcpyDeviceToHost, ln.stream)) != hipSuccess) {
       set_error("hipMemcpyAsync(D2H)", e);
-      return TMV_ERR_LAUNCH;
+      return drain(TMV_ERR_LAUNCH);
     }
     ctx->m_d2h += n;
     return 0;
@@ -1994,7 +2045,9 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
             r = wait_rc(e);
           }
         }
+        tm.mark("waited", ln.n);
         if (ok && r == 0) std::memcpy(out + ln.lo, ln.h_out.ptr, ln.n);
+        tm.mark("copied out", ln.n);
         // the chunk's copies are done (its stream waited on every part's copy);
         // if they may not be (a failed or skipped wait), the caller's pages
         // stay registered and only the records are dropped: unregistering
@@ -2002,6 +2055,7 @@ static int run_batch(tmv_ctx *ctx, Scheme sch, const uint8_t *kind, const uint8_
         // memory, would be worse (include/tmverify.h, TMV_ERR_TIMEOUT)
         if (r == 0 && (ok || !d.faulted)) ln.unpin();
         else leak_pins(d.id, ln);  // released once its streams drain (release_leaked_pins)
+        tm.mark("unpinned", ln.n);
         std::lock_guard<std::mutex> lk(d.mu);
         if (ok && r == 0 && ctx->stats) collect_stats(ctx, d, ln.stream);
         ln.n = 0;

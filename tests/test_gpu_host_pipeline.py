@@ -126,6 +126,25 @@ assert np.array_equal(st.astype(np.uint8), want)
 payload = hb.pk.nbytes + hb.sig.nbytes + hb.msg.nbytes + hb.off.nbytes
 h2d = ctx.metrics()["h2d_bytes"]
 assert payload <= h2d <= payload + 4 * 64, (h2d, payload)
+# two calls at once on the same caller buffers (each claims its own lanes):
+# the second one's registrations of the same pages fail, so it stages them
+from concurrent.futures import ThreadPoolExecutor
+with ThreadPoolExecutor(2) as ex:
+    res = list(ex.map(lambda _: ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, hb.pk, hb.sig,
+                                                    hb.msg, hb.off)[1], range(2)))
+for st in res:
+    assert np.array_equal(st.astype(np.uint8), want)
+# read-only mappings of the caller's inputs (a file mapped PROT_READ)
+import tempfile, os
+with tempfile.TemporaryDirectory() as td:
+    ro = []
+    for name, a in (("pk", hb.pk), ("sig", hb.sig), ("msg", hb.msg)):
+        path = os.path.join(td, name)
+        a.tofile(path)
+        ro.append(np.memmap(path, dtype=a.dtype, mode="r", shape=a.shape))
+    ok, st = ctx.verify_batch_ex(N.TMV_KIND_ED25519, N.TMV_FLAG_BATCH_EQUATION, ro[0], ro[1], ro[2], hb.off)
+    assert np.array_equal(st.astype(np.uint8), want)
+    del ro
 print("ok")
 """
 
@@ -134,9 +153,10 @@ def test_streamed_c2_host_batches():
     """The driver-sized host batch (BASELINE C2 tiled to 200k and 40k entries)
     streamed with the default parts: the vector equals the committed C2
     bitmap repeated, twice in a row on the same lane, with the caller's pages
-    pinned part by part -- misaligned buffers (the bytes around the pinned
-    pages staged) and an already-pinned buffer (its registration fails, so it
-    is staged) included."""
+    pinned -- misaligned buffers (the bytes around the pinned pages staged),
+    an already-pinned buffer (its registration fails, so it is staged), two
+    calls at once on the same buffers and read-only file mappings included;
+    the statuses come back into the caller's pinned pages."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", BIG], cwd=root, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
