@@ -47,7 +47,6 @@
 namespace tmv {
 
 constexpr uint32_t kMsmWideRows = 65536;     // (group, window) rows from which k_msm_wpart runs one lane per window
-constexpr uint32_t kLocParts = 4;            // running-sum lanes per window of the located pass (few live groups)
 constexpr int kMsmChunkMax = 32;             // sorted entries per accumulation lane: 16 or 32
 constexpr uint32_t kMsmEmpty = 0xffffffffu;  // padding entry / no bucket
 constexpr int kMsmSortBlock = 256;
@@ -117,13 +116,15 @@ struct MsmParams {
   // profiles/r03/ab_join_compact.txt.)
   TMV_HD uint32_t bucket(uint32_t w, uint32_t i) const { return w * H + i; }
   TMV_HD uint32_t chunks_per_group() const { return cap / L; }
-  // running-sum lanes per window of the located fallback's second MSM: its
-  // grid covers every group but only the failing ones (~10-25%) are live, so
-  // the chain, not the work, sets its time -- 2 H / P + 3 P + log2(H / P)
-  // additions instead of 2 H (c = 6: 31 instead of 64)
-  TMV_HD uint32_t loc_parts() const { return merged ? P : (H >= kLocParts ? (P > kLocParts ? P : kLocParts) : P); }
-  // window-part slots the workspace holds per (group, window)
-  TMV_HD uint32_t wpart_slots() const { return loc_parts() > P ? loc_parts() : P; }
+  // window-part slots the workspace holds per (group, window).  The located
+  // fallback's second MSM runs its running sums with the launch's own P
+  // (one lane per window at the located sizes): round 5's 4 lanes per window
+  // shortened the chain but cost 2.75x the additions plus the k_msm_wsum
+  // join, and a 2.56M launch's 3,744 failing groups are throughput work --
+  // C2 bench +1.3% (4 of 4 same-box pairs), 2.56M alone 19.53 / 19.74 ->
+  // 19.27 / 19.30 ms, 500k and 1M equal or better
+  // (profiles/r06/ab_loc_parts_bench.txt)
+  TMV_HD uint32_t wpart_slots() const { return P; }
 
   static MsmParams make(uint32_t n, uint32_t m_log2, uint32_t c, bool merged = false) {
     MsmParams p;

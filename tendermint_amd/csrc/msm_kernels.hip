@@ -15,7 +15,6 @@
 #include "ktimer.h"
 #include "verify_kernels.h"
 #include "halfscalar.h"
-#include "knobs.h"
 
 #include <atomic>
 #include <mutex>
@@ -1369,16 +1368,9 @@ static hipError_t launch_tail(const uint8_t *sig, const uint32_t *idx, const uin
         hipSuccess)
       return e;
     const uint32_t n_slots = p.groups << p.m_log2;
-    MsmParams pl = p;  // running sums split over loc_parts() lanes per window (few live slots: the chain sets the time)
-    pl.P = p.loc_parts();
-    static const uint32_t lp_ab = [] {  // A/B (knobs.h): TMV_LOC_PARTS, a power of two <= loc_parts()
-      const char *v = ab_knob("TMV_LOC_PARTS");
-      return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
-    }();
-    if (lp_ab && lp_ab <= pl.P && !(lp_ab & (lp_ab - 1))) pl.P = lp_ab;
-    if ((e = launch_buckets(mw.loc_count, n_slots, mw, pl, stream, false)) != hipSuccess) return e;
+    if ((e = launch_buckets(mw.loc_count, n_slots, mw, p, stream, false)) != hipSuccess) return e;
     hipLaunchKernelGGL((k_msm_horner<SR, false, true>), dim3((p.groups + 15) / 16), dim3(64), 0, stream,
-                       mw.loc_count, n_slots, mw, pl, nullptr, 0u);
+                       mw.loc_count, n_slots, mw, p, nullptr, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_loc_search<SR>, dim3(p.groups), dim3(64), 0, stream, count_ptr, n, mw, p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
