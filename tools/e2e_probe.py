@@ -37,6 +37,19 @@ def main():
         hb = Batch.concat([one] * (NBC // NB))
         pk, sig, msg, off = hb.pk, hb.sig, hb.msg, hb.off
     from tendermint_amd import _native as N
+    # TMV_E2E_TORCH_STREAMS=K: K torch streams, each used once, before the
+    # engine's lanes create theirs (bench.py's order: its in-flight streams
+    # first) -- do they share the device's hardware queues with the lanes?
+    ks = int(os.environ.get("TMV_E2E_TORCH_STREAMS", "0"))
+    keep = []
+    if ks:
+        import torch
+        for _ in range(ks):
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                keep.append(torch.ones(1024, device="cuda") * 2)
+            keep.append(st)
+        torch.cuda.synchronize()
     ctx = N.Context(1)
     flags = N.TMV_FLAG_BATCH_EQUATION
     n = len(off) - 1

@@ -44,6 +44,13 @@ def main():
     import torch
     from tendermint_amd import _native as N
     dev = torch.device("cuda", 0)
+    keep = []
+    for _ in range(int(os.environ.get("TMV_E2E_TORCH_STREAMS", "0"))):  # see tools/e2e_probe.py
+        st = torch.cuda.Stream(dev)
+        with torch.cuda.stream(st):
+            keep.append(torch.ones(1024, device=dev) * 2)
+        keep.append(st)
+    torch.cuda.synchronize(dev)
     ctx = N.Context(1)
     if a.group_log2 or a.window_bits:
         ctx.set_batch_options(group_log2=a.group_log2, window_bits=a.window_bits)
