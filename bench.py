@@ -831,7 +831,8 @@ def main():
         the exact full vector, which must equal want_full.  Kernel only:
         inputs resident in HBM, the gathered vector left on the device; end
         to end: the shard from host buffers through the host C-ABI, the
-        gathered vector copied back to the host.  Wall time per repetition =
+        gathered vector copied back to the host (one rank: the call's own
+        host vector, nothing to gather).  Wall time per repetition =
         the max over ranks (barrier + device syncs around it)."""
         counts = [b - a for a, b in (shard_range(n_total, world, r) for r in range(world))]
         lo, hi = shard_range(n_total, world, rank)
@@ -872,8 +873,11 @@ def main():
                 v = ctx.verify_batch_ex(key_kind_s, flags_s, local.pk, local.sig, local.msg, local.off)[1]
             else:
                 v = ctx.verify_mixed_batch_ex(flags_s, kind_local, local.pk, local.sig, local.msg, local.off)[1]
+            v = np.asarray(v, np.int8)
+            if world == 1:  # the call already returned the whole vector on the host: nothing to gather
+                return torch.from_numpy(v if statuses else (v == 1).astype(np.uint8))
             with stream_ctx(st):
-                return full(tdev(np.asarray(v, np.int8))).cpu()
+                return full(tdev(v)).cpu()
 
         k_t, g = timed_reps(kernel_only, args.strong_reps)
         assert torch.equal(g, want_dev), "strong scaling: gathered vector differs from the known one (kernel path)"
