@@ -33,6 +33,7 @@
 #include "merlin_dev.h"
 #include "host/pool.h"
 #include "host/shard_plan.h"
+#include "host/stream_plan.h"
 #include "host/shard_run.h"
 #include "host/wait.h"
 #include "knobs.h"
@@ -1105,14 +1106,7 @@ using PartFeeder = std::function<int(uint32_t e0, uint32_t e1, hipEvent_t *ready
 // Part boundaries of a streamed launch of n entries: whole groups, the first
 // part g_stream_first entries, then g_stream_part each.
 static std::vector<uint32_t> stream_parts(uint32_t n, uint32_t m) {
-  std::vector<uint32_t> b{0};
-  uint32_t want = g_stream_first;
-  while (b.back() < n) {
-    const uint64_t e1 = std::min<uint64_t>(n, ((uint64_t)b.back() + want + m - 1) / m * m);
-    b.push_back((uint32_t)e1);
-    want = g_stream_ramp ? std::min<uint32_t>(g_stream_part, 2 * want) : g_stream_part;
-  }
-  return b;
+  return tmh::stream_part_bounds(n, m, g_stream_first, g_stream_part, g_stream_ramp != 0);
 }
 
 // feed: streamed launch, parts alternating between s and s2 (if given,
@@ -1190,12 +1184,8 @@ static int mixed_check_streamed(Device &d, const LaunchOpts &o_in, const uint8_t
   uint32_t *ib = static_cast<uint32_t *>(ws->idx.ptr);
   uint32_t *counts = ib, *idx_ed = ib + 16, *idx_sr = ib + 16 + n, *cursor = ib + 16 + 2ull * n;
   // parts: the one-kind schedule (a short first part), at most kMaxStreamParts
-  uint32_t part_len = g_stream_part;
-  while ((n - std::min(n, g_stream_first) + part_len - 1) / part_len + 1 + (g_stream_ramp ? 32 : 0) > kMaxStreamParts)
-    part_len *= 2;
-  std::vector<uint32_t> b{0};
-  for (uint32_t want = g_stream_first; b.back() < n; want = g_stream_ramp ? std::min(part_len, 2 * want) : part_len)
-    b.push_back(std::min<uint64_t>(n, (uint64_t)b.back() + want));
+  const std::vector<uint32_t> b =
+      tmh::mixed_part_bounds(n, g_stream_first, g_stream_part, g_stream_ramp != 0, kMaxStreamParts);
   const size_t parts = b.size() - 1;
   hipError_t e;
   if ((e = hipMemsetAsync(ib, 0, 64, s)) != hipSuccess ||
@@ -1671,10 +1661,7 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
     // cannot be registered (read-only, already registered), for the rest of
     // the chunk.
     constexpr uintptr_t kPage = 4096;
-    struct Reg {
-      uintptr_t lo = 0, mid = 0, hi = 0;  // registered [lo, mid) and [mid, hi) (mid == hi: one range)
-      bool failed = false;
-    } reg[4];
+    tmh::SpanPins reg[4];  // host/stream_plan.h
     const uintptr_t span_end[4] = {(uintptr_t)(pk + 32ull * (lo + n)), (uintptr_t)(sig + 64ull * (lo + n)),
                                    mbytes ? (uintptr_t)(msg + msg_off[lo + n]) : 0,
                                    mixed_stream ? (uintptr_t)(kind + lo + n) : 0};
@@ -1687,39 +1674,28 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
         size_t at;
         const uint8_t *src;
         size_t len;
-        size_t d0, d1;
-      } sp[4] = {{L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a), 0, 0},
-                 {L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a), 0, 0},
-                 {L.msg + m0, msg + base + m0, m1 - m0, 0, 0},
-                 {kind_at + a, mixed_stream ? kind + lo + a : nullptr, mixed_stream ? (size_t)(b - a) : 0, 0, 0}};
+        size_t d0, d1, cut;
+      } sp[4] = {{L.pk + 32ull * a, pk + 32ull * (lo + a), 32ull * (b - a), 0, 0, 0},
+                 {L.sig + 64ull * a, sig + 64ull * (lo + a), 64ull * (b - a), 0, 0, 0},
+                 {L.msg + m0, msg + base + m0, m1 - m0, 0, 0, 0},
+                 {kind_at + a, mixed_stream ? kind + lo + a : nullptr, mixed_stream ? (size_t)(b - a) : 0, 0, 0, 0}};
       const auto t0 = std::chrono::steady_clock::now();
       for (int k = 0; k < 4; k++) {
         Span &x = sp[k];
-        Reg &r = reg[k];
+        tmh::SpanPins &r = reg[k];
         if (!pin_ok || r.failed || x.len < 4 * kPage) continue;
         const uintptr_t s0 = (uintptr_t)x.src, s1 = s0 + x.len;
-        if (s1 > r.hi && (r.hi == 0 || r.hi < (span_end[k] & ~(kPage - 1)))) {
-          const uintptr_t r0 = r.hi ? r.hi : (s0 + kPage - 1) & ~(kPage - 1);
-          const uintptr_t r1 = (r.hi ? span_end[k] : s1) & ~(kPage - 1);
-          if (r1 >= r0 + kPage) {
-            if (hipHostRegister(reinterpret_cast<void *>(r0), r1 - r0, hipHostRegisterDefault) != hipSuccess) {
-              (void)hipGetLastError();
-              r.failed = true;  // stage this span for the rest of the chunk
-              continue;
-            }
-            ln.pinned.push_back(reinterpret_cast<void *>(r0));
-            if (!r.hi) r.lo = r0;
-            r.mid = r.hi ? r.hi : r1;
-            r.hi = r1;
+        uintptr_t r0, r1;
+        if (tmh::next_pin_range(r, s0, s1, span_end[k], kPage, &r0, &r1)) {
+          if (hipHostRegister(reinterpret_cast<void *>(r0), r1 - r0, hipHostRegisterDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            r.failed = true;  // stage this span for the rest of the chunk
+            continue;
           }
+          ln.pinned.push_back(reinterpret_cast<void *>(r0));
+          tmh::commit_pin_range(r, r0, r1);
         }
-        if (r.hi) {
-          const uintptr_t c0 = std::max(s0, r.lo), c1 = std::min(s1, r.hi);
-          if (c1 > c0) {
-            x.d0 = c0 - s0;
-            x.d1 = c1 - s0;
-          }
-        }
+        tmh::direct_piece(r, s0, s1, &x.d0, &x.d1, &x.cut);
       }
       pin_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       CopySpan cs[8];
@@ -1757,9 +1733,8 @@ static int stage_and_launch(tmv_ctx *ctx, uint32_t flags, Device &d, HostLane &l
         bool ok;
         if (x.d1 == 0) {
           ok = h2d(x.at, h + x.at, x.len);
-        } else {  // staged head, the registered middle (one DMA per registered range), staged tail
-          const uintptr_t s0 = (uintptr_t)x.src, mid = reg[k].mid;
-          const size_t cut = mid > s0 + x.d0 && mid < s0 + x.d1 ? mid - s0 : x.d1;
+        } else {  // staged head, the locked middle (one DMA per locked range), staged tail
+          const size_t cut = x.cut;
           ok = h2d(x.at, h + x.at, x.d0) && h2d(x.at + x.d0, x.src + x.d0, cut - x.d0) &&
                h2d(x.at + cut, x.src + cut, x.d1 - cut) && h2d(x.at + x.d1, h + x.at + x.d1, x.len - x.d1);
         }

@@ -21,6 +21,7 @@
 #include "../../include/tmverify.h"
 #include "../../tendermint_amd/csrc/host/tm_light.h"
 #include "../../tendermint_amd/csrc/host/shard_plan.h"
+#include "../../tendermint_amd/csrc/host/stream_plan.h"
 #include "../../tendermint_amd/csrc/host/shard_run.h"
 #include "../../tendermint_amd/csrc/host/wait.h"
 #include "../../tendermint_amd/csrc/host/tm_types.h"
@@ -339,4 +340,56 @@ extern "C" uint32_t commitcheck_shard_plan(uint32_t n, uint32_t ndev, uint32_t h
       w++;
     }
   return w;
+}
+
+// The runtime's streamed part schedules (host/stream_plan.h): boundaries of
+// a one-kind launch (group-aligned) or of a mixed chunk (kind = 1).
+// Returns the number of boundaries written (or needed, if cap is short).
+extern "C" uint32_t commitcheck_stream_parts(uint32_t n, uint32_t m, uint32_t first, uint32_t part, int ramp, int mixed,
+                                             uint32_t max_parts, uint32_t *out, uint32_t cap) {
+  const std::vector<uint32_t> b = mixed ? tmh::mixed_part_bounds(n, first, part, ramp != 0, max_parts)
+                                        : tmh::stream_part_bounds(n, m, first, part, ramp != 0);
+  for (size_t i = 0; i < b.size() && i < cap; i++) out[i] = b[i];
+  return (uint32_t)b.size();
+}
+
+// The runtime's caller-page locking over one span split into parts
+// (host/stream_plan.h, stage_and_launch's feed): span [base, base + len) in
+// parts of the given lengths, page size `page`, the lock attempt number
+// `fail_at` (0-based, < 0: none) failing.  Per part: [d0, d1, cut]; then the
+// locked ranges [r0, r1) in order.  Returns the number of locked ranges
+// (out: 3 x parts words, then 2 x ranges words, at most 8 ranges).
+extern "C" uint32_t commitcheck_pin_walk(uint64_t base, const uint64_t *part_len, uint32_t parts, uint64_t page,
+                                         int fail_at, uint64_t min_len, uint64_t *out) {
+  tmh::SpanPins r;
+  uint64_t end = base;
+  for (uint32_t i = 0; i < parts; i++) end += part_len[i];
+  uint64_t s0 = base;
+  uint32_t ranges = 0;
+  int attempts = 0;
+  for (uint32_t i = 0; i < parts; i++) {
+    const uint64_t s1 = s0 + part_len[i];
+    size_t d0 = 0, d1 = 0, cut = 0;
+    if (!r.failed && part_len[i] >= min_len) {
+      uintptr_t r0, r1;
+      bool ok = true;
+      if (tmh::next_pin_range(r, s0, s1, end, page, &r0, &r1)) {
+        if (attempts++ == fail_at) {
+          r.failed = true;
+          ok = false;
+        } else {
+          tmh::commit_pin_range(r, r0, r1);
+          out[3ull * parts + 2 * ranges] = r0;
+          out[3ull * parts + 2 * ranges + 1] = r1;
+          ranges++;
+        }
+      }
+      if (ok) tmh::direct_piece(r, s0, s1, &d0, &d1, &cut);
+    }
+    out[3 * i] = d0;
+    out[3 * i + 1] = d1;
+    out[3 * i + 2] = cut;
+    s0 = s1;
+  }
+  return ranges;
 }
